@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""bench.py -- streaming connected components on RMAT-26 (BASELINE.json metric).
+
+One step = one full pass of the hot path over the whole synthetic stream:
+reset the summary, fold every 2^20-edge micro-batch (SummaryBulkAggregation window
+-> UpdateCC.foldEdges -> DisjointSet.union), combine across ranks after every
+global micro-batch (N > 1), then the final canonical label pass (every vertex ->
+min id of its component, written to HBM). Edges are generated into HBM before the
+timed region (each rank its own contiguous 1/N shard of the 2^30-edge stream).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--scale 26] [--log-batch 20]
+N > 1 is launched by torch.distributed.run (one process per GPU, RCCL).
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+BYTES_PER_EDGE_SPARSE = 48   # 16 B edge + 2 x 12 B relabel probe + 2 x 4 B parent read
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--scale", type=int, default=26)
+    p.add_argument("--edge-factor", type=int, default=16)
+    p.add_argument("--log-batch", type=int, default=20)
+    p.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED0026)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample-log2", type=int, default=24)
+    p.add_argument("--no-profile-pass", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import gsamd as gs
+    from gelly_streaming_amd.distributed import DeltaExchangeFold
+
+    E = (1 << args.scale) * args.edge_factor
+    B = 1 << args.log_batch
+    per = E // world
+    start = rank * per
+    nbatch = (per + B - 1) // B
+
+    summ = gs.Summary("cc", device=local, capacity_hint=1 << args.scale)
+    st = summ.stream
+    gs_stream = torch.cuda.ExternalStream(st, device=dev)
+    src = torch.empty(per, dtype=torch.int64, device=dev)
+    dst = torch.empty(per, dtype=torch.int64, device=dev)
+    gs.gen_rmat(src, dst, start, per, args.scale, args.seed, True, stream=st)
+    summ.sync()
+    # final label pass output (device): at most min(2^scale, 2E) vertices
+    vcap = min(1 << args.scale, 2 * E) + 16
+    out_v = torch.empty(vcap, dtype=torch.int64, device=dev)
+    out_l = torch.empty(vcap, dtype=torch.int64, device=dev)
+    xch = DeltaExchangeFold(summ, 3 * B, dev) if world > 1 else None
+
+    nlabels = [0]
+
+    def one_step():
+        summ.reset()
+        if xch is not None:
+            summ.set_delta_tracking(True)
+        for b in range(nbatch):
+            o = b * B
+            n = min(B, per - o)
+            if xch is None:
+                summ.fold_device(src[o:], dst[o:], n=n)
+            else:
+                xch.step(src[o:], dst[o:], n)
+        nlabels[0] = summ.export_labels_device(out_v, out_l)  # canonical label pass (syncs)
+
+    def barrier():
+        summ.sync()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        one_step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_edges = E * args.steps
+    value = total_edges / elapsed
+
+    # Roofline of the dominant kernel (k_fold): HIP events around every launch on
+    # the summary's own stream, over one extra full step (same work as a timed step).
+    roof = None
+    fold_avg_ms = None
+    if not args.no_profile_pass:
+        summ.set_profiling(True)
+        one_step()
+        summ.sync()
+        nf, fold_ms = summ.kernel_stats("fold")
+        nh, hook_ms = summ.kernel_stats("hook")
+        ne, exp_ms = summ.kernel_stats("export")
+        summ.set_profiling(False)
+        fold_avg_ms = fold_ms / max(nf, 1)
+        edges_per_launch = per / max(nf, 1) if world == 1 else B  # own-shard launches dominate
+        achieved = BYTES_PER_EDGE_SPARSE * edges_per_launch / (fold_avg_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_fold_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                pm = json.load(f)
+            if pm.get("workload") == "rmat%d-cc-stream" % args.scale and pm.get("batch") == B:
+                traffic = pm.get("hbm_bytes_per_launch")
+        roof = {"kernel": "k_fold", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "bytes_per_edge": BYTES_PER_EDGE_SPARSE, "edges_per_launch": int(edges_per_launch),
+                "fold_avg_us": round(fold_avg_ms * 1e3, 2), "fold_launches": int(nf),
+                "hook_avg_us": round(hook_ms * 1e3 / max(nh, 1), 2), "hook_launches": int(nh),
+                "export_ms": round(exp_ms, 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle  # CPU baseline leg only
+        m = 1 << args.cpu_sample_log2
+        hs = src[:m].cpu().numpy()
+        hd = dst[:m].cpu().numpy()
+        secs = oracle.cpu_baseline_cc(hs, hd, B, threads=1)
+        cpu = {"value": round(m / secs, 1), "unit": "edges/s", "cores": 1, "kind": "port",
+               "sample": "first 2^%d edges of the same RMAT-%d stream, %d-edge windows, C++ restatement of "
+                         "DisjointSet.union + CombineCC/Merger per window (oracle/gs_oracle.cpp), 1 thread, %.1f s"
+                         % (args.cpu_sample_log2, args.scale, B, secs)}
+
+    if rank == 0:
+        line = {
+            "metric": "edges/sec (whole node) for streaming CC on RMAT-%d" % args.scale,
+            "value": round(value, 1),
+            "unit": "edges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic",
+            "config": {"workload": "rmat%d-cc-stream" % args.scale, "scale": args.scale,
+                       "edges": E, "micro_batch": B, "ids": "sparse 64-bit (scrambled)",
+                       "vertices_labelled": int(nlabels[0]),
+                       "parallelism": "edge-shard x%d, per-batch delta all-gather" % world},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    summ.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,280 @@
+"""gelly-streaming_amd -- MI355X-native summary aggregation for gelly-streaming.
+
+Python binding (ctypes) of the C ABI in include/gs_summary.h / include/gs_gen.h.
+The compute path is lib/libgs_summary.so (hand-written HIP for gfx950); there is
+no CPU fallback: constructing a Summary without the library or without a GPU
+raises.
+
+The directory name is not a Python identifier; import it through the root-level
+shim `gsamd` (``import gsamd``), which loads this package as
+``gelly_streaming_amd``.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgs_summary.so")
+
+KIND_CC = 0
+KIND_SIGNED = 1
+
+GS_OK = 0
+GS_ERR_INVALID = -1
+GS_ERR_HIP = -2
+GS_ERR_CAPACITY = -3
+GS_ERR_TRUNCATED = -4
+
+KERNEL_IDS = {"fold": 0, "hook": 1, "export": 2, "init": 3}
+
+# Every symbol include/gs_summary.h and include/gs_gen.h declare.
+EXPORTED_SYMBOLS = (
+    "gs_last_error", "gs_version", "gs_create", "gs_destroy", "gs_reset", "gs_fold", "gs_fold_device",
+    "gs_combine", "gs_sync", "gs_num_vertices", "gs_find", "gs_export_labels", "gs_export_labels_device",
+    "gs_bip_status", "gs_export_colouring", "gs_serialize", "gs_deserialize", "gs_set_delta_tracking",
+    "gs_take_delta_device", "gs_get_stream", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity",
+    "gs_gen_rmat", "gs_gen_er", "gs_gen_bip",
+)
+
+
+class GSError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("gs error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_u64 = ctypes.c_uint64
+_i64 = ctypes.c_int64
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", _HERE, "-j4"])
+
+
+def lib():
+    """Load the HIP library (raises if it was not built: no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libgs_summary.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    L.gs_last_error.restype = ctypes.c_char_p
+    L.gs_create.argtypes = [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int, _u64]
+    L.gs_destroy.argtypes = [_vp]
+    L.gs_reset.argtypes = [_vp]
+    L.gs_fold.argtypes = [_vp, _vp, _vp, _sz]
+    L.gs_fold_device.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz]
+    L.gs_combine.argtypes = [_vp, _vp]
+    L.gs_sync.argtypes = [_vp]
+    L.gs_num_vertices.argtypes = [_vp, ctypes.POINTER(_u64)]
+    L.gs_find.argtypes = [_vp, _i64, ctypes.POINTER(_i64), ctypes.POINTER(ctypes.c_int)]
+    L.gs_export_labels.argtypes = [_vp, _vp, _vp, _sz, ctypes.POINTER(_sz)]
+    L.gs_export_labels_device.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.POINTER(_sz)]
+    L.gs_bip_status.argtypes = [_vp, ctypes.POINTER(ctypes.c_int)]
+    L.gs_export_colouring.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.POINTER(_sz)]
+    L.gs_serialize.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
+    L.gs_deserialize.argtypes = [_vp, _vp, _sz]
+    L.gs_set_delta_tracking.argtypes = [_vp, ctypes.c_int]
+    L.gs_take_delta_device.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.POINTER(_sz)]
+    L.gs_get_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
+    L.gs_set_profiling.argtypes = [_vp, ctypes.c_int]
+    L.gs_kernel_stats.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double)]
+    L.gs_table_capacity.argtypes = [_vp, ctypes.POINTER(_u64)]
+    L.gs_gen_rmat.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, ctypes.c_int]
+    L.gs_gen_er.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, ctypes.c_int]
+    L.gs_gen_bip.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, _vp, _sz]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != GS_OK:
+        raise GSError(rc, lib().gs_last_error().decode())
+    return rc
+
+
+def _ptr(x):
+    """Device/host address of a torch tensor, numpy array, int or None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        assert x.flags["C_CONTIGUOUS"]
+        return x.ctypes.data
+    raise TypeError(type(x))
+
+
+class Summary:
+    """One GPU-resident summary (DisjointSet for kind 'cc', signed forest for
+    kind 'signed'). Thin owner of a gs_handle; see include/gs_summary.h."""
+
+    def __init__(self, kind="cc", device=0, capacity_hint=1 << 20):
+        self.kind = {"cc": KIND_CC, "signed": KIND_SIGNED}[kind] if isinstance(kind, str) else int(kind)
+        self.device = device
+        h = _vp()
+        _check(lib().gs_create(ctypes.byref(h), device, self.kind, capacity_hint))
+        self._h = h
+
+    # --- lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().gs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def reset(self):
+        _check(lib().gs_reset(self._h))
+
+    def sync(self):
+        _check(lib().gs_sync(self._h))
+
+    # --- fold / combine
+    def fold(self, src, dst):
+        """Fold host edges (int64 numpy arrays or sequences)."""
+        s = np.ascontiguousarray(np.asarray(src, dtype=np.int64))
+        d = np.ascontiguousarray(np.asarray(dst, dtype=np.int64))
+        assert s.shape == d.shape
+        _check(lib().gs_fold(self._h, s.ctypes.data, d.ctypes.data, len(s)))
+
+    def fold_device(self, src, dst, n=None, stride=1, w=None):
+        """Fold device-resident edges (torch tensors on this device or raw pointers)."""
+        if n is None:
+            n = src.numel() // (stride if stride > 1 else 1) if hasattr(src, "numel") else None
+        _check(lib().gs_fold_device(self._h, _ptr(src), _ptr(dst), _ptr(w), int(n), int(stride)))
+
+    def combine(self, other):
+        _check(lib().gs_combine(self._h, other._h))
+
+    # --- queries
+    def num_vertices(self):
+        n = _u64()
+        _check(lib().gs_num_vertices(self._h, ctypes.byref(n)))
+        return n.value
+
+    def find(self, v):
+        lab = _i64()
+        found = ctypes.c_int()
+        _check(lib().gs_find(self._h, int(v), ctypes.byref(lab), ctypes.byref(found)))
+        return lab.value if found.value else None
+
+    def labels(self):
+        """(vertex, canonical label) numpy arrays, sorted by vertex."""
+        n = self.num_vertices()
+        v = np.empty(n, np.int64)
+        lab = np.empty(n, np.int64)
+        got = _sz()
+        _check(lib().gs_export_labels(self._h, v.ctypes.data, lab.ctypes.data, n, ctypes.byref(got)))
+        o = np.argsort(v[: got.value], kind="stable")
+        return v[: got.value][o], lab[: got.value][o]
+
+    def export_labels_device(self, v, label, parity=None):
+        got = _sz()
+        cap = v.numel() if hasattr(v, "numel") else len(v)
+        _check(lib().gs_export_labels_device(self._h, _ptr(v), _ptr(label), _ptr(parity), cap, ctypes.byref(got)))
+        return got.value
+
+    def ok(self):
+        o = ctypes.c_int()
+        _check(lib().gs_bip_status(self._h, ctypes.byref(o)))
+        return bool(o.value)
+
+    def colouring(self):
+        """(ok, comp, v, sign) sorted by (comp, v); empty arrays when not bipartite."""
+        n = self.num_vertices()
+        comp = np.empty(max(n, 1), np.int64)
+        v = np.empty(max(n, 1), np.int64)
+        sign = np.empty(max(n, 1), np.uint8)
+        got = _sz()
+        _check(lib().gs_export_colouring(self._h, comp.ctypes.data, v.ctypes.data, sign.ctypes.data, max(n, 1),
+                                         ctypes.byref(got)))
+        k = got.value
+        comp, v, sign = comp[:k], v[:k], sign[:k]
+        o = np.lexsort((v, comp))
+        return self.ok(), comp[o], v[o], sign[o]
+
+    def serialize(self):
+        ln = _sz()
+        _check(lib().gs_serialize(self._h, None, 0, ctypes.byref(ln)))
+        buf = ctypes.create_string_buffer(ln.value)
+        _check(lib().gs_serialize(self._h, buf, ln.value, ctypes.byref(ln)))
+        return buf.raw[: ln.value]
+
+    def deserialize(self, data):
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        _check(lib().gs_deserialize(self._h, buf, len(data)))
+
+    # --- delta (multi-GPU exchange)
+    def set_delta_tracking(self, on=True):
+        _check(lib().gs_set_delta_tracking(self._h, 1 if on else 0))
+
+    def take_delta_device(self, a, b, w):
+        got = _sz()
+        cap = a.numel() if hasattr(a, "numel") else len(a)
+        _check(lib().gs_take_delta_device(self._h, _ptr(a), _ptr(b), _ptr(w), cap, ctypes.byref(got)))
+        return got.value
+
+    # --- introspection
+    @property
+    def stream(self):
+        s = _vp()
+        _check(lib().gs_get_stream(self._h, ctypes.byref(s)))
+        return s.value
+
+    def set_profiling(self, on=True):
+        _check(lib().gs_set_profiling(self._h, 1 if on else 0))
+
+    def kernel_stats(self, name):
+        n = _u64()
+        ms = ctypes.c_double()
+        _check(lib().gs_kernel_stats(self._h, KERNEL_IDS[name], ctypes.byref(n), ctypes.byref(ms)))
+        return n.value, ms.value
+
+    def table_capacity(self):
+        n = _u64()
+        _check(lib().gs_table_capacity(self._h, ctypes.byref(n)))
+        return n.value
+
+
+# ---------------------------------------------------------------- generators
+def gen_rmat(src, dst, start, count, scale, seed, scramble=True, stream=None):
+    rc = lib().gs_gen_rmat(stream, _ptr(src), _ptr(dst), start, count, scale, seed, 1 if scramble else 0)
+    if rc:
+        raise GSError(rc, "gs_gen_rmat failed")
+
+
+def gen_er(src, dst, start, count, logn, seed, scramble=True, stream=None):
+    rc = lib().gs_gen_er(stream, _ptr(src), _ptr(dst), start, count, logn, seed, 1 if scramble else 0)
+    if rc:
+        raise GSError(rc, "gs_gen_er failed")
+
+
+def gen_bip(src, dst, start, count, logside, seed, inject=(), stream=None):
+    inj = np.ascontiguousarray(np.sort(np.asarray(inject, dtype=np.uint64)))
+    rc = lib().gs_gen_bip(stream, _ptr(src), _ptr(dst), start, count, logside, seed,
+                          inj.ctypes.data if len(inj) else None, len(inj))
+    if rc:
+        raise GSError(rc, "gs_gen_bip failed")

@@ -1,0 +1,750 @@
+// gs_capi.cpp -- implementation of the C ABI in include/gs_summary.h.
+//
+// One handle = one GPU-resident summary: the slot table (relabel + forest), the
+// sharded counters, the active-edge lists, the optional delta lists, pinned
+// staging for host-pointer folds, and the handle's own HIP stream. All device
+// work is enqueued on that stream; the host only synchronises when it must return
+// data (counts, exports) or when the vertex table may need to grow.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gs_kernels.hpp"
+#include "gs_summary.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define GS_HIP(call)                                                                                  \
+  do {                                                                                                \
+    hipError_t e_ = (call);                                                                           \
+    if (e_ != hipSuccess)                                                                             \
+      return fail(GS_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));                     \
+  } while (0)
+
+constexpr uint32_t kMaxChunk = 1u << 22;     // edges per k_fold launch
+constexpr uint32_t kStageChunk = 1u << 20;   // edges per pinned staging buffer
+constexpr double kMaxLoad = 0.70;            // grow the table past this load factor
+constexpr uint64_t kMaxCap = 1ull << 30;     // link holds slot << 1 in 32 bits
+
+enum { KID_FOLD = 0, KID_HOOK = 1, KID_EXPORT = 2, KID_INIT = 3, KID_N = 4 };
+
+uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+struct gs_summary {
+  int device = 0;
+  int kind = GS_KIND_CC;
+  hipStream_t stream = nullptr;
+  // table
+  gs::Slot* tab = nullptr;
+  uint64_t cap = 0;
+  int logcap = 0;
+  uint32_t* ctr = nullptr;
+  uint64_t nv_ub = 0;  // host upper bound of the vertex count
+  // lists
+  uint2* act = nullptr;
+  uint32_t act_shard_cap = 0;
+  bool track = false;
+  int64_t* da = nullptr;
+  int64_t* db = nullptr;
+  uint8_t* dw = nullptr;
+  uint32_t delta_shard_cap = 0;
+  uint64_t delta_fill_ub = 0;  // worst-case per-shard fill since the last take
+  int actset = 0;
+  bool fused = false;
+  // staging for host folds
+  int64_t* d_stage = nullptr;  // [2][2][kStageChunk]
+  uint8_t* d_wstage = nullptr; // [2][kStageChunk]
+  int64_t* h_stage = nullptr;  // pinned, same shape
+  uint8_t* h_wstage = nullptr;
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  int stage_next = 0;
+  int64_t* d_scratch = nullptr;  // small scratch (find_one)
+  // profiling
+  bool profiling = false;
+  struct Pending {
+    int kid;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> ev_pool;
+  uint64_t launches[KID_N] = {0, 0, 0, 0};
+  double total_ms[KID_N] = {0, 0, 0, 0};
+
+  gs::Table table() const {
+    gs::Table t;
+    t.tab = tab;
+    t.ctr = ctr;
+    t.capidx = (uint32_t)cap;
+    t.mask = (uint32_t)(cap - 1);
+    t.shift = 64 - logcap;
+    return t;
+  }
+  gs::Lists lists() const {
+    gs::Lists L;
+    L.act = act;
+    L.act_shard_cap = act_shard_cap;
+    L.da = da;
+    L.db = db;
+    L.dw = dw;
+    L.delta_shard_cap = delta_shard_cap;
+    return L;
+  }
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+hipEvent_t take_event(gs_summary* h) {
+  if (!h->ev_pool.empty()) {
+    hipEvent_t e = h->ev_pool.back();
+    h->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// Bracket one launch with events when profiling.
+struct Prof {
+  gs_summary* h;
+  int kid;
+  hipEvent_t a = nullptr;
+  Prof(gs_summary* h_, int k) : h(h_), kid(k) {
+    if (h->profiling) {
+      a = take_event(h);
+      (void)hipEventRecord(a, h->stream);
+    }
+  }
+  ~Prof() {
+    if (h->profiling) {
+      hipEvent_t b = take_event(h);
+      (void)hipEventRecord(b, h->stream);
+      h->pending.push_back({kid, a, b});
+    }
+  }
+};
+
+void drain_profile(gs_summary* h) {
+  for (auto& p : h->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      h->launches[p.kid] += 1;
+      h->total_ms[p.kid] += ms;
+    }
+    h->ev_pool.push_back(p.a);
+    h->ev_pool.push_back(p.b);
+  }
+  h->pending.clear();
+}
+
+int check_device_flags(gs_summary* h) {
+  uint32_t flags[2] = {0, 0};
+  GS_HIP(hipMemcpyAsync(&flags[0], h->ctr + gs::ctr_index(gs::CTR_ERR), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipMemcpyAsync(&flags[1], h->ctr + gs::ctr_index(gs::CTR_OVF), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  if (flags[0]) return fail(GS_ERR_CAPACITY, "vertex table overflow (device probe limit)");
+  if (flags[1]) return fail(GS_ERR_CAPACITY, "delta/active list overflow: take the delta after each fold");
+  return GS_OK;
+}
+
+int read_nv(gs_summary* h, uint64_t* nv) {
+  std::vector<uint32_t> c(gs::CTR_COUNT * gs::kCtrStride);
+  GS_HIP(hipMemcpyAsync(c.data(), h->ctr, c.size() * 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  uint64_t s = 0;
+  for (int i = 0; i < gs::kShards; ++i) s += c[gs::ctr_index(gs::CTR_NV + i)];
+  *nv = s;
+  return GS_OK;
+}
+
+// keep_delta: a rebuild (grow) keeps the pending delta counters.
+int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
+  h->cap = cap;
+  h->logcap = 0;
+  while ((1ull << h->logcap) < cap) ++h->logcap;
+  GS_HIP(hipMalloc(&h->tab, (cap + 1) * sizeof(gs::Slot)));
+  if (keep_delta) {
+    GS_HIP(hipMemsetAsync(h->ctr, 0, gs::ctr_index(gs::CTR_DELTA) * 4, h->stream));
+    GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 0,
+                          (gs::CTR_COUNT - gs::CTR_FAIL) * gs::kCtrStride * 4, h->stream));
+  } else {
+    GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
+  }
+  {
+    Prof p(h, KID_INIT);
+    gs::launch_init(h->tab, cap + 1, h->stream);
+  }
+  GS_HIP(hipGetLastError());
+  h->nv_ub = 0;
+  h->actset = 0;
+  return GS_OK;
+}
+
+int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
+                     size_t stride, bool check_cap = true);
+
+// Export every (vertex, label, parity) into device arrays; returns count.
+int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n) {
+  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, h->stream));
+  {
+    Prof pr(h, KID_EXPORT);
+    gs::launch_export(h->kind == GS_KIND_SIGNED, h->table(), v, l, p, cap, h->stream);
+  }
+  GS_HIP(hipGetLastError());
+  uint32_t cnt = 0;
+  GS_HIP(hipMemcpyAsync(&cnt, h->ctr + gs::ctr_index(gs::CTR_EXPORT), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  *n = cnt;
+  if (cnt > cap) return fail(GS_ERR_TRUNCATED, "output capacity " + std::to_string(cap) + " < " + std::to_string(cnt));
+  return GS_OK;
+}
+
+// Rebuild into a table of capacity new_cap by re-folding (v, label, parity).
+int grow(gs_summary* h, uint64_t new_cap) {
+  if (new_cap > kMaxCap) return fail(GS_ERR_CAPACITY, "vertex table would exceed 2^30 slots");
+  uint64_t nv = 0;
+  int rc = read_nv(h, &nv);
+  if (rc) return rc;
+  int64_t *v = nullptr, *l = nullptr;
+  uint8_t* p = nullptr;
+  const size_t m = nv + 1;
+  GS_HIP(hipMalloc(&v, m * 8));
+  GS_HIP(hipMalloc(&l, m * 8));
+  GS_HIP(hipMalloc(&p, m));
+  size_t got = 0;
+  rc = export_device_impl(h, v, l, p, m, &got);
+  if (rc) return rc;
+  uint32_t fail_flag = 0;
+  GS_HIP(hipMemcpyAsync(&fail_flag, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  GS_HIP(hipFree(h->tab));
+  h->tab = nullptr;
+  const bool track = h->track;
+  h->track = false;  // the rebuild is not a delta
+  rc = alloc_table(h, new_cap, /*keep_delta=*/true);
+  if (rc) return rc;
+  if (fail_flag) GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, h->stream));
+  h->nv_ub = got;
+  rc = fold_device_impl(h, v, l, p, got, 1, /*check_cap=*/false);
+  h->track = track;
+  if (rc) return rc;
+  GS_HIP(hipStreamSynchronize(h->stream));
+  GS_HIP(hipFree(v));
+  GS_HIP(hipFree(l));
+  GS_HIP(hipFree(p));
+  return GS_OK;
+}
+
+int ensure_capacity(gs_summary* h, size_t n) {
+  const double limit = kMaxLoad * (double)h->cap;
+  h->nv_ub += 2 * (uint64_t)n;
+  if ((double)h->nv_ub <= limit) return GS_OK;
+  uint64_t nv = 0;
+  int rc = read_nv(h, &nv);
+  if (rc) return rc;
+  h->nv_ub = nv + 2 * (uint64_t)n;
+  if ((double)h->nv_ub <= limit) return GS_OK;
+  uint64_t nc = h->cap;
+  while (kMaxLoad * (double)nc < (double)h->nv_ub) nc <<= 1;
+  rc = grow(h, nc);
+  if (rc) return rc;
+  h->nv_ub += 2 * (uint64_t)n;
+  return GS_OK;
+}
+
+int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
+                     size_t stride, bool check_cap) {
+  if (n == 0) return GS_OK;
+  if (check_cap) {
+    int rc = ensure_capacity(h, n);
+    if (rc) return rc;
+  }
+  const bool sign = h->kind == GS_KIND_SIGNED;
+  for (size_t off = 0; off < n; off += kMaxChunk) {
+    const uint32_t c = (uint32_t)std::min<size_t>(kMaxChunk, n - off);
+    const uint32_t blocks = (c + 255) / 256;
+    const uint32_t per_shard_blocks = (blocks + gs::kShards - 1) / gs::kShards;
+    if (h->track) {
+      h->delta_fill_ub += (uint64_t)per_shard_blocks * 256 * 3;
+      if (h->delta_fill_ub > h->delta_shard_cap)
+        return fail(GS_ERR_CAPACITY, "delta list full: call gs_take_delta_device after each fold of <= 2^22 edges");
+    }
+    {
+      Prof p(h, KID_FOLD);
+      gs::launch_fold(sign, h->fused, h->track, h->table(), h->lists(), src + off * stride, dst + off * stride,
+                      w ? w + off : nullptr, c, (uint32_t)stride, h->actset, h->stream);
+    }
+    GS_HIP(hipGetLastError());
+    if (!h->fused) {
+      const int sub = (int)std::min<uint32_t>(per_shard_blocks, 16u);
+      {
+        Prof p(h, KID_HOOK);
+        gs::launch_hook(sign, h->track, h->table(), h->lists(), h->actset, sub, h->stream);
+      }
+      GS_HIP(hipGetLastError());
+      h->actset ^= 1;
+    }
+  }
+  return GS_OK;
+}
+
+int check(gs_handle h) {
+  if (!h) return fail(GS_ERR_INVALID, "null handle");
+  return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gs_last_error(void) { return g_err.c_str(); }
+
+int gs_version(void) { return 100; }
+
+int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
+  if (!out) return fail(GS_ERR_INVALID, "out is null");
+  *out = nullptr;
+  if (kind != GS_KIND_CC && kind != GS_KIND_SIGNED) return fail(GS_ERR_INVALID, "unknown kind");
+  int ndev = 0;
+  GS_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(GS_ERR_HIP, "no HIP device " + std::to_string(device));
+  DeviceGuard g(device);
+  gs_summary* h = new gs_summary();
+  h->device = device;
+  h->kind = kind;
+  const char* fz = getenv("GS_FUSED_HOOK");
+  h->fused = fz && fz[0] == '1';
+  uint64_t cap = next_pow2(std::max<uint64_t>(2 * std::max<uint64_t>(capacity_hint, 1), 1024));
+  if (cap > kMaxCap) cap = kMaxCap;
+  int rc = GS_OK;
+  auto bail = [&](int code) {
+    gs_destroy(h);
+    return code;
+  };
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(GS_ERR_HIP, "hipStreamCreate failed"));
+  if (hipMalloc(&h->ctr, gs::CTR_COUNT * gs::kCtrStride * 4) != hipSuccess)
+    return bail(fail(GS_ERR_HIP, "hipMalloc(counters) failed"));
+  h->act_shard_cap = ((kMaxChunk / 256 + gs::kShards - 1) / gs::kShards) * 256;
+  if (hipMalloc(&h->act, sizeof(uint2) * 2 * gs::kShards * (size_t)h->act_shard_cap) != hipSuccess)
+    return bail(fail(GS_ERR_HIP, "hipMalloc(active list) failed"));
+  if (hipMalloc(&h->d_stage, sizeof(int64_t) * 4 * kStageChunk) != hipSuccess ||
+      hipMalloc(&h->d_wstage, 2 * kStageChunk) != hipSuccess || hipMalloc(&h->d_scratch, 64) != hipSuccess)
+    return bail(fail(GS_ERR_HIP, "hipMalloc(staging) failed"));
+  if (hipHostMalloc(&h->h_stage, sizeof(int64_t) * 4 * kStageChunk, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&h->h_wstage, 2 * kStageChunk, hipHostMallocDefault) != hipSuccess)
+    return bail(fail(GS_ERR_HIP, "hipHostMalloc(staging) failed"));
+  for (int i = 0; i < 2; ++i)
+    if (hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming) != hipSuccess)
+      return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
+  rc = alloc_table(h, cap);
+  if (rc) return bail(rc);
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "init failed"));
+  *out = h;
+  return GS_OK;
+}
+
+int gs_destroy(gs_handle h) {
+  if (!h) return GS_OK;
+  DeviceGuard g(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  drain_profile(h);
+  for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+  for (int i = 0; i < 2; ++i)
+    if (h->stage_ev[i]) (void)hipEventDestroy(h->stage_ev[i]);
+  (void)hipFree(h->tab);
+  (void)hipFree(h->ctr);
+  (void)hipFree(h->act);
+  (void)hipFree(h->da);
+  (void)hipFree(h->db);
+  (void)hipFree(h->dw);
+  (void)hipFree(h->d_stage);
+  (void)hipFree(h->d_wstage);
+  (void)hipFree(h->d_scratch);
+  if (h->h_stage) (void)hipHostFree(h->h_stage);
+  if (h->h_wstage) (void)hipHostFree(h->h_wstage);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return GS_OK;
+}
+
+int gs_reset(gs_handle h) {
+  if (int rc = check(h)) return rc;
+  DeviceGuard g(h->device);
+  GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
+  {
+    Prof p(h, KID_INIT);
+    gs::launch_init(h->tab, h->cap + 1, h->stream);
+  }
+  GS_HIP(hipGetLastError());
+  h->nv_ub = 0;
+  h->actset = 0;
+  h->delta_fill_ub = 0;
+  return GS_OK;
+}
+
+static int fold_host_impl(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n) {
+  for (size_t off = 0; off < n; off += kStageChunk) {
+    const size_t c = std::min<size_t>(kStageChunk, n - off);
+    const int b = h->stage_next;
+    h->stage_next ^= 1;
+    GS_HIP(hipEventSynchronize(h->stage_ev[b]));  // the pinned buffer's previous copy is done
+    int64_t* hs = h->h_stage + (size_t)b * 2 * kStageChunk;
+    int64_t* ds = h->d_stage + (size_t)b * 2 * kStageChunk;
+    memcpy(hs, src + off, c * 8);
+    memcpy(hs + kStageChunk, dst + off, c * 8);
+    GS_HIP(hipMemcpyAsync(ds, hs, c * 8, hipMemcpyHostToDevice, h->stream));
+    GS_HIP(hipMemcpyAsync(ds + kStageChunk, hs + kStageChunk, c * 8, hipMemcpyHostToDevice, h->stream));
+    uint8_t* dwp = nullptr;
+    if (w) {
+      memcpy(h->h_wstage + (size_t)b * kStageChunk, w + off, c);
+      dwp = h->d_wstage + (size_t)b * kStageChunk;
+      GS_HIP(hipMemcpyAsync(dwp, h->h_wstage + (size_t)b * kStageChunk, c, hipMemcpyHostToDevice, h->stream));
+    }
+    GS_HIP(hipEventRecord(h->stage_ev[b], h->stream));
+    int rc = fold_device_impl(h, ds, ds + kStageChunk, dwp, c, 1);
+    if (rc) return rc;
+  }
+  return GS_OK;
+}
+
+int gs_fold(gs_handle h, const int64_t* src, const int64_t* dst, size_t n) {
+  if (int rc = check(h)) return rc;
+  if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
+  DeviceGuard g(h->device);
+  return fold_host_impl(h, src, dst, nullptr, n);
+}
+
+int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n, size_t stride) {
+  if (int rc = check(h)) return rc;
+  if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
+  if (stride == 0) return fail(GS_ERR_INVALID, "stride must be >= 1");
+  DeviceGuard g(h->device);
+  return fold_device_impl(h, src, dst, w, n, stride);
+}
+
+int gs_sync(gs_handle h) {
+  if (int rc = check(h)) return rc;
+  DeviceGuard g(h->device);
+  GS_HIP(hipStreamSynchronize(h->stream));
+  return check_device_flags(h);
+}
+
+int gs_num_vertices(gs_handle h, uint64_t* n) {
+  if (int rc = check(h)) return rc;
+  if (!n) return fail(GS_ERR_INVALID, "n is null");
+  DeviceGuard g(h->device);
+  int rc = read_nv(h, n);
+  if (rc) return rc;
+  return check_device_flags(h);
+}
+
+int gs_find(gs_handle h, int64_t v, int64_t* label, int* found) {
+  if (int rc = check(h)) return rc;
+  if (!label || !found) return fail(GS_ERR_INVALID, "null output");
+  DeviceGuard g(h->device);
+  gs::launch_find_one(h->table(), v, h->d_scratch, h->stream);
+  GS_HIP(hipGetLastError());
+  int64_t out[2];
+  GS_HIP(hipMemcpyAsync(out, h->d_scratch, 16, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  *found = (int)out[0];
+  *label = out[1];
+  return GS_OK;
+}
+
+int gs_export_labels_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* parity, size_t cap, size_t* n) {
+  if (int rc = check(h)) return rc;
+  if (!n) return fail(GS_ERR_INVALID, "n is null");
+  DeviceGuard g(h->device);
+  return export_device_impl(h, v, label, parity, cap, n);
+}
+
+static int export_host(gs_handle h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n) {
+  uint64_t nv = 0;
+  int rc = read_nv(h, &nv);
+  if (rc) return rc;
+  *n = nv;
+  if (cap < nv) return fail(GS_ERR_TRUNCATED, "output capacity " + std::to_string(cap) + " < " + std::to_string(nv));
+  if (nv == 0) return GS_OK;
+  int64_t *dv = nullptr, *dl = nullptr;
+  uint8_t* dp = nullptr;
+  GS_HIP(hipMalloc(&dv, nv * 8));
+  GS_HIP(hipMalloc(&dl, nv * 8));
+  GS_HIP(hipMalloc(&dp, nv));
+  size_t got = 0;
+  rc = export_device_impl(h, dv, dl, dp, nv, &got);
+  if (rc == GS_OK) {
+    if (v) GS_HIP(hipMemcpyAsync(v, dv, got * 8, hipMemcpyDeviceToHost, h->stream));
+    if (l) GS_HIP(hipMemcpyAsync(l, dl, got * 8, hipMemcpyDeviceToHost, h->stream));
+    if (p) GS_HIP(hipMemcpyAsync(p, dp, got, hipMemcpyDeviceToHost, h->stream));
+    GS_HIP(hipStreamSynchronize(h->stream));
+    *n = got;
+  }
+  (void)hipFree(dv);
+  (void)hipFree(dl);
+  (void)hipFree(dp);
+  return rc;
+}
+
+int gs_export_labels(gs_handle h, int64_t* v, int64_t* label, size_t cap, size_t* n) {
+  if (int rc = check(h)) return rc;
+  if (!n) return fail(GS_ERR_INVALID, "n is null");
+  DeviceGuard g(h->device);
+  return export_host(h, v, label, nullptr, cap, n);
+}
+
+int gs_bip_status(gs_handle h, int* ok) {
+  if (int rc = check(h)) return rc;
+  if (!ok) return fail(GS_ERR_INVALID, "ok is null");
+  DeviceGuard g(h->device);
+  uint32_t f = 0;
+  GS_HIP(hipMemcpyAsync(&f, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  *ok = f ? 0 : 1;
+  return GS_OK;
+}
+
+int gs_export_colouring(gs_handle h, int64_t* comp, int64_t* v, uint8_t* sign, size_t cap, size_t* n) {
+  if (int rc = check(h)) return rc;
+  if (!n) return fail(GS_ERR_INVALID, "n is null");
+  int ok = 1;
+  int rc = gs_bip_status(h, &ok);
+  if (rc) return rc;
+  if (!ok) {
+    *n = 0;
+    return GS_OK;
+  }
+  DeviceGuard g(h->device);
+  rc = export_host(h, v, comp, sign, cap, n);
+  if (rc) return rc;
+  if (sign)
+    for (size_t i = 0; i < *n; ++i) sign[i] = sign[i] ? 0 : 1;  // parity 0 <=> same colour as the minimum
+  return GS_OK;
+}
+
+int gs_combine(gs_handle dst, gs_handle src) {
+  if (int rc = check(dst)) return rc;
+  if (int rc = check(src)) return rc;
+  if (dst == src) return GS_OK;
+  if (dst->kind != src->kind) return fail(GS_ERR_INVALID, "summaries of different kinds");
+  uint64_t nv = 0;
+  int64_t *sv = nullptr, *sl = nullptr;
+  uint8_t* sp = nullptr;
+  size_t got = 0;
+  uint32_t sfail = 0;
+  {
+    DeviceGuard g(src->device);
+    int rc = read_nv(src, &nv);
+    if (rc) return rc;
+    GS_HIP(hipMemcpyAsync(&sfail, src->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, src->stream));
+    GS_HIP(hipStreamSynchronize(src->stream));
+    if (nv) {
+      GS_HIP(hipMalloc(&sv, nv * 8));
+      GS_HIP(hipMalloc(&sl, nv * 8));
+      GS_HIP(hipMalloc(&sp, nv));
+      rc = export_device_impl(src, sv, sl, sp, nv, &got);
+      if (rc) return rc;
+    }
+  }
+  DeviceGuard g(dst->device);
+  int rc = GS_OK;
+  if (sfail) {
+    GS_HIP(hipMemsetAsync(dst->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, dst->stream));
+  } else if (got) {
+    int64_t *dv = sv, *dl = sl;
+    uint8_t* dp = sp;
+    if (dst->device != src->device) {
+      GS_HIP(hipMalloc(&dv, got * 8));
+      GS_HIP(hipMalloc(&dl, got * 8));
+      GS_HIP(hipMalloc(&dp, got));
+      GS_HIP(hipMemcpyPeerAsync(dv, dst->device, sv, src->device, got * 8, dst->stream));
+      GS_HIP(hipMemcpyPeerAsync(dl, dst->device, sl, src->device, got * 8, dst->stream));
+      GS_HIP(hipMemcpyPeerAsync(dp, dst->device, sp, src->device, got, dst->stream));
+    }
+    rc = fold_device_impl(dst, dv, dl, dp, got, 1);
+    GS_HIP(hipStreamSynchronize(dst->stream));
+    if (dv != sv) {
+      (void)hipFree(dv);
+      (void)hipFree(dl);
+      (void)hipFree(dp);
+    }
+  }
+  (void)hipFree(sv);
+  (void)hipFree(sl);
+  (void)hipFree(sp);
+  return rc;
+}
+
+// Serialized image: u32 magic 'GSS1', u32 kind, u32 ok, u32 0, u64 n, int64 v[n], int64 label[n], u8 parity[n]
+int gs_serialize(gs_handle h, void* buf, size_t cap, size_t* len) {
+  if (int rc = check(h)) return rc;
+  if (!len) return fail(GS_ERR_INVALID, "len is null");
+  DeviceGuard g(h->device);
+  uint64_t nv = 0;
+  int rc = read_nv(h, &nv);
+  if (rc) return rc;
+  const size_t need = 24 + nv * 17;
+  *len = need;
+  if (!buf) return GS_OK;
+  if (cap < need) return fail(GS_ERR_TRUNCATED, "buffer too small");
+  int ok = 1;
+  rc = gs_bip_status(h, &ok);
+  if (rc) return rc;
+  uint8_t* b = static_cast<uint8_t*>(buf);
+  std::vector<int64_t> v(nv), l(nv);
+  std::vector<uint8_t> p(nv);
+  size_t got = 0;
+  if (nv) {
+    rc = export_host(h, v.data(), l.data(), p.data(), nv, &got);
+    if (rc) return rc;
+  }
+  const uint32_t hdr[4] = {0x31535347u, (uint32_t)h->kind, (uint32_t)ok, 0u};
+  const uint64_t n64 = got;
+  memcpy(b, hdr, 16);
+  memcpy(b + 16, &n64, 8);
+  memcpy(b + 24, v.data(), got * 8);
+  memcpy(b + 24 + got * 8, l.data(), got * 8);
+  memcpy(b + 24 + got * 16, p.data(), got);
+  *len = 24 + got * 17;
+  return GS_OK;
+}
+
+int gs_deserialize(gs_handle h, const void* buf, size_t len) {
+  if (int rc = check(h)) return rc;
+  if (!buf || len < 24) return fail(GS_ERR_INVALID, "truncated image");
+  const uint8_t* b = static_cast<const uint8_t*>(buf);
+  uint32_t hdr[4];
+  uint64_t n = 0;
+  memcpy(hdr, b, 16);
+  memcpy(&n, b + 16, 8);
+  if (hdr[0] != 0x31535347u) return fail(GS_ERR_INVALID, "bad magic");
+  if ((int)hdr[1] != h->kind) return fail(GS_ERR_INVALID, "image of a different summary kind");
+  if (len < 24 + n * 17) return fail(GS_ERR_INVALID, "truncated image");
+  int rc = gs_reset(h);
+  if (rc) return rc;
+  DeviceGuard g(h->device);
+  if (!hdr[2]) {
+    GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, h->stream));
+    return gs_sync(h);
+  }
+  const int64_t* v = reinterpret_cast<const int64_t*>(b + 24);
+  std::vector<int64_t> vv(v, v + n), ll(n);
+  memcpy(ll.data(), b + 24 + n * 8, n * 8);
+  rc = fold_host_impl(h, vv.data(), ll.data(), b + 24 + n * 16, n);
+  if (rc) return rc;
+  return gs_sync(h);
+}
+
+int gs_set_delta_tracking(gs_handle h, int on) {
+  if (int rc = check(h)) return rc;
+  DeviceGuard g(h->device);
+  if (on && !h->da) {
+    // worst case between two takes: one fold chunk of kMaxChunk edges
+    h->delta_shard_cap = ((kMaxChunk / 256 + gs::kShards - 1) / gs::kShards) * 256 * 3;
+    const size_t m = (size_t)gs::kShards * h->delta_shard_cap;
+    GS_HIP(hipMalloc(&h->da, m * 8));
+    GS_HIP(hipMalloc(&h->db, m * 8));
+    GS_HIP(hipMalloc(&h->dw, m));
+  }
+  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, gs::kShards * gs::kCtrStride * 4, h->stream));
+  h->delta_fill_ub = 0;
+  h->track = on != 0;
+  return GS_OK;
+}
+
+int gs_take_delta_device(gs_handle h, int64_t* a, int64_t* b, uint8_t* w, size_t cap, size_t* n) {
+  if (int rc = check(h)) return rc;
+  if (!n) return fail(GS_ERR_INVALID, "n is null");
+  if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
+  DeviceGuard g(h->device);
+  std::vector<uint32_t> c(gs::kShards * gs::kCtrStride);
+  GS_HIP(hipMemcpyAsync(c.data(), h->ctr + gs::ctr_index(gs::CTR_DELTA), c.size() * 4, hipMemcpyDeviceToHost,
+                        h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  int rc = check_device_flags(h);
+  if (rc) return rc;
+  uint64_t total = 0;
+  uint32_t mx = 0;
+  for (int s = 0; s < gs::kShards; ++s) {
+    total += c[s * gs::kCtrStride];
+    mx = std::max(mx, c[s * gs::kCtrStride]);
+  }
+  *n = total;
+  if (total > cap) return fail(GS_ERR_TRUNCATED, "delta capacity too small");
+  if (total) {
+    const int sub = (int)std::min<uint32_t>((mx + 255) / 256, 64u);
+    gs::launch_pack(h->table(), h->lists(), a, b, w, cap, std::max(sub, 1), h->stream);
+    GS_HIP(hipGetLastError());
+  }
+  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, gs::kShards * gs::kCtrStride * 4, h->stream));
+  h->delta_fill_ub = 0;
+  return GS_OK;
+}
+
+int gs_get_stream(gs_handle h, void** stream) {
+  if (int rc = check(h)) return rc;
+  if (!stream) return fail(GS_ERR_INVALID, "stream is null");
+  *stream = (void*)h->stream;
+  return GS_OK;
+}
+
+int gs_set_profiling(gs_handle h, int on) {
+  if (int rc = check(h)) return rc;
+  DeviceGuard g(h->device);
+  (void)hipStreamSynchronize(h->stream);
+  drain_profile(h);
+  h->profiling = on != 0;
+  for (int i = 0; i < KID_N; ++i) {
+    h->launches[i] = 0;
+    h->total_ms[i] = 0;
+  }
+  return GS_OK;
+}
+
+int gs_kernel_stats(gs_handle h, int id, uint64_t* launches, double* total_ms) {
+  if (int rc = check(h)) return rc;
+  if (id < 0 || id >= KID_N || !launches || !total_ms) return fail(GS_ERR_INVALID, "bad kernel id");
+  DeviceGuard g(h->device);
+  drain_profile(h);
+  *launches = h->launches[id];
+  *total_ms = h->total_ms[id];
+  return GS_OK;
+}
+
+int gs_table_capacity(gs_handle h, uint64_t* slots) {
+  if (int rc = check(h)) return rc;
+  if (!slots) return fail(GS_ERR_INVALID, "slots is null");
+  *slots = h->cap;
+  return GS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,20 @@
+// gs_kernels.hpp -- host-side launchers of the summary kernels (gs_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gs_device.hpp"
+
+namespace gs {
+
+void launch_init(Slot* tab, uint64_t nslots, hipStream_t st);
+void launch_fold(bool sign, bool fused, bool track, const Table& t, const Lists& L, const int64_t* src,
+                 const int64_t* dst, const uint8_t* w, uint32_t n, uint32_t stride, int actset, hipStream_t st);
+void launch_hook(bool sign, bool track, const Table& t, const Lists& L, int actset, int sub, hipStream_t st);
+void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out,
+                   hipStream_t st);
+void launch_pack(const Table& t, const Lists& L, int64_t* oa, int64_t* ob, uint8_t* ow, uint64_t cap_out, int sub,
+                 hipStream_t st);
+void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st);
+
+}  // namespace gs

@@ -1,0 +1,150 @@
+/*
+ * gs_summary.h -- C ABI of the MI355X-native summary-aggregation hot path.
+ *
+ * Drop-in boundary for gelly-streaming's SimpleEdgeStream.aggregate() ->
+ * SummaryBulkAggregation path as used by ConnectedComponents (DisjointSet summary)
+ * and BipartitenessCheck (Candidates summary). A GPU-resident union-find forest
+ * (CC) or signed union-find forest (bipartiteness) lives behind an opaque handle;
+ * the JVM-side summary objects buffer their per-edge callbacks and flush them here
+ * (binding stubs: INTEGRATION.md). Reference paths are relative to
+ * src/main/java/org/apache/flink/graph/streaming/ in jiexray/gelly-streaming.
+ *
+ * Conventions
+ *   - Every function returns GS_OK (0) or a negative GS_ERR_* code; the message of
+ *     the last failure on the calling thread is gs_last_error() (the reference's
+ *     `throws Exception` on foldEdges/reduce, EdgesFold.java:47).
+ *   - Plain pointers and sizes only. "host" buffers are caller-owned and copied
+ *     before the call returns; "device" buffers must live on the handle's device.
+ *   - A handle is thread-compatible (one thread at a time), the library is
+ *     re-entrant across handles. Work is enqueued on the handle's own HIP stream;
+ *     functions that return data to the host synchronise that stream.
+ *   - Vertex ids are signed 64-bit (Edge<Long,...>; Integer ids widen losslessly).
+ *     Canonical component label = minimum signed id in the component.
+ */
+#ifndef GS_SUMMARY_H
+#define GS_SUMMARY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gs_summary* gs_handle;
+
+enum gs_status {
+  GS_OK = 0,
+  GS_ERR_INVALID = -1,  /* bad argument / handle */
+  GS_ERR_HIP = -2,      /* HIP runtime error (device missing, OOM, launch failure) */
+  GS_ERR_CAPACITY = -3, /* vertex table cannot grow further */
+  GS_ERR_TRUNCATED = -4 /* output buffer too small; *n holds the required count */
+};
+
+enum gs_kind {
+  GS_KIND_CC = 0,     /* DisjointSet (DisjointSet.java:25-151) via ConnectedComponents */
+  GS_KIND_SIGNED = 1  /* Candidates (Candidates.java:27-196) via BipartitenessCheck  */
+};
+
+/* Last error message of the calling thread ("" if none). */
+const char* gs_last_error(void);
+
+/* Library/ABI version (major*10000 + minor*100 + patch). */
+int gs_version(void);
+
+/* Create an empty summary on HIP device `device`. `capacity_hint` = expected
+ * number of distinct vertices (the table grows past it automatically).
+ * Replaces the summary's initial value: `new DisjointSet<>()`
+ * (ConnectedComponents.java:52-54) / `new Candidates(true)` (BipartitenessCheck.java:50-52). */
+int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint);
+
+/* Release the handle and its device memory. */
+int gs_destroy(gs_handle h);
+
+/* Reset to the initial value (empty forest, verdict true). Replaces
+ * `summary = initialVal` of a transient Merger (SummaryAggregation.java:113-115). */
+int gs_reset(gs_handle h);
+
+/* Fold n edges from HOST memory: for each i, union(src[i], dst[i]).
+ * Replaces UpdateCC.foldEdges -> DisjointSet.union (ConnectedComponents.java:83-86,
+ * DisjointSet.java:92-118) and updateFunction.foldEdges ->
+ * candidates.merge(edgeToCandidate(u, v)) (BipartitenessCheck.java:54-61,93-95),
+ * called once per buffered micro-batch instead of once per edge.
+ * New endpoints are added (DisjointSet.makeSet :53-56); a self-loop adds its vertex
+ * and never fails the bipartiteness verdict (BipartitenessCheck.java:58-59). */
+int gs_fold(gs_handle h, const int64_t* src, const int64_t* dst, size_t n);
+
+/* Same, from DEVICE memory already resident on the handle's device. Element i is
+ * src[i*stride], dst[i*stride] (stride 1: two arrays; stride 2 with dst = src + 1:
+ * interleaved pairs). `w` (device, optional, may be NULL) gives the required colour
+ * parity per edge for GS_KIND_SIGNED (1 = different sides, the edge default;
+ * 0 = same side, used when a serialized/exported summary is merged back). The
+ * caller guarantees the inputs are complete before work on the handle's stream. */
+int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n, size_t stride);
+
+/* Merge summary `src` into `dst` (either may be on any device; `src` is unchanged).
+ * Replaces CombineCC.reduce -> DisjointSet.merge (ConnectedComponents.java:116-126,
+ * DisjointSet.java:127-131) and combineFunction.reduce -> Candidates.merge
+ * (BipartitenessCheck.java:128-130, Candidates.java:77-139); the verdict is the AND. */
+int gs_combine(gs_handle dst, gs_handle src);
+
+/* Block until all work queued on the handle has finished. */
+int gs_sync(gs_handle h);
+
+/* Number of distinct vertices seen (DisjointSet.getMatches().size(), :44-46). */
+int gs_num_vertices(gs_handle h, uint64_t* n);
+
+/* Canonical label of one vertex: *label = min id of its component; *found = 0 if
+ * the vertex was never seen (DisjointSet.find returns null, :66-69). */
+int gs_find(gs_handle h, int64_t v, int64_t* label, int* found);
+
+/* Export every (vertex, canonical label) pair to HOST arrays of capacity `cap`,
+ * unordered. *n = number of vertices (GS_ERR_TRUNCATED if cap < *n; nothing
+ * written). Replaces getMatches()/find()/toString() sinks (DisjointSet.java:44-46,
+ * 134-150; ConnectedComponentsExample.FlattenSet :143-156). */
+int gs_export_labels(gs_handle h, int64_t* v, int64_t* label, size_t cap, size_t* n);
+
+/* Same into DEVICE arrays; *n is written on the host (synchronises). Used for
+ * the final canonical label pass without a device->host copy. `parity` (device,
+ * may be NULL) receives parity(v) xor parity(label) for GS_KIND_SIGNED. */
+int gs_export_labels_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* parity, size_t cap, size_t* n);
+
+/* Bipartiteness verdict so far (Candidates.getSuccess, :44-46): 1 = bipartite. */
+int gs_bip_status(gs_handle h, int* ok);
+
+/* Canonical colouring to HOST arrays (Candidates.getMap, :48-50): comp = min id of
+ * the component, sign = 1 when v has the colour of comp (SignedVertex sign,
+ * SignedVertex.java:23-40). Unordered. When the verdict is false, *n = 0
+ * (the reference's fail() state is (false,{}), Candidates.java:194-196). */
+int gs_export_colouring(gs_handle h, int64_t* comp, int64_t* v, uint8_t* sign, size_t cap, size_t* n);
+
+/* Checkpoint: compact (vertex, label, parity) image of the summary plus the
+ * verdict, for Merger.snapshotState/restoreState (SummaryAggregation.java:127-135).
+ * Call with buf = NULL to get *len. gs_deserialize replaces the summary. */
+int gs_serialize(gs_handle h, void* buf, size_t cap, size_t* len);
+int gs_deserialize(gs_handle h, const void* buf, size_t len);
+
+/* ---- streaming delta (multi-GPU combine; see DESIGN.md "Multi-GPU") ----------
+ * While tracking is on, every fold records the structural changes it made as
+ * (key, key2, parity) triples: each newly seen vertex as (v, v, 0) and each
+ * successful hook as (root, new parent, parity). Folding another replica's delta
+ * into this summary reproduces that replica's changes (union is associative and
+ * commutative). gs_take_delta_device packs the delta since the previous take into
+ * DEVICE arrays and clears it. */
+int gs_set_delta_tracking(gs_handle h, int on);
+int gs_take_delta_device(gs_handle h, int64_t* a, int64_t* b, uint8_t* w, size_t cap, size_t* n);
+
+/* ---- introspection -----------------------------------------------------------
+ * The HIP stream (hipStream_t) the handle enqueues on, and per-kernel timing:
+ * when profiling is on, every launch is bracketed by HIP events on that stream;
+ * gs_kernel_stats returns (launches, total milliseconds) for kernel `id`
+ * (0 = fold/find, 1 = hook, 2 = export, 3 = init). */
+int gs_get_stream(gs_handle h, void** stream);
+int gs_set_profiling(gs_handle h, int on);
+int gs_kernel_stats(gs_handle h, int id, uint64_t* launches, double* total_ms);
+int gs_table_capacity(gs_handle h, uint64_t* slots);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GS_SUMMARY_H */

@@ -1,0 +1,55 @@
+"""CPU: the C-ABI library loads, exports every symbol include/*.h declares, and
+refuses to run without a GPU (no CPU fallback). No compute calls here."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    names = set()
+    for h in ("gs_summary.h", "gs_gen.h"):
+        with open(os.path.join(ROOT, "include", h)) as f:
+            text = f.read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names.update(re.findall(r"\b(gs_[a-z_]+)\s*\(", text))
+    return names
+
+
+def test_library_exports_every_declared_symbol(gs):
+    declared = _declared_symbols()
+    assert len(declared) >= 20
+    L = ctypes.CDLL(gs.LIB_PATH)
+    missing = [n for n in sorted(declared) if not hasattr(L, n)]
+    assert not missing, missing
+    assert declared == set(gs.EXPORTED_SYMBOLS)
+
+
+def test_version_and_error_string(gs):
+    assert gs.lib().gs_version() >= 100
+    assert isinstance(gs.lib().gs_last_error(), bytes)
+
+
+def test_null_arguments_are_rejected(gs):
+    L = gs.lib()
+    assert L.gs_create(None, 0, 0, 16) == gs.GS_ERR_INVALID
+    assert L.gs_fold(None, None, None, 0) == gs.GS_ERR_INVALID
+    assert b"null" in L.gs_last_error()
+    assert L.gs_destroy(None) == gs.GS_OK
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is present")
+def test_no_gpu_fails_loudly(gs):
+    with pytest.raises(gs.GSError) as e:
+        gs.Summary("cc", device=0, capacity_hint=16)
+    assert e.value.code == gs.GS_ERR_HIP
+
+
+def test_library_is_gfx950_code_object(gs):
+    # the shared object carries a gfx950 offload bundle
+    with open(gs.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"gfx950" in blob

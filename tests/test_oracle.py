@@ -1,0 +1,181 @@
+"""CPU: pin the oracle (CPU restatement) to the reference's own test vectors, the
+derived goldens of the bundled default streams, and independent truth."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _pins():
+    with open(os.path.join(GOLD, "reference_pins.json")) as f:
+        return json.load(f)
+
+
+def _derived():
+    with open(os.path.join(GOLD, "derived.json")) as f:
+        return json.load(f)
+
+
+def test_connected_components_test_pin(oracle_mod):
+    # ConnectedComponentsTest.test (ConnectedComponentsTest.java:25-47), p = 1
+    p = _pins()["cc_test"]
+    s, d = zip(*p["edges"])
+    emissions = oracle_mod.cc_dataflow(s, d)
+    assert oracle_mod.cc_test_parser(emissions) == p["expected_lines"]
+
+
+def test_connected_components_test_pin_any_window_split(oracle_mod):
+    # 5 ms ingestion-time windows may split the collection anywhere; only the
+    # last emission is asserted by the reference test.
+    p = _pins()["cc_test"]
+    s, d = zip(*p["edges"])
+    for cut in range(len(s) + 1):
+        win = [0] * cut + [1] * (len(s) - cut)
+        assert oracle_mod.cc_test_parser(oracle_mod.cc_dataflow(s, d, win)) == p["expected_lines"]
+
+
+def test_bipartiteness_test_pins(oracle_mod):
+    pins = _pins()
+    for key in ("bip_test_bipartite", "bip_test_non_bipartite"):
+        p = pins[key]
+        s, d = zip(*p["edges"])
+        assert oracle_mod.bip_dataflow(s, d) == p["expected"], key
+
+
+def test_disjointset_unit_test(oracle_mod):
+    # DisjointSetTest.testGetMatches/testFind/testMerge on the restatement
+    assert oracle_mod.disjointset_unit_test() == 0
+
+
+def test_cc_default_stream_golden(oracle_mod):
+    g = _derived()["cc_default_stream"]
+    k = np.arange(1, 101, dtype=np.int64)
+    em = oracle_mod.cc_dataflow(k, k + 2, (k * 100) // 1000)
+    assert em == g["emissions"]
+    assert len(em) == 11  # windows of 9,10,...,10,1 edges
+    assert em[-1].startswith("{1=[1, 3, 5") and "2=[2, 4, 6" in em[-1]
+
+
+def test_bip_default_stream_golden(oracle_mod):
+    g = _derived()["bip_default_stream"]
+    k = np.repeat(np.arange(1, 101, dtype=np.int64), 10)
+    em = oracle_mod.bip_dataflow(k, 2 * k + 1)
+    assert em == g["emissions"]
+    assert em[0].startswith("(true,{1={1=(1,true), 3=(3,false), 7=(7,true), 15=(15,false), 31=(31,true), "
+                            "63=(63,false), 127=(127,true)}, 2={2=(2,true), 5=(5,false),")
+
+
+def test_candidates_order_quirk_reproduced(oracle_mod):
+    # the reference's Candidates.merge is order dependent.
+    g = _derived()["bip_triangle_quirk"]
+    assert oracle_mod.bip_dataflow([2, 1, 1], [3, 2, 3]) == g["order_231"] == [
+        "(true,{1={1=(1,false), 2=(2,true), 3=(3,true)}})"]
+    assert oracle_mod.bip_dataflow([1, 2, 1], [2, 3, 3]) == g["order_123"] == ["(false,{})"]
+
+
+def test_self_loop_never_fails(oracle_mod):
+    # BipartitenessCheck.edgeToCandidate ignores the second add (:58-59)
+    assert oracle_mod.bip_dataflow([5], [5]) == ["(true,{5={5=(5,true)}})"]
+    ok, comp, v, sign = oracle_mod.bip_truth([5, 1], [5, 2])
+    assert ok and oracle_mod.canonical_candidates_string(ok, comp, v, sign) == \
+        "(true,{1={1=(1,true), 2=(2,false)}, 5={5=(5,true)}})"
+
+
+def test_generators_match_fixture(oracle_mod):
+    z = np.load(os.path.join(GOLD, "streams.npz"))
+    s, d = oracle_mod.rmat_edges(0x5EED0020, 20, 0, 4096, True)
+    assert np.array_equal(s, z["rmat20_prefix_src"]) and np.array_equal(d, z["rmat20_prefix_dst"])
+    s, d = oracle_mod.rmat_edges(0x5EED0026, 26, (1 << 29) - 2048, 4096, True)
+    assert np.array_equal(s, z["rmat26_mid_src"]) and np.array_equal(d, z["rmat26_mid_dst"])
+    s, d = oracle_mod.er_edges(0x5EED00E5, 22, 0, 4096, True)
+    assert np.array_equal(s, z["er22_prefix_src"]) and np.array_equal(d, z["er22_prefix_dst"])
+    s, d = oracle_mod.bip_edges(0x5EED0B1B, 19, 0, 4096, z["bip19_prefix_inject"])
+    assert np.array_equal(s, z["bip19_prefix_src"]) and np.array_equal(d, z["bip19_prefix_dst"])
+
+
+def test_rmat_unscrambled_is_in_range(oracle_mod):
+    s, d = oracle_mod.rmat_edges(7, 10, 0, 1 << 12, False)
+    assert s.min() >= 0 and s.max() < 1 << 10 and d.min() >= 0 and d.max() < 1 << 10
+    # skew: vertex 0 (quadrant a at every level) is the hub
+    assert np.bincount(np.concatenate([s, d])).argmax() == 0
+
+
+def test_cc_labels_vs_networkx(oracle_mod):
+    nx = pytest.importorskip("networkx")
+    rng = np.random.default_rng(1)
+    for trial in range(20):
+        n = int(rng.integers(1, 60))
+        m = int(rng.integers(0, 80))
+        s = rng.integers(-n, n, m)
+        d = rng.integers(-n, n, m)
+        v, lab = oracle_mod.cc_labels(s, d)
+        g = nx.Graph()
+        g.add_edges_from(zip(s.tolist(), d.tolist()))
+        truth = {}
+        for c in nx.connected_components(g):
+            for x in c:
+                truth[x] = min(c)
+        assert sorted(truth) == v.tolist()
+        assert [truth[x] for x in v.tolist()] == lab.tolist()
+
+
+def test_bip_truth_vs_networkx(oracle_mod):
+    nx = pytest.importorskip("networkx")
+    rng = np.random.default_rng(2)
+    for trial in range(40):
+        n = int(rng.integers(2, 40))
+        m = int(rng.integers(1, 60))
+        s = rng.integers(0, n, m)
+        d = rng.integers(0, n, m)
+        keep = s != d
+        s, d = s[keep], d[keep]
+        if len(s) == 0:
+            continue
+        g = nx.Graph()
+        g.add_edges_from(zip(s.tolist(), d.tolist()))
+        ok, comp, v, sign = oracle_mod.bip_truth(s, d)
+        assert ok == nx.is_bipartite(g)
+
+
+def _first_appearance(s, d):
+    ids = {}
+    for a, b in zip(s.tolist(), d.tolist()):
+        for x in (a, b):
+            if x not in ids:
+                ids[x] = len(ids) + 1
+    return (np.array([ids[x] for x in s.tolist()], np.int64), np.array([ids[x] for x in d.tolist()], np.int64))
+
+
+def test_quirk_oracle_exact_regime_matches_truth(oracle_mod):
+    # first-appearance ids + one window + p = 1 => the reference's
+    # Candidates result equals the canonical truth.
+    rng = np.random.default_rng(3)
+    for trial in range(150):
+        n = int(rng.integers(2, 30))
+        m = int(rng.integers(1, 40))
+        s = rng.integers(0, n, m)
+        d = rng.integers(0, n, m)
+        s, d = _first_appearance(s, d)
+        quirk = oracle_mod.bip_dataflow(s, d)
+        truth = oracle_mod.canonical_candidates_string(*oracle_mod.bip_truth(s, d))
+        assert quirk == [truth], (s, d)
+
+
+def test_cc_dataflow_partitions_and_windows_are_order_free(oracle_mod):
+    rng = np.random.default_rng(4)
+    s, d = oracle_mod.rmat_edges(11, 10, 0, 3000, True)
+    base = oracle_mod.cc_dataflow(s, d)[-1]
+    for p in (2, 3, 7):
+        part = rng.integers(0, p, len(s)).astype(np.int32)
+        win = np.sort(rng.integers(0, 5, len(s)))
+        assert oracle_mod.cc_dataflow(s, d, win, part)[-1] == base
+
+
+def test_cpu_baseline_runs(oracle_mod):
+    s, d = oracle_mod.rmat_edges(0x5EED0026, 16, 0, 1 << 14, True)
+    assert oracle_mod.cpu_baseline_cc(s, d, 1 << 12) > 0
+    assert oracle_mod.cpu_baseline_cc(s, d, 1 << 12, threads=2) > 0
+    assert oracle_mod.cpu_baseline_bip(s[:256], d[:256]) > 0
