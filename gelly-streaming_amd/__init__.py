@@ -63,6 +63,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError("libgs_summary.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+    # torch (ROCm 7.0 wheel) bundles its own libamdhip64.so.7 with the same SONAME as
+    # /opt/rocm's: whichever loads first serves the whole process. Load torch's first
+    # so torch tensors and this library share one HIP runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     L.gs_last_error.restype = ctypes.c_char_p
     L.gs_create.argtypes = [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int, _u64]

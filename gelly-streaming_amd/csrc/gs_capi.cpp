@@ -340,8 +340,9 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   gs_summary* h = new gs_summary();
   h->device = device;
   h->kind = kind;
+  // hook inside k_fold (default) or compacted into k_hook (GS_FUSED_HOOK=0)
   const char* fz = getenv("GS_FUSED_HOOK");
-  h->fused = fz && fz[0] == '1';
+  h->fused = !(fz && fz[0] == '0');
   uint64_t cap = next_pow2(std::max<uint64_t>(2 * std::max<uint64_t>(capacity_hint, 1), 1024));
   if (cap > kMaxCap) cap = kMaxCap;
   int rc = GS_OK;

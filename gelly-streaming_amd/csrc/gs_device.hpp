@@ -92,9 +92,12 @@ __device__ __forceinline__ int64_t settle_key(const Table& t, uint32_t s, int64_
   return k;
 }
 
-// Insert-or-find of one id. Returns the slot (dense id), the slot's observed link
-// and whether this call inserted it. Linear probing over 16-B slots (4 per 64-B line).
-__device__ __forceinline__ uint32_t lookup_insert(const Table& t, int64_t key, uint32_t& link, bool& fresh) {
+// Insert-or-find of one id whose first probe slot h was already loaded as (k, l)
+// (callers issue both endpoints' first loads back to back so they overlap).
+// Returns the slot (dense id), the slot's observed link and whether this call
+// inserted it. Linear probing over 16-B slots (4 per 64-B line).
+__device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, uint32_t h, int64_t k, uint32_t l,
+                                                   uint32_t& link, bool& fresh) {
   fresh = false;
   if (key == kEmpty) {
     const uint32_t old = atomicOr(&t.tab[t.capidx].aux, 1u);
@@ -102,11 +105,7 @@ __device__ __forceinline__ uint32_t lookup_insert(const Table& t, int64_t key, u
     link = t.capidx << 1;  // the minimum id is always a root
     return t.capidx;
   }
-  uint32_t h = hash_slot(key, t.shift);
   for (uint32_t probes = 0; probes <= t.mask; ++probes) {
-    int64_t k;
-    uint32_t l;
-    load_slot(t.tab + h, k, l);
     if (k == key) {
       link = l;
       return h;
@@ -125,42 +124,81 @@ __device__ __forceinline__ uint32_t lookup_insert(const Table& t, int64_t key, u
       }
     }
     h = (h + 1) & t.mask;
+    load_slot(t.tab + h, k, l);
   }
   atomicOr(&t.ctr[ctr_index(CTR_ERR)], 1u);
   return kNoSlot;
 }
 
-// Find with path halving. (x, lx, kx) = start slot, its observed link and key.
-// Returns the (believed) root, the parity x->root and the root's key.
-// FRESH: read links with agent-scope loads (hook phase, where roots move).
+__device__ __forceinline__ uint32_t lookup_insert(const Table& t, int64_t key, uint32_t& link, bool& fresh) {
+  const uint32_t h = hash_slot(key, t.shift);
+  int64_t k;
+  uint32_t l;
+  load_slot(t.tab + h, k, l);
+  return lookup_resolve(t, key, h, k, l, link, fresh);
+}
+
+// One step of a find with path splitting. (x, lx, kx): current slot, its link and
+// key; (kp, lp): the loaded slot of p = parent(x). Moves x to p; when p is not a
+// root, x is re-pointed at its grandparent with the composed parity first (x is a
+// non-root forever and the grandparent is an ancestor: a benign race).
+__device__ __forceinline__ void find_step(const Table& t, uint32_t& x, uint32_t& lx, int64_t& kx, uint32_t& acc,
+                                          bool& done, int64_t kp, uint32_t lp) {
+  const uint32_t p = lx >> 1;
+  const uint32_t gp = lp >> 1;
+  acc ^= lx & 1u;
+  if (gp != p) t.tab[x].link = (gp << 1) | ((lx ^ lp) & 1u);
+  else done = true;
+  x = p;
+  lx = lp;
+  kx = kp;
+}
+
+// Find of one slot: on return x is the (believed) root, acc the parity from the
+// start, kx the root's key. FRESH: read links with agent-scope loads (hook phase).
+template <bool FRESH>
+__device__ __forceinline__ void find_root1(const Table& t, uint32_t& x, uint32_t& lx, int64_t& kx, uint32_t& acc) {
+  bool done = (lx >> 1) == x;
+  while (!done) {
+    int64_t kp;
+    uint32_t lp;
+    load_slot(t.tab + (lx >> 1), kp, lp);
+    if (FRESH) lp = load_link_fresh(t.tab + (lx >> 1));
+    find_step(t, x, lx, kx, acc, done, kp, lp);
+  }
+  kx = settle_key(t, x, kx);
+}
+
+// Two finds advanced in lockstep so that their dependent loads overlap.
+template <bool FRESH>
+__device__ __forceinline__ void find_root2(const Table& t, uint32_t& xa, uint32_t& la, int64_t& ka, uint32_t& acca,
+                                           uint32_t& xb, uint32_t& lb, int64_t& kb, uint32_t& accb) {
+  bool da = (la >> 1) == xa, db = (lb >> 1) == xb;
+  while (!(da && db)) {
+    int64_t kpa = 0, kpb = 0;
+    uint32_t lpa = 0, lpb = 0;
+    if (!da) load_slot(t.tab + (la >> 1), kpa, lpa);
+    if (!db) load_slot(t.tab + (lb >> 1), kpb, lpb);
+    if (FRESH) {
+      if (!da) lpa = load_link_fresh(t.tab + (la >> 1));
+      if (!db) lpb = load_link_fresh(t.tab + (lb >> 1));
+    }
+    if (!da) find_step(t, xa, la, ka, acca, da, kpa, lpa);
+    if (!db) find_step(t, xb, lb, kb, accb, db, kpb, lpb);
+  }
+  ka = settle_key(t, xa, ka);
+  kb = settle_key(t, xb, kb);
+}
+
+// Compatibility wrapper: (root, parity, key) of slot x with observed link lx.
 template <bool FRESH>
 __device__ __forceinline__ void find_root(const Table& t, uint32_t x, uint32_t lx, int64_t kx, uint32_t& root,
                                           uint32_t& par, int64_t& rkey) {
   uint32_t acc = 0;
-  while (true) {
-    const uint32_t p = lx >> 1;
-    if (p == x) break;
-    int64_t kp;
-    uint32_t lp;
-    load_slot(t.tab + p, kp, lp);
-    if (FRESH) lp = load_link_fresh(t.tab + p);
-    const uint32_t gp = lp >> 1;
-    if (gp == p) {  // parent is the root
-      acc ^= lx & 1u;
-      x = p;
-      kx = kp;
-      break;
-    }
-    const uint32_t nl = (gp << 1) | ((lx ^ lp) & 1u);
-    t.tab[x].link = nl;  // halving: x is a non-root forever, gp is an ancestor
-    acc ^= nl & 1u;
-    x = gp;
-    load_slot(t.tab + gp, kx, lx);
-    if (FRESH) lx = load_link_fresh(t.tab + gp);
-  }
+  find_root1<FRESH>(t, x, lx, kx, acc);
   root = x;
   par = acc;
-  rkey = settle_key(t, x, kx);
+  rkey = kx;
 }
 
 // Hook loop: make a and b one set with colour(a) ^ colour(b) == need (SIGNED).
@@ -170,9 +208,8 @@ template <bool SIGNED, bool TRACK>
 __device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, uint32_t a, uint32_t la, int64_t ka,
                                      uint32_t b, uint32_t lb, int64_t kb, uint32_t need) {
   while (true) {
-    uint32_t pa, pb;
-    find_root<true>(t, a, la, ka, a, pa, ka);
-    find_root<true>(t, b, lb, kb, b, pb, kb);
+    uint32_t pa = 0, pb = 0;
+    find_root2<true>(t, a, la, ka, pa, b, lb, kb, pb);
     la = a << 1;
     lb = b << 1;
     need ^= pa ^ pb;

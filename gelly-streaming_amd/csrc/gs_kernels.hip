@@ -40,14 +40,20 @@ __global__ __launch_bounds__(256) void k_fold(Table t, Lists L, const int64_t* _
   uint32_t need = 0;
   if (SIGNED) need = w ? (w[i] & 1u) : 1u;
 
+  // both first relabel probes in flight together
+  const uint32_t hu = hash_slot(ks, t.shift), hv = hash_slot(kd, t.shift);
+  int64_t k0u, k0v;
+  uint32_t l0u, l0v;
+  load_slot(t.tab + hu, k0u, l0u);
+  load_slot(t.tab + hv, k0v, l0v);
   uint32_t lu, lv;
   bool nu, nv;
-  const uint32_t su = lookup_insert(t, ks, lu, nu);
-  const uint32_t sv = lookup_insert(t, kd, lv, nv);
+  const uint32_t su = lookup_resolve(t, ks, hu, k0u, l0u, lu, nu);
+  const uint32_t sv = lookup_resolve(t, kd, hv, k0v, l0v, lv, nv);
   if (nu || nv) {
-    atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], (nu ? 1u : 0u) + (nv && sv != su ? 1u : 0u));
+    const uint32_t cnt = (nu ? 1u : 0u) + (nv && sv != su ? 1u : 0u);
+    atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], cnt);
     if (TRACK) {
-      const uint32_t cnt = (nu ? 1u : 0u) + (nv && sv != su ? 1u : 0u);
       uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_DELTA + shard)], cnt);
       if (pos + cnt <= L.delta_shard_cap) {
         const size_t o = (size_t)shard * L.delta_shard_cap + pos;
@@ -55,10 +61,9 @@ __global__ __launch_bounds__(256) void k_fold(Table t, Lists L, const int64_t* _
           L.da[o] = ks;
           L.db[o] = ks;
           L.dw[o] = 0;
-          ++pos;
         }
         if (nv && sv != su) {
-          const size_t o2 = (size_t)shard * L.delta_shard_cap + pos;
+          const size_t o2 = o + (nu ? 1 : 0);
           L.da[o2] = kd;
           L.db[o2] = kd;
           L.dw[o2] = 0;
@@ -70,11 +75,21 @@ __global__ __launch_bounds__(256) void k_fold(Table t, Lists L, const int64_t* _
   }
   if (su == kNoSlot || sv == kNoSlot || su == sv) return;  // self-loop: vertex added, never a conflict
 
-  uint32_t ru, rv, pu, pv;
-  int64_t kru, krv;
-  find_root<false>(t, su, lu, ks, ru, pu, kru);
-  find_root<false>(t, sv, lv, kd, rv, pv, krv);
-  need ^= pu ^ pv;
+  // shortcut: a shared parent (the common case once trees are flat) or a direct
+  // parent/child pair decides the edge without touching a root
+  const uint32_t pu = lu >> 1, pv = lv >> 1;
+  if (pu == pv || pu == sv || pv == su) {
+    if (SIGNED) {
+      const uint32_t par = (pu == pv) ? ((lu ^ lv) & 1u) : (pu == sv ? (lu & 1u) : (lv & 1u));
+      if ((need ^ par) & 1u) atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);
+    }
+    return;
+  }
+
+  uint32_t ru = su, rv = sv, pru = 0, prv = 0;
+  int64_t kru = ks, krv = kd;
+  find_root2<false>(t, ru, lu, kru, pru, rv, lv, krv, prv);
+  need ^= pru ^ prv;
   if (ru == rv) {
     if (SIGNED && (need & 1u)) atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);
     return;

@@ -1,0 +1,78 @@
+"""Summarise a tools/rocprof_round.sh output directory into profiles/<tag>_*.{json,md}.
+
+Per kernel: dispatches, average duration (kernel trace), and per-dispatch averages of
+every PMC counter collected in the separate --pmc passes. HBM traffic per k_fold
+launch is derived from FETCH_SIZE/WRITE_SIZE (KiB) with the gfx950 note of
+MI355X_MICROARCH.md (HBM section): FETCH_SIZE tallies 128-B requests at 64 B, i.e.
+reads x2 for wide requests; TCC_EA0_RDREQ gives the request count directly.
+Usage: python tools/rocprof_summary.py gpurun_out/rocprof_r01 r01
+"""
+import glob
+import json
+import os
+import sqlite3
+import sys
+from collections import defaultdict
+
+d, tag = sys.argv[1], sys.argv[2]
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+out = {"tag": tag, "kernels": {}}
+
+
+def short(name):
+    """'void gs::k_fold<false, true, false>(gs::Table, ...)' -> 'k_fold<false, true, false>'."""
+    base = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    tmpl = ""
+    if "<" in base.split("(")[0]:
+        head = base.split("(")[0]
+        tmpl = head[head.index("<"):]
+        base = head[:head.index("<")]
+    else:
+        base = base.split("(")[0]
+    return base.split("::")[-1] + tmpl
+
+
+tr = glob.glob(os.path.join(d, "trace", "*.db"))[0]
+db = sqlite3.connect(tr)
+for name, calls, tot, avg, pct in db.execute("select name,total_calls,total_duration,average,percentage from top_kernels"):
+    out["kernels"].setdefault(short(name), {}).update(
+        {"calls": calls, "total_us": round(tot, 1), "avg_us": round(avg, 3), "pct": round(pct, 2)})
+
+for pdir in sorted(glob.glob(os.path.join(d, "pmc_*"))):
+    dbs = glob.glob(os.path.join(pdir, "*.db"))
+    if not dbs:
+        continue
+    c = sqlite3.connect(dbs[0])
+    agg = defaultdict(lambda: defaultdict(list))
+    for kname, cname, val in c.execute("select kernel_name, counter_name, value from counters_collection"):
+        key = short(kname)
+        agg[key][cname].append(val)
+    for k, cs in agg.items():
+        for cname, vals in cs.items():
+            out["kernels"].setdefault(k, {})["pmc_" + cname] = round(sum(vals) / len(vals), 3)
+
+fold = [k for k in out["kernels"] if k.startswith("k_fold")]
+for k in fold:
+    r = out["kernels"][k]
+    if "pmc_FETCH_SIZE" in r:
+        rd_req = r.get("pmc_TCC_EA0_RDREQ_sum")
+        r["derived"] = {
+            # gfx950: one L2->fabric read request moves 128 B for streaming AND for random
+            # 16-B loads (profiles/r01_calib_random_pmc.json); FETCH_SIZE tallies 64 B each.
+            "hbm_read_bytes": (rd_req * 128) if rd_req else r["pmc_FETCH_SIZE"] * 1024 * 2,
+            "fetch_bytes_raw": r["pmc_FETCH_SIZE"] * 1024,
+            "write_bytes": r.get("pmc_WRITE_SIZE", 0) * 1024,
+            "read_requests": rd_req,
+            "l2_hit_rate": (r["pmc_TCC_HIT_sum"] / (r["pmc_TCC_HIT_sum"] + r["pmc_TCC_MISS_sum"]))
+            if "pmc_TCC_HIT_sum" in r else None,
+        }
+os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
+with open(os.path.join(root, "profiles", "%s_rocprof_summary.json" % tag), "w") as f:
+    json.dump(out, f, indent=1)
+lines = ["# rocprofv3 summary %s" % tag, "", "| kernel | calls | avg us | total us | % | extra |", "|---|---|---|---|---|---|"]
+for k, r in sorted(out["kernels"].items(), key=lambda kv: -kv[1].get("total_us", 0)):
+    extra = ", ".join("%s=%s" % (a[4:], b) for a, b in r.items() if a.startswith("pmc_"))
+    lines.append("| %s | %s | %s | %s | %s | %s |" % (k, r.get("calls"), r.get("avg_us"), r.get("total_us"), r.get("pct"), extra))
+with open(os.path.join(root, "profiles", "%s_rocprof_summary.md" % tag), "w") as f:
+    f.write("\n".join(lines) + "\n")
+print("\n".join(lines))
