@@ -66,8 +66,14 @@ struct gs_summary {
   uint8_t* dw = nullptr;
   uint32_t delta_shard_cap = 0;
   uint64_t delta_fill_ub = 0;  // worst-case per-shard fill since the last take
-  int actset = 0;
-  bool fused = false;
+  // hook policy (DESIGN.md "Kernels"): FUSED hooks in k_fold; DEFER hooks waves
+  // with <= inline_max active edges in place and hands the rest to the next
+  // k_fold launch (triple-buffered active sets); COMPACT runs k_hook per chunk.
+  enum Mode { FUSED = 0, DEFER = 1, COMPACT = 2 } mode = FUSED;
+  int inline_max = 4;
+  int ept = 1;        // edges per k_fold thread
+  uint64_t epoch = 0; // k_fold launches since reset (selects the active set)
+  int pending = -1;   // active set still waiting to be drained
   // staging for host folds
   int64_t* d_stage = nullptr;  // [2][2][kStageChunk]
   uint8_t* d_wstage = nullptr; // [2][kStageChunk]
@@ -82,7 +88,7 @@ struct gs_summary {
     int kid;
     hipEvent_t a, b;
   };
-  std::vector<Pending> pending;
+  std::vector<Pending> prof_pending;
   std::vector<hipEvent_t> ev_pool;
   uint64_t launches[KID_N] = {0, 0, 0, 0};
   double total_ms[KID_N] = {0, 0, 0, 0};
@@ -147,13 +153,13 @@ struct Prof {
     if (h->profiling) {
       hipEvent_t b = take_event(h);
       (void)hipEventRecord(b, h->stream);
-      h->pending.push_back({kid, a, b});
+      h->prof_pending.push_back({kid, a, b});
     }
   }
 };
 
 void drain_profile(gs_summary* h) {
-  for (auto& p : h->pending) {
+  for (auto& p : h->prof_pending) {
     float ms = 0.f;
     if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
       h->launches[p.kid] += 1;
@@ -162,7 +168,7 @@ void drain_profile(gs_summary* h) {
     h->ev_pool.push_back(p.a);
     h->ev_pool.push_back(p.b);
   }
-  h->pending.clear();
+  h->prof_pending.clear();
 }
 
 int check_device_flags(gs_summary* h) {
@@ -204,15 +210,30 @@ int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
   }
   GS_HIP(hipGetLastError());
   h->nv_ub = 0;
-  h->actset = 0;
+  h->epoch = 0;
+  h->pending = -1;
   return GS_OK;
 }
 
 int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
                      size_t stride, bool check_cap = true);
 
+// Hook the deferred active edges (DEFER mode) so the forest is complete.
+int flush_hooks(gs_summary* h) {
+  if (h->pending < 0) return GS_OK;
+  {
+    Prof p(h, KID_HOOK);
+    gs::launch_hook(h->kind == GS_KIND_SIGNED, h->track, h->table(), h->lists(), h->pending, gs::kShards * 16,
+                    h->stream);
+  }
+  GS_HIP(hipGetLastError());
+  h->pending = -1;
+  return GS_OK;
+}
+
 // Export every (vertex, label, parity) into device arrays; returns count.
 int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n) {
+  if (int rc = flush_hooks(h)) return rc;
   GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, h->stream));
   {
     Prof pr(h, KID_EXPORT);
@@ -290,27 +311,34 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
   const bool sign = h->kind == GS_KIND_SIGNED;
   for (size_t off = 0; off < n; off += kMaxChunk) {
     const uint32_t c = (uint32_t)std::min<size_t>(kMaxChunk, n - off);
-    const uint32_t blocks = (c + 255) / 256;
-    const uint32_t per_shard_blocks = (blocks + gs::kShards - 1) / gs::kShards;
+    const uint32_t per_block = 256u * (uint32_t)h->ept;
+    const uint32_t blocks = (c + per_block - 1) / per_block;
+    const uint32_t per_shard_edges = ((blocks + gs::kShards - 1) / gs::kShards) * per_block;
     if (h->track) {
-      h->delta_fill_ub += (uint64_t)per_shard_blocks * 256 * 3;
+      h->delta_fill_ub += (uint64_t)per_shard_edges * 3;
       if (h->delta_fill_ub > h->delta_shard_cap)
         return fail(GS_ERR_CAPACITY, "delta list full: call gs_take_delta_device after each fold of <= 2^22 edges");
     }
+    const int cur = (int)(h->epoch % gs::kActSets);
+    const int zero = (int)((h->epoch + 1) % gs::kActSets);
+    const int inline_max = h->mode == gs_summary::FUSED ? 64 : (h->mode == gs_summary::COMPACT ? 0 : h->inline_max);
+    const int drain = h->mode == gs_summary::DEFER ? h->pending : -1;
     {
       Prof p(h, KID_FOLD);
-      gs::launch_fold(sign, h->fused, h->track, h->table(), h->lists(), src + off * stride, dst + off * stride,
-                      w ? w + off : nullptr, c, (uint32_t)stride, h->actset, h->stream);
+      gs::launch_fold(sign, h->track, h->ept, h->table(), h->lists(), src + off * stride, dst + off * stride,
+                      w ? w + off : nullptr, c, (uint32_t)stride, cur, drain, zero, inline_max, h->stream);
     }
     GS_HIP(hipGetLastError());
-    if (!h->fused) {
-      const int sub = (int)std::min<uint32_t>(per_shard_blocks, 16u);
+    h->epoch++;
+    h->pending = h->mode == gs_summary::FUSED ? -1 : cur;
+    if (h->mode == gs_summary::COMPACT) {
+      const int sub = (int)std::min<uint32_t>((blocks + gs::kShards - 1) / gs::kShards, 16u);
       {
         Prof p(h, KID_HOOK);
-        gs::launch_hook(sign, h->track, h->table(), h->lists(), h->actset, sub, h->stream);
+        gs::launch_hook(sign, h->track, h->table(), h->lists(), cur, gs::kShards * sub, h->stream);
       }
       GS_HIP(hipGetLastError());
-      h->actset ^= 1;
+      h->pending = -1;
     }
   }
   return GS_OK;
@@ -340,9 +368,12 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   gs_summary* h = new gs_summary();
   h->device = device;
   h->kind = kind;
-  // hook inside k_fold (default) or compacted into k_hook (GS_FUSED_HOOK=0)
-  const char* fz = getenv("GS_FUSED_HOOK");
-  h->fused = !(fz && fz[0] == '0');
+  if (const char* m = getenv("GS_HOOK_MODE")) {
+    if (!strcmp(m, "defer")) h->mode = gs_summary::DEFER;
+    if (!strcmp(m, "compact")) h->mode = gs_summary::COMPACT;
+  }
+  if (const char* m = getenv("GS_INLINE_MAX")) h->inline_max = std::max(0, std::min(64, atoi(m)));
+  if (const char* m = getenv("GS_EPT")) h->ept = atoi(m) == 2 ? 2 : 1;
   uint64_t cap = next_pow2(std::max<uint64_t>(2 * std::max<uint64_t>(capacity_hint, 1), 1024));
   if (cap > kMaxCap) cap = kMaxCap;
   int rc = GS_OK;
@@ -355,7 +386,7 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   if (hipMalloc(&h->ctr, gs::CTR_COUNT * gs::kCtrStride * 4) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipMalloc(counters) failed"));
   h->act_shard_cap = ((kMaxChunk / 256 + gs::kShards - 1) / gs::kShards) * 256;
-  if (hipMalloc(&h->act, sizeof(uint2) * 2 * gs::kShards * (size_t)h->act_shard_cap) != hipSuccess)
+  if (hipMalloc(&h->act, sizeof(uint2) * gs::kActSets * gs::kShards * (size_t)h->act_shard_cap) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipMalloc(active list) failed"));
   if (hipMalloc(&h->d_stage, sizeof(int64_t) * 4 * kStageChunk) != hipSuccess ||
       hipMalloc(&h->d_wstage, 2 * kStageChunk) != hipSuccess || hipMalloc(&h->d_scratch, 64) != hipSuccess)
@@ -407,7 +438,8 @@ int gs_reset(gs_handle h) {
   }
   GS_HIP(hipGetLastError());
   h->nv_ub = 0;
-  h->actset = 0;
+  h->epoch = 0;
+  h->pending = -1;
   h->delta_fill_ub = 0;
   return GS_OK;
 }
@@ -455,6 +487,7 @@ int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const ui
 int gs_sync(gs_handle h) {
   if (int rc = check(h)) return rc;
   DeviceGuard g(h->device);
+  if (int rc = flush_hooks(h)) return rc;
   GS_HIP(hipStreamSynchronize(h->stream));
   return check_device_flags(h);
 }
@@ -472,6 +505,7 @@ int gs_find(gs_handle h, int64_t v, int64_t* label, int* found) {
   if (int rc = check(h)) return rc;
   if (!label || !found) return fail(GS_ERR_INVALID, "null output");
   DeviceGuard g(h->device);
+  if (int rc = flush_hooks(h)) return rc;
   gs::launch_find_one(h->table(), v, h->d_scratch, h->stream);
   GS_HIP(hipGetLastError());
   int64_t out[2];
@@ -527,6 +561,7 @@ int gs_bip_status(gs_handle h, int* ok) {
   if (int rc = check(h)) return rc;
   if (!ok) return fail(GS_ERR_INVALID, "ok is null");
   DeviceGuard g(h->device);
+  if (int rc = flush_hooks(h)) return rc;
   uint32_t f = 0;
   GS_HIP(hipMemcpyAsync(&f, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream));
   GS_HIP(hipStreamSynchronize(h->stream));
@@ -668,6 +703,7 @@ int gs_deserialize(gs_handle h, const void* buf, size_t len) {
 int gs_set_delta_tracking(gs_handle h, int on) {
   if (int rc = check(h)) return rc;
   DeviceGuard g(h->device);
+  if (int rc = flush_hooks(h)) return rc;  // deferred hooks belong to the previous tracking state
   if (on && !h->da) {
     // worst case between two takes: one fold chunk of kMaxChunk edges
     h->delta_shard_cap = ((kMaxChunk / 256 + gs::kShards - 1) / gs::kShards) * 256 * 3;
@@ -687,6 +723,7 @@ int gs_take_delta_device(gs_handle h, int64_t* a, int64_t* b, uint8_t* w, size_t
   if (!n) return fail(GS_ERR_INVALID, "n is null");
   if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
   DeviceGuard g(h->device);
+  if (int rc = flush_hooks(h)) return rc;
   std::vector<uint32_t> c(gs::kShards * gs::kCtrStride);
   GS_HIP(hipMemcpyAsync(c.data(), h->ctr + gs::ctr_index(gs::CTR_DELTA), c.size() * 4, hipMemcpyDeviceToHost,
                         h->stream));

@@ -32,12 +32,12 @@ constexpr int64_t kEmpty = INT64_MIN;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 constexpr int kShards = 64;      // sharded append counters (one 128-B line each)
 constexpr int kCtrStride = 32;   // u32 per counter line
+constexpr int kActSets = 3;     // active-edge lists: appended at epoch e, drained at e+1, zeroed at e+2
 enum CounterBlock : int {
   CTR_NV = 0,                    // [kShards] new-vertex counts
-  CTR_ACT0 = kShards,            // [kShards] active-edge counts, set 0
-  CTR_ACT1 = 2 * kShards,        // [kShards] active-edge counts, set 1
-  CTR_DELTA = 3 * kShards,       // [kShards] delta counts
-  CTR_FAIL = 4 * kShards,        // sticky bipartiteness failure
+  CTR_ACT = kShards,             // [kActSets][kShards] active-edge counts
+  CTR_DELTA = (1 + kActSets) * kShards,  // [kShards] delta counts
+  CTR_FAIL = (2 + kActSets) * kShards,   // sticky bipartiteness failure
   CTR_ERR,                       // device-side error (table overflow)
   CTR_EXPORT,                    // export append counter
   CTR_OVF,                       // delta / active list overflow
@@ -60,7 +60,7 @@ struct Table {
 };
 
 struct Lists {
-  uint2* act;            // active (root, root, parity) entries, [2][kShards][act_shard_cap]
+  uint2* act;            // active (root<<1|parity, root) entries, [kActSets][kShards][act_shard_cap]
   uint32_t act_shard_cap;
   int64_t* da;           // delta triples, [kShards][delta_shard_cap]
   int64_t* db;

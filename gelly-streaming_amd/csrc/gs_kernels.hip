@@ -27,99 +27,13 @@ __global__ __launch_bounds__(256) void k_init(Slot* tab, uint64_t nslots) {
   }
 }
 
-template <bool SIGNED, bool FUSED, bool TRACK>
-__global__ __launch_bounds__(256) void k_fold(Table t, Lists L, const int64_t* __restrict__ src,
-                                              const int64_t* __restrict__ dst, const uint8_t* __restrict__ w,
-                                              uint32_t n, uint32_t stride, int actset) {
-  if (SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0) return;
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  const int shard = blockIdx.x & (kShards - 1);
-  if (i >= n) return;
-  const int64_t ks = src[(size_t)i * stride];
-  const int64_t kd = dst[(size_t)i * stride];
-  uint32_t need = 0;
-  if (SIGNED) need = w ? (w[i] & 1u) : 1u;
-
-  // both first relabel probes in flight together
-  const uint32_t hu = hash_slot(ks, t.shift), hv = hash_slot(kd, t.shift);
-  int64_t k0u, k0v;
-  uint32_t l0u, l0v;
-  load_slot(t.tab + hu, k0u, l0u);
-  load_slot(t.tab + hv, k0v, l0v);
-  uint32_t lu, lv;
-  bool nu, nv;
-  const uint32_t su = lookup_resolve(t, ks, hu, k0u, l0u, lu, nu);
-  const uint32_t sv = lookup_resolve(t, kd, hv, k0v, l0v, lv, nv);
-  if (nu || nv) {
-    const uint32_t cnt = (nu ? 1u : 0u) + (nv && sv != su ? 1u : 0u);
-    atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], cnt);
-    if (TRACK) {
-      uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_DELTA + shard)], cnt);
-      if (pos + cnt <= L.delta_shard_cap) {
-        const size_t o = (size_t)shard * L.delta_shard_cap + pos;
-        if (nu) {
-          L.da[o] = ks;
-          L.db[o] = ks;
-          L.dw[o] = 0;
-        }
-        if (nv && sv != su) {
-          const size_t o2 = o + (nu ? 1 : 0);
-          L.da[o2] = kd;
-          L.db[o2] = kd;
-          L.dw[o2] = 0;
-        }
-      } else {
-        atomicOr(&t.ctr[ctr_index(CTR_OVF)], 1u);
-      }
-    }
-  }
-  if (su == kNoSlot || sv == kNoSlot || su == sv) return;  // self-loop: vertex added, never a conflict
-
-  // shortcut: a shared parent (the common case once trees are flat) or a direct
-  // parent/child pair decides the edge without touching a root
-  const uint32_t pu = lu >> 1, pv = lv >> 1;
-  if (pu == pv || pu == sv || pv == su) {
-    if (SIGNED) {
-      const uint32_t par = (pu == pv) ? ((lu ^ lv) & 1u) : (pu == sv ? (lu & 1u) : (lv & 1u));
-      if ((need ^ par) & 1u) atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);
-    }
-    return;
-  }
-
-  uint32_t ru = su, rv = sv, pru = 0, prv = 0;
-  int64_t kru = ks, krv = kd;
-  find_root2<false>(t, ru, lu, kru, pru, rv, lv, krv, prv);
-  need ^= pru ^ prv;
-  if (ru == rv) {
-    if (SIGNED && (need & 1u)) atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);
-    return;
-  }
-  if (FUSED) {
-    hook<SIGNED, TRACK>(t, L, shard, ru, ru << 1, kru, rv, rv << 1, krv, need);
-  } else {
-    const uint32_t pos = atomicAdd(&t.ctr[ctr_index((actset ? CTR_ACT1 : CTR_ACT0) + shard)], 1u);
-    if (pos < L.act_shard_cap) {
-      L.act[((size_t)actset * kShards + shard) * L.act_shard_cap + pos] =
-          make_uint2((ru << 1) | (SIGNED ? (need & 1u) : 0u), rv);
-    } else {
-      atomicOr(&t.ctr[ctr_index(CTR_OVF)], 1u);
-    }
-  }
-}
-
-// grid = kShards * sub blocks; block b drains shard b % kShards of active set `actset`
-// and zeroes the other set's counters (it is free: its k_hook has finished and the
-// next k_fold that uses it has not started -- same-stream order).
+// Hook every entry of one shard slice of active set `set` (entries j = j0, j0+step, ...).
 template <bool SIGNED, bool TRACK>
-__global__ __launch_bounds__(256) void k_hook(Table t, Lists L, int actset, int sub) {
-  const int shard = blockIdx.x & (kShards - 1);
-  const int part = blockIdx.x / kShards;
-  if (blockIdx.x == 0 && threadIdx.x < kShards)
-    t.ctr[ctr_index((actset ? CTR_ACT0 : CTR_ACT1) + threadIdx.x)] = 0u;
-  if (SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0) return;
-  const uint32_t cnt = min(t.ctr[ctr_index((actset ? CTR_ACT1 : CTR_ACT0) + shard)], L.act_shard_cap);
-  const uint2* act = L.act + ((size_t)actset * kShards + shard) * L.act_shard_cap;
-  for (uint32_t j = part * 256u + threadIdx.x; j < cnt; j += (uint32_t)sub * 256u) {
+__device__ __forceinline__ void drain_entries(const Table& t, const Lists& L, int set, int s, uint32_t j0,
+                                              uint32_t step) {
+  const uint32_t cnt = min(t.ctr[ctr_index(CTR_ACT + set * kShards + s)], L.act_shard_cap);
+  const uint2* act = L.act + ((size_t)set * kShards + s) * L.act_shard_cap;
+  for (uint32_t j = j0; j < cnt; j += step) {
     const uint2 e = act[j];
     const uint32_t a = e.x >> 1, b = e.y;
     int64_t ka, kb;
@@ -128,8 +42,151 @@ __global__ __launch_bounds__(256) void k_hook(Table t, Lists L, int actset, int 
     load_slot(t.tab + b, kb, lb);
     la = load_link_fresh(t.tab + a);
     lb = load_link_fresh(t.tab + b);
-    hook<SIGNED, TRACK>(t, L, shard, a, la, settle_key(t, a, ka), b, lb, settle_key(t, b, kb), e.x & 1u);
+    hook<SIGNED, TRACK>(t, L, s, a, la, settle_key(t, a, ka), b, lb, settle_key(t, b, kb), e.x & 1u);
   }
+}
+
+// Drain a whole active set with the current grid (any size).
+template <bool SIGNED, bool TRACK>
+__device__ __forceinline__ void drain_set(const Table& t, const Lists& L, int set) {
+  const uint32_t G = gridDim.x;
+  if (G >= (uint32_t)kShards) {
+    const uint32_t nparts = G / kShards, part = blockIdx.x / kShards;
+    if (part < nparts) drain_entries<SIGNED, TRACK>(t, L, set, blockIdx.x % kShards, part * 256u + threadIdx.x, nparts * 256u);
+  } else {
+    for (uint32_t s = blockIdx.x; s < (uint32_t)kShards; s += G)
+      drain_entries<SIGNED, TRACK>(t, L, set, (int)s, threadIdx.x, 256u);
+  }
+}
+
+// k_fold: EPT edges per thread (edge i = block*256*EPT + e*256 + tid: coalesced).
+// For every edge: both relabel probes issued back to back, shortcut on a shared
+// parent, lockstep finds of the two roots; an edge whose roots differ is hooked
+// in place when its wave has <= a.inline_max such edges, otherwise appended to
+// active set a.cur (drained by the next launch, or by k_hook on a flush).
+// The block also drains its slice of set a.drain and block 0 zeroes set a.zero.
+struct FoldArgs {
+  const int64_t* src;
+  const int64_t* dst;
+  const uint8_t* w;
+  uint32_t n;
+  uint32_t stride;
+  int cur;
+  int drain;
+  int zero;
+  int inline_max;
+};
+
+template <bool SIGNED, bool TRACK, int EPT>
+__global__ __launch_bounds__(256) void k_fold(Table t, Lists L, FoldArgs a) {
+  if (SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0) return;
+  const int shard = blockIdx.x & (kShards - 1);
+  if (a.zero >= 0 && blockIdx.x == 0 && threadIdx.x < kShards)
+    t.ctr[ctr_index(CTR_ACT + a.zero * kShards + threadIdx.x)] = 0u;
+
+  bool valid[EPT], act[EPT];
+  int64_t ks[EPT], kd[EPT];
+  uint32_t need[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const uint32_t i = blockIdx.x * (256u * EPT) + e * 256u + threadIdx.x;
+    valid[e] = i < a.n;
+    act[e] = false;
+    ks[e] = valid[e] ? a.src[(size_t)i * a.stride] : 0;
+    kd[e] = valid[e] ? a.dst[(size_t)i * a.stride] : 0;
+    need[e] = SIGNED ? ((valid[e] && a.w) ? (a.w[i] & 1u) : 1u) : 0u;
+  }
+  // all first relabel probes of the thread in flight together
+  uint32_t hu[EPT], hv[EPT], l0u[EPT], l0v[EPT];
+  int64_t k0u[EPT], k0v[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    hu[e] = hash_slot(ks[e], t.shift);
+    hv[e] = hash_slot(kd[e], t.shift);
+    if (valid[e]) {
+      load_slot(t.tab + hu[e], k0u[e], l0u[e]);
+      load_slot(t.tab + hv[e], k0v[e], l0v[e]);
+    }
+  }
+  uint32_t ru[EPT], rv[EPT], lu[EPT], lv[EPT];
+  int64_t kru[EPT], krv[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    if (!valid[e]) continue;
+    bool nu, nv;
+    const uint32_t su = lookup_resolve(t, ks[e], hu[e], k0u[e], l0u[e], lu[e], nu);
+    const uint32_t sv = lookup_resolve(t, kd[e], hv[e], k0v[e], l0v[e], lv[e], nv);
+    if (nu || nv) {
+      const uint32_t cnt = (nu ? 1u : 0u) + (nv && sv != su ? 1u : 0u);
+      atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], cnt);
+      if (TRACK) {
+        const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_DELTA + shard)], cnt);
+        if (pos + cnt <= L.delta_shard_cap) {
+          const size_t o = (size_t)shard * L.delta_shard_cap + pos;
+          if (nu) {
+            L.da[o] = ks[e];
+            L.db[o] = ks[e];
+            L.dw[o] = 0;
+          }
+          if (nv && sv != su) {
+            const size_t o2 = o + (nu ? 1 : 0);
+            L.da[o2] = kd[e];
+            L.db[o2] = kd[e];
+            L.dw[o2] = 0;
+          }
+        } else {
+          atomicOr(&t.ctr[ctr_index(CTR_OVF)], 1u);
+        }
+      }
+    }
+    ru[e] = su;
+    rv[e] = sv;
+    if (su == kNoSlot || sv == kNoSlot || su == sv) continue;  // self-loop: vertex added, never a conflict
+    // shortcut: shared parent (the common case once trees are flat) or parent/child
+    const uint32_t pu = lu[e] >> 1, pv = lv[e] >> 1;
+    if (pu == pv || pu == sv || pv == su) {
+      if (SIGNED) {
+        const uint32_t par = (pu == pv) ? ((lu[e] ^ lv[e]) & 1u) : (pu == sv ? (lu[e] & 1u) : (lv[e] & 1u));
+        if ((need[e] ^ par) & 1u) atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);
+      }
+      continue;
+    }
+    uint32_t pru = 0, prv = 0;
+    kru[e] = ks[e];
+    krv[e] = kd[e];
+    find_root2<false>(t, ru[e], lu[e], kru[e], pru, rv[e], lv[e], krv[e], prv);
+    need[e] ^= pru ^ prv;
+    if (ru[e] == rv[e]) {
+      if (SIGNED && (need[e] & 1u)) atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);
+      continue;
+    }
+    act[e] = true;
+  }
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const unsigned long long m = __ballot(act[e]);
+    const bool in_place = __popcll(m) <= (unsigned)a.inline_max;
+    if (!act[e]) continue;
+    if (in_place) {
+      hook<SIGNED, TRACK>(t, L, shard, ru[e], ru[e] << 1, kru[e], rv[e], rv[e] << 1, krv[e], need[e]);
+    } else {
+      const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_ACT + a.cur * kShards + shard)], 1u);
+      if (pos < L.act_shard_cap) {
+        L.act[((size_t)a.cur * kShards + shard) * L.act_shard_cap + pos] =
+            make_uint2((ru[e] << 1) | (SIGNED ? (need[e] & 1u) : 0u), rv[e]);
+      } else {
+        atomicOr(&t.ctr[ctr_index(CTR_OVF)], 1u);
+      }
+    }
+  }
+  if (a.drain >= 0) drain_set<SIGNED, TRACK>(t, L, a.drain);
+}
+
+// Flush / compacted mode: drain active set `set` with a dedicated launch.
+template <bool SIGNED, bool TRACK>
+__global__ __launch_bounds__(256) void k_hook(Table t, Lists L, int set) {
+  if (SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0) return;
+  drain_set<SIGNED, TRACK>(t, L, set);
 }
 
 // Export (vertex, label, parity) of every occupied slot. Each thread owns 16 slots
@@ -258,31 +315,34 @@ void launch_init(Slot* tab, uint64_t nslots, hipStream_t st) {
   hipLaunchKernelGGL(k_init, dim3(g), dim3(256), 0, st, tab, nslots);
 }
 
-void launch_fold(bool sign, bool fused, bool track, const Table& t, const Lists& L, const int64_t* src,
-                 const int64_t* dst, const uint8_t* w, uint32_t n, uint32_t stride, int actset, hipStream_t st) {
-  const dim3 g((n + 255) / 256), b(256);
-#define GS_FOLD(S, F, T)                                                                         \
-  if (sign == S && fused == F && track == T) {                                                   \
-    hipLaunchKernelGGL((k_fold<S, F, T>), g, b, 0, st, t, L, src, dst, w, n, stride, actset);    \
-    return;                                                                                      \
+void launch_fold(bool sign, bool track, int ept, const Table& t, const Lists& L, const int64_t* src,
+                 const int64_t* dst, const uint8_t* w, uint32_t n, uint32_t stride, int cur, int drain, int zero,
+                 int inline_max, hipStream_t st) {
+  FoldArgs a{src, dst, w, n, stride, cur, drain, zero, inline_max};
+  const uint32_t per_block = 256u * (uint32_t)ept;
+  const dim3 g((n + per_block - 1) / per_block), b(256);
+#define GS_FOLD(S, T, E)                                                          \
+  if (sign == S && track == T && ept == E) {                                      \
+    hipLaunchKernelGGL((k_fold<S, T, E>), g, b, 0, st, t, L, a);                  \
+    return;                                                                       \
   }
-  GS_FOLD(false, false, false)
-  GS_FOLD(false, false, true)
-  GS_FOLD(false, true, false)
-  GS_FOLD(false, true, true)
-  GS_FOLD(true, false, false)
-  GS_FOLD(true, false, true)
-  GS_FOLD(true, true, false)
-  GS_FOLD(true, true, true)
+  GS_FOLD(false, false, 1)
+  GS_FOLD(false, true, 1)
+  GS_FOLD(true, false, 1)
+  GS_FOLD(true, true, 1)
+  GS_FOLD(false, false, 2)
+  GS_FOLD(false, true, 2)
+  GS_FOLD(true, false, 2)
+  GS_FOLD(true, true, 2)
 #undef GS_FOLD
 }
 
-void launch_hook(bool sign, bool track, const Table& t, const Lists& L, int actset, int sub, hipStream_t st) {
-  const dim3 g(kShards * sub), b(256);
-  if (!sign && !track) hipLaunchKernelGGL((k_hook<false, false>), g, b, 0, st, t, L, actset, sub);
-  if (!sign && track) hipLaunchKernelGGL((k_hook<false, true>), g, b, 0, st, t, L, actset, sub);
-  if (sign && !track) hipLaunchKernelGGL((k_hook<true, false>), g, b, 0, st, t, L, actset, sub);
-  if (sign && track) hipLaunchKernelGGL((k_hook<true, true>), g, b, 0, st, t, L, actset, sub);
+void launch_hook(bool sign, bool track, const Table& t, const Lists& L, int set, int blocks, hipStream_t st) {
+  const dim3 g(blocks), b(256);
+  if (!sign && !track) hipLaunchKernelGGL((k_hook<false, false>), g, b, 0, st, t, L, set);
+  if (!sign && track) hipLaunchKernelGGL((k_hook<false, true>), g, b, 0, st, t, L, set);
+  if (sign && !track) hipLaunchKernelGGL((k_hook<true, false>), g, b, 0, st, t, L, set);
+  if (sign && track) hipLaunchKernelGGL((k_hook<true, true>), g, b, 0, st, t, L, set);
 }
 
 void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, hipStream_t st) {

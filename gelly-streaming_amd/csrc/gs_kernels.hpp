@@ -8,9 +8,14 @@
 namespace gs {
 
 void launch_init(Slot* tab, uint64_t nslots, hipStream_t st);
-void launch_fold(bool sign, bool fused, bool track, const Table& t, const Lists& L, const int64_t* src,
-                 const int64_t* dst, const uint8_t* w, uint32_t n, uint32_t stride, int actset, hipStream_t st);
-void launch_hook(bool sign, bool track, const Table& t, const Lists& L, int actset, int sub, hipStream_t st);
+// inline_max: an edge whose roots differ is hooked inside k_fold when its wave has
+// <= inline_max such edges (64: always), else appended to active set `cur`.
+// drain: active set hooked by this launch too (-1: none); zero: set whose counters
+// this launch resets (-1: none).
+void launch_fold(bool sign, bool track, int ept, const Table& t, const Lists& L, const int64_t* src,
+                 const int64_t* dst, const uint8_t* w, uint32_t n, uint32_t stride, int cur, int drain, int zero,
+                 int inline_max, hipStream_t st);
+void launch_hook(bool sign, bool track, const Table& t, const Lists& L, int set, int blocks, hipStream_t st);
 void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out,
                    hipStream_t st);
 void launch_pack(const Table& t, const Lists& L, int64_t* oa, int64_t* ob, uint8_t* ow, uint64_t cap_out, int sub,

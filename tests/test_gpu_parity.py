@@ -323,3 +323,28 @@ def test_gpu_generators_match_oracle(gs, oracle_mod):
     torch.cuda.synchronize()
     os_, od = oracle_mod.er_edges(0x5EED00E5, 22, 777, n, True)
     assert np.array_equal(s.cpu().numpy(), os_) and np.array_equal(d.cpu().numpy(), od)
+
+
+# ------------------------------------------------------------- hook policies / kernel variants
+@pytest.mark.parametrize("mode,inline_max,ept", [("fused", "64", "1"), ("fused", "64", "2"), ("defer", "0", "1"),
+                                                  ("defer", "4", "2"), ("compact", "0", "1")])
+def test_hook_policies_agree(gs, oracle_mod, monkeypatch, mode, inline_max, ept):
+    monkeypatch.setenv("GS_HOOK_MODE", mode)
+    monkeypatch.setenv("GS_INLINE_MAX", inline_max)
+    monkeypatch.setenv("GS_EPT", ept)
+    s, d = oracle_mod.rmat_edges(0x5EED0016, 16, 0, 1 << 19, True)
+    with gs.Summary("cc", capacity_hint=1 << 16) as ds:
+        for i in range(0, len(s), 1 << 15):
+            ds.fold(s[i:i + (1 << 15)], d[i:i + (1 << 15)])
+        _assert_cc_equal(ds, oracle_mod, s, d)
+    rng = np.random.default_rng(8)
+    for trial in range(6):
+        n = int(rng.integers(50, 3000))
+        m = int(rng.integers(10, 5000))
+        bs = rng.integers(-n, n, m)
+        bd = rng.integers(-n, n, m)
+        with gs.Summary("signed", capacity_hint=256) as c:
+            for i in range(0, m, 997):
+                c.fold(bs[i:i + 997], bd[i:i + 997])
+            truth = oracle_mod.canonical_candidates_string(*oracle_mod.bip_truth(bs, bd))
+            assert oracle_mod.canonical_candidates_string(*c.colouring()) == truth
