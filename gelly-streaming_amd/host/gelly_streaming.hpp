@@ -1,0 +1,505 @@
+// gelly_streaming.hpp -- C++ host mirror of gelly-streaming's summary-aggregation API,
+// backed by the MI355X C ABI (include/gs_summary.h).
+//
+// The reference is Java 8 / Flink 1.8 (pom.xml:15-17) and no JVM exists in this
+// image, so the host side above the C ABI is C++ with the reference's names,
+// argument meanings and error behaviour (exceptions where Java throws):
+//
+//   EdgesFold<K,EV,T>           EdgesFold.java:33-47
+//   SummaryAggregation          SummaryAggregation.java:36-136 (fold/combine/transform/
+//                               initial value/transient contract + Merger)
+//   SummaryBulkAggregation      SummaryBulkAggregation.java:44-131 (run(): partition tag ->
+//                               keyed window fold -> all-window reduce -> Merger)
+//   SimpleEdgeStream::aggregate SimpleEdgeStream.java:100-102
+//   DisjointSet                 summaries/DisjointSet.java:25-151  (GPU-resident forest)
+//   Candidates                  summaries/Candidates.java:27-196   (GPU-resident signed forest)
+//   ConnectedComponents         library/ConnectedComponents.java:41-134
+//   BipartitenessCheck          library/BipartitenessCheck.java:37-133
+//
+// Summaries are held by std::shared_ptr (Java object references). A GPU-backed
+// summary buffers its per-edge callbacks (union / merge of a one-edge candidate)
+// and flushes them to the device as one micro-batch on any read, combine or
+// serialization -- the drop-in design of INTEGRATION.md.
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "gs_summary.h"
+
+namespace gelly {
+
+struct NullValue {};
+
+class GsException : public std::runtime_error {
+ public:
+  GsException(int code, const std::string& what) : std::runtime_error(what), code_(code) {}
+  int code() const { return code_; }
+
+ private:
+  int code_;
+};
+
+inline void gs_check(int rc) {
+  if (rc != GS_OK) throw GsException(rc, std::string("gs: ") + gs_last_error());
+}
+
+// Edge<K, EV> is a Tuple3 (f0 = source, f1 = target, f2 = value).
+template <typename K, typename EV>
+struct Edge {
+  K f0;
+  K f1;
+  EV f2;
+  K getSource() const { return f0; }
+  K getTarget() const { return f1; }
+  EV getValue() const { return f2; }
+};
+
+// EdgesFold.java:47 -- T foldEdges(T accum, K vertexID, K neighborID, EV edgeValue)
+template <typename K, typename EV, typename T>
+struct EdgesFold {
+  virtual ~EdgesFold() = default;
+  virtual T foldEdges(T accum, K vertexID, K neighborID, EV edgeValue) = 0;
+};
+
+// Flink ReduceFunction<S> / MapFunction<S, T>
+template <typename S>
+struct ReduceFunction {
+  virtual ~ReduceFunction() = default;
+  virtual S reduce(S value1, S value2) = 0;
+};
+template <typename S, typename T>
+struct MapFunction {
+  virtual ~MapFunction() = default;
+  virtual T map(S value) = 0;
+};
+
+// --------------------------------------------------------------------------
+// GPU-resident summaries
+// --------------------------------------------------------------------------
+class GpuSummary {
+ public:
+  GpuSummary(int kind, int device, uint64_t capacity_hint, size_t flush_edges)
+      : kind_(kind), device_(device), flush_edges_(flush_edges) {
+    gs_check(gs_create(&h_, device, kind, capacity_hint));
+  }
+  virtual ~GpuSummary() {
+    if (h_) gs_destroy(h_);
+  }
+  GpuSummary(const GpuSummary&) = delete;
+  GpuSummary& operator=(const GpuSummary&) = delete;
+
+  // push one buffered edge (flushes a full micro-batch)
+  void push(int64_t u, int64_t v) {
+    src_.push_back(u);
+    dst_.push_back(v);
+    if (src_.size() >= flush_edges_) flush();
+  }
+  void flush() {
+    if (src_.empty()) return;
+    gs_check(gs_fold(h_, src_.data(), dst_.data(), src_.size()));
+    src_.clear();
+    dst_.clear();
+  }
+  gs_handle handle() {
+    flush();
+    return h_;
+  }
+  size_t size() {
+    uint64_t n = 0;
+    gs_check(gs_num_vertices(handle(), &n));
+    return (size_t)n;
+  }
+  void reset() {
+    src_.clear();
+    dst_.clear();
+    gs_check(gs_reset(h_));
+  }
+  // all (vertex, canonical label, parity) rows, sorted by vertex
+  struct Row {
+    int64_t v, label;
+    uint8_t parity;
+  };
+  std::vector<Row> rows() {
+    gs_handle h = handle();
+    uint64_t n = 0;
+    gs_check(gs_num_vertices(h, &n));
+    std::vector<int64_t> v(n), l(n);
+    std::vector<uint8_t> s(n);
+    size_t got = 0;
+    if (kind_ == GS_KIND_SIGNED) {
+      int ok = 1;
+      gs_check(gs_bip_status(h, &ok));
+      if (!ok) return {};
+      gs_check(gs_export_colouring(h, l.data(), v.data(), s.data(), n, &got));
+    } else {
+      gs_check(gs_export_labels(h, v.data(), l.data(), n, &got));
+    }
+    std::vector<Row> r(got);
+    for (size_t i = 0; i < got; ++i) r[i] = {v[i], l[i], (uint8_t)(kind_ == GS_KIND_SIGNED ? s[i] : 0)};
+    std::sort(r.begin(), r.end(), [](const Row& a, const Row& b) { return a.v < b.v; });
+    return r;
+  }
+  std::vector<uint8_t> serialize() {
+    size_t len = 0;
+    gs_check(gs_serialize(handle(), nullptr, 0, &len));
+    std::vector<uint8_t> buf(len);
+    gs_check(gs_serialize(h_, buf.data(), len, &len));
+    buf.resize(len);
+    return buf;
+  }
+  void deserialize(const std::vector<uint8_t>& buf) {
+    src_.clear();
+    dst_.clear();
+    gs_check(gs_deserialize(h_, buf.data(), buf.size()));
+  }
+  int device() const { return device_; }
+
+ protected:
+  int kind_;
+  int device_;
+  size_t flush_edges_;
+  gs_handle h_ = nullptr;
+  std::vector<int64_t> src_, dst_;
+};
+
+// DisjointSet<Long> (DisjointSet.java:25-151) over the GPU forest. find() returns
+// the canonical representative (minimum id of the component): the reference
+// returns an arbitrary member as root (:66-80); every caller only compares roots
+// for equality or prints components, which the canonical choice preserves.
+class DisjointSet : public GpuSummary {
+ public:
+  explicit DisjointSet(int device = 0, uint64_t capacity_hint = 1 << 16, size_t flush_edges = 1 << 20)
+      : GpuSummary(GS_KIND_CC, device, capacity_hint, flush_edges) {}
+
+  void makeSet(int64_t e) { push(e, e); }               // :53-56
+  void union_(int64_t e1, int64_t e2) { push(e1, e2); }  // :92-118 ("union" is a C++ keyword)
+  std::optional<int64_t> find(int64_t e) {               // :66-80 (null -> nullopt)
+    int64_t label = 0;
+    int found = 0;
+    gs_check(gs_find(handle(), e, &label, &found));
+    if (!found) return std::nullopt;
+    return label;
+  }
+  void merge(DisjointSet& other) {  // :127-131
+    if (&other == this) return;
+    gs_check(gs_combine(handle(), other.handle()));
+  }
+  // getMatches() (:44-46) as (vertex, representative) pairs
+  std::vector<std::pair<int64_t, int64_t>> getMatches() {
+    std::vector<std::pair<int64_t, int64_t>> m;
+    for (const Row& r : rows()) m.push_back({r.v, r.label});
+    return m;
+  }
+  // toString() (:134-150): "{root=[members], ...}", components keyed by their
+  // minimum id, members ascending (the reference prints HashMap order).
+  std::string toString() {
+    std::map<int64_t, std::vector<int64_t>> comps;
+    for (const Row& r : rows()) comps[r.label].push_back(r.v);
+    std::string s = "{";
+    bool first = true;
+    for (auto& kv : comps) {
+      if (!first) s += ", ";
+      first = false;
+      s += std::to_string(kv.first) + "=[";
+      for (size_t i = 0; i < kv.second.size(); ++i) s += (i ? ", " : "") + std::to_string(kv.second[i]);
+      s += "]";
+    }
+    return s + "}";
+  }
+};
+
+// Candidates (Candidates.java:27-196) over the GPU signed forest. A one-edge
+// candidate (BipartitenessCheck.edgeToCandidate, :54-61) is a host-only value
+// that merge() buffers; merging two GPU summaries runs gs_combine.
+class Candidates : public GpuSummary {
+ public:
+  struct EdgeCandidate {  // {min(u,v): {min: +, max: -}}
+    int64_t u, v;
+  };
+  explicit Candidates(bool success = true, int device = 0, uint64_t capacity_hint = 1 << 16,
+                      size_t flush_edges = 1 << 20)
+      : GpuSummary(GS_KIND_SIGNED, device, capacity_hint, flush_edges) {
+    if (!success) fail();
+  }
+  bool getSuccess() {  // :44-46
+    int ok = 1;
+    gs_check(gs_bip_status(handle(), &ok));
+    return ok != 0;
+  }
+  // :77-139: merge(input) with input = one edge (the fold) ...
+  Candidates& merge(const EdgeCandidate& e) {
+    push(e.u, e.v);
+    return *this;
+  }
+  // ... or another summary (the combine); the verdict is the AND.
+  Candidates& merge(Candidates& input) {
+    if (&input != this) gs_check(gs_combine(handle(), input.handle()));
+    return *this;
+  }
+  // getMap() (:48-50): component (min id) -> {vertex -> sign}
+  std::map<int64_t, std::map<int64_t, bool>> getMap() {
+    std::map<int64_t, std::map<int64_t, bool>> m;
+    for (const Row& r : rows()) m[r.label][r.v] = r.parity != 0;
+    return m;
+  }
+  // Tuple2.toString(): "(true,{1={1=(1,true), 2=(2,false)}, ...})" / "(false,{})"
+  std::string toString() {
+    const bool ok = getSuccess();
+    std::string s = std::string("(") + (ok ? "true" : "false") + ",{";
+    if (ok) {
+      bool first = true;
+      for (auto& c : getMap()) {
+        if (!first) s += ", ";
+        first = false;
+        s += std::to_string(c.first) + "={";
+        bool f2 = true;
+        for (auto& v : c.second) {
+          if (!f2) s += ", ";
+          f2 = false;
+          s += std::to_string(v.first) + "=(" + std::to_string(v.first) + "," + (v.second ? "true" : "false") + ")";
+        }
+        s += "}";
+      }
+    }
+    return s + "})";
+  }
+
+ private:
+  // :194-196 fail() == new Candidates(false): load the serialized image of a failed,
+  // empty summary (header only: magic 'GSS1', kind, ok = 0, n = 0).
+  void fail() {
+    std::vector<uint8_t> img(24, 0);
+    const uint32_t hdr[4] = {0x31535347u, (uint32_t)GS_KIND_SIGNED, 0u, 0u};
+    std::memcpy(img.data(), hdr, 16);
+    deserialize(img);
+  }
+};
+
+// --------------------------------------------------------------------------
+// Operators
+// --------------------------------------------------------------------------
+// SummaryAggregation<K, EV, S, T> (SummaryAggregation.java:36-91)
+template <typename K, typename EV, typename S, typename T>
+class SummaryAggregation {
+ public:
+  using Fold = EdgesFold<K, EV, S>;
+  using Combine = ReduceFunction<S>;
+  using Transform = MapFunction<S, T>;
+  using Factory = std::function<S()>;  // the initial value (Flink copies it per window)
+
+  SummaryAggregation(std::shared_ptr<Fold> updateFun, std::shared_ptr<Combine> combineFun,
+                     std::shared_ptr<Transform> transform, Factory initialValue, bool transientState)
+      : updateFun_(std::move(updateFun)),
+        combineFun_(std::move(combineFun)),
+        transform_(std::move(transform)),
+        initialValue_(std::move(initialValue)),
+        transientState_(transientState) {}
+  virtual ~SummaryAggregation() = default;
+
+  std::shared_ptr<Combine> getCombineFun() const { return combineFun_; }
+  std::shared_ptr<Fold> getUpdateFun() const { return updateFun_; }
+  std::shared_ptr<Transform> getTransform() const { return transform_; }
+  bool isTransientState() const { return transientState_; }
+  S getInitialValue() const { return initialValue_(); }
+
+  // Merger (SummaryAggregation.java:93-136): running combine at parallelism 1.
+  class Merger {
+   public:
+    Merger(Factory initialVal, std::shared_ptr<Combine> combiner, bool transientState)
+        : initialVal_(std::move(initialVal)), combiner_(std::move(combiner)), transientState_(transientState) {
+      summary_ = initialVal_();
+    }
+    // flatMap (:107-119): summary = combine.reduce(s, summary); emit; reset if transient
+    S flatMap(S s) {
+      if (!combiner_) return s;
+      summary_ = combiner_->reduce(s, summary_);
+      S out = summary_;
+      if (transientState_) summary_ = initialVal_();
+      return out;
+    }
+    // snapshotState / restoreState (:127-135) through the summary's serializer
+    S snapshotState() { return summary_; }
+    void restoreState(S s) { summary_ = std::move(s); }
+
+   private:
+    Factory initialVal_;
+    std::shared_ptr<Combine> combiner_;
+    bool transientState_;
+    S summary_;
+  };
+
+ protected:
+  std::shared_ptr<Fold> updateFun_;
+  std::shared_ptr<Combine> combineFun_;
+  std::shared_ptr<Transform> transform_;
+  Factory initialValue_;
+  bool transientState_;
+};
+
+// A bounded, timestamped edge stream with a source parallelism: the stand-in for
+// DataStream<Edge<K, EV>> (SimpleEdgeStream.java:69-90). Edges are dealt to the p
+// fold subtasks round-robin (a rebalanced parallelism-1 source).
+template <typename K, typename EV>
+struct EdgeStream {
+  std::vector<Edge<K, EV>> edges;
+  std::vector<int64_t> timestamps;  // event/ingestion time in ms (empty: all 0)
+  int parallelism = 1;
+};
+
+// SummaryBulkAggregation (SummaryBulkAggregation.java:44-131)
+template <typename K, typename EV, typename S, typename T>
+class SummaryBulkAggregation : public SummaryAggregation<K, EV, S, T> {
+  using Base = SummaryAggregation<K, EV, S, T>;
+
+ public:
+  SummaryBulkAggregation(std::shared_ptr<typename Base::Fold> updateFun,
+                         std::shared_ptr<typename Base::Combine> combineFun,
+                         std::shared_ptr<typename Base::Transform> transformFun, typename Base::Factory initialVal,
+                         int64_t timeMillis, bool transientState)
+      : Base(std::move(updateFun), std::move(combineFun), std::move(transformFun), std::move(initialVal),
+             transientState),
+        timeMillis_(timeMillis) {}
+  SummaryBulkAggregation(std::shared_ptr<typename Base::Fold> updateFun,
+                         std::shared_ptr<typename Base::Combine> combineFun, typename Base::Factory initialVal,
+                         int64_t timeMillis, bool transientState)
+      : SummaryBulkAggregation(std::move(updateFun), std::move(combineFun), nullptr, std::move(initialVal),
+                               timeMillis, transientState) {}
+
+  // run (:68-90): PartitionMapper -> keyBy(partition).timeWindow(t).fold(initial,
+  // PartialAgg) -> timeWindowAll(t).reduce(combine) -> Merger -> (transform).
+  // Returns every emission in order (one per window that holds edges).
+  std::vector<T> run(const EdgeStream<K, EV>& stream) {
+    const size_t n = stream.edges.size();
+    const int p = std::max(1, stream.parallelism);
+    typename Base::Merger merger(this->initialValue_, this->combineFun_, this->transientState_);
+    std::vector<T> out;
+    size_t i = 0;
+    while (i < n) {
+      const int64_t w = window_of(stream, i);
+      size_t j = i;
+      while (j < n && window_of(stream, j) == w) ++j;
+      std::vector<S> partial(p);  // per-(partition, window) fold state
+      for (size_t k = i; k < j; ++k) {
+        const int part = (int)(k % (size_t)p);  // PartitionMapper.map (:103-105)
+        if (!partial[part]) partial[part] = this->getInitialValue();
+        const Edge<K, EV>& e = stream.edges[k];
+        partial[part] = this->updateFun_->foldEdges(partial[part], e.getSource(), e.getTarget(), e.getValue());
+      }
+      S acc{};
+      for (int q = 0; q < p; ++q) {  // timeWindowAll reduce, arrival order = partition order
+        if (!partial[q]) continue;
+        acc = acc ? this->combineFun_->reduce(acc, partial[q]) : partial[q];
+      }
+      S emitted = merger.flatMap(acc);
+      out.push_back(emit(emitted));
+      i = j;
+    }
+    return out;
+  }
+
+ private:
+  int64_t window_of(const EdgeStream<K, EV>& s, size_t i) const {
+    const int64_t ts = s.timestamps.empty() ? 0 : s.timestamps[i];
+    return timeMillis_ > 0 ? ts / timeMillis_ : 0;
+  }
+  T emit(S s) {
+    if constexpr (std::is_same<S, T>::value) {
+      if (!this->transform_) return s;
+    }
+    return this->transform_->map(s);
+  }
+  int64_t timeMillis_;
+};
+
+// SimpleEdgeStream.aggregate (SimpleEdgeStream.java:100-102)
+template <typename K, typename EV>
+class SimpleEdgeStream {
+ public:
+  explicit SimpleEdgeStream(EdgeStream<K, EV> edges) : edges_(std::move(edges)) {}
+  template <typename S, typename T>
+  std::vector<T> aggregate(SummaryBulkAggregation<K, EV, S, T>& summaryAggregation) {
+    return summaryAggregation.run(edges_);
+  }
+
+ private:
+  EdgeStream<K, EV> edges_;
+};
+
+// --------------------------------------------------------------------------
+// Library algorithms
+// --------------------------------------------------------------------------
+using DisjointSetRef = std::shared_ptr<DisjointSet>;
+using CandidatesRef = std::shared_ptr<Candidates>;
+
+// ConnectedComponents<K, EV> (ConnectedComponents.java:41-134)
+template <typename EV = NullValue>
+class ConnectedComponents : public SummaryBulkAggregation<int64_t, EV, DisjointSetRef, DisjointSetRef> {
+  using Base = SummaryBulkAggregation<int64_t, EV, DisjointSetRef, DisjointSetRef>;
+
+ public:
+  // UpdateCC.foldEdges (:83-86): ds.union(vertex, vertex2); return ds
+  struct UpdateCC : EdgesFold<int64_t, EV, DisjointSetRef> {
+    DisjointSetRef foldEdges(DisjointSetRef ds, int64_t vertex, int64_t vertex2, EV) override {
+      ds->union_(vertex, vertex2);
+      return ds;
+    }
+  };
+  // CombineCC.reduce (:116-126): merge the smaller into the larger
+  struct CombineCC : ReduceFunction<DisjointSetRef> {
+    DisjointSetRef reduce(DisjointSetRef s1, DisjointSetRef s2) override {
+      if (s1->size() <= s2->size()) {
+        s2->merge(*s1);
+        return s2;
+      }
+      s1->merge(*s2);
+      return s1;
+    }
+  };
+  // ConnectedComponents(long mergeWindowTime) (:52-54); device/capacity are the GPU knobs
+  explicit ConnectedComponents(int64_t mergeWindowTime, int device = 0, uint64_t capacity_hint = 1 << 16)
+      : Base(std::make_shared<UpdateCC>(), std::make_shared<CombineCC>(),
+             [device, capacity_hint] { return std::make_shared<DisjointSet>(device, capacity_hint); },
+             mergeWindowTime, false) {}
+};
+
+// BipartitenessCheck<K, EV> (BipartitenessCheck.java:37-133)
+template <typename EV = NullValue>
+class BipartitenessCheck : public SummaryBulkAggregation<int64_t, EV, CandidatesRef, CandidatesRef> {
+  using Base = SummaryBulkAggregation<int64_t, EV, CandidatesRef, CandidatesRef>;
+
+ public:
+  // edgeToCandidate (:54-61)
+  static Candidates::EdgeCandidate edgeToCandidate(int64_t v1, int64_t v2) {
+    return {std::min(v1, v2), std::max(v1, v2)};
+  }
+  // updateFunction.foldEdges (:93-95): candidates.merge(edgeToCandidate(v1, v2))
+  struct updateFunction : EdgesFold<int64_t, EV, CandidatesRef> {
+    CandidatesRef foldEdges(CandidatesRef candidates, int64_t v1, int64_t v2, EV) override {
+      candidates->merge(edgeToCandidate(v1, v2));
+      return candidates;
+    }
+  };
+  // combineFunction.reduce (:128-130): c1.merge(c2)
+  struct combineFunction : ReduceFunction<CandidatesRef> {
+    CandidatesRef reduce(CandidatesRef c1, CandidatesRef c2) override {
+      c1->merge(*c2);
+      return c1;
+    }
+  };
+  explicit BipartitenessCheck(int64_t mergeWindowTime, int device = 0, uint64_t capacity_hint = 1 << 16)
+      : Base(std::make_shared<updateFunction>(), std::make_shared<combineFunction>(),
+             [device, capacity_hint] { return std::make_shared<Candidates>(true, device, capacity_hint); },
+             mergeWindowTime, false) {}
+};
+
+}  // namespace gelly

@@ -1,0 +1,146 @@
+// The reference's hot-path JUnit tests, restated against the C++ host mirror on the
+// GPU (gelly-streaming_amd/host/gelly_streaming.hpp -> libgs_summary.so):
+//   ConnectedComponentsTest.test      (example/test/ConnectedComponentsTest.java:25-47)
+//   BipartitenessCheckTest.testBipartite / testNonBipartite (BipartitenessCheckTest.java:24-67)
+//   DisjointSetTest.testGetMatches / testFind / testMerge   (util/DisjointSetTest.java:30-77)
+// plus the Merger checkpoint round trip (SummaryAggregation.java:127-135).
+// Prints "PASS <name>" / "FAIL <name>: <why>"; exit status = number of failures.
+#include <algorithm>
+#include <cstdio>
+#include <set>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "gelly_streaming.hpp"
+
+using namespace gelly;
+
+static int failures = 0;
+#define CHECK(name, cond, why)                                      \
+  do {                                                              \
+    if (!(cond)) {                                                  \
+      std::printf("FAIL %s: %s\n", name, std::string(why).c_str()); \
+      ++failures;                                                   \
+      return;                                                       \
+    }                                                               \
+  } while (0)
+
+static EdgeStream<int64_t, NullValue> stream_of(const std::vector<std::pair<int64_t, int64_t>>& es) {
+  EdgeStream<int64_t, NullValue> s;
+  for (auto& e : es) s.edges.push_back({e.first, e.second, NullValue{}});
+  return s;
+}
+
+// ConnectedComponentsTest.parser (:65-81): last emission, split on '=', keep '[...]'
+static std::vector<std::string> parser(const std::vector<std::string>& list) {
+  const std::string& r = list.back();
+  std::vector<std::string> out;
+  std::stringstream ss(r);
+  std::string g;
+  while (std::getline(ss, g, '=')) {
+    if (g.find('[') != std::string::npos) {
+      std::string k = g.substr(0, g.find(']'));
+      out.push_back(k.substr(1));
+    }
+  }
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+static void connected_components_test() {
+  SimpleEdgeStream<int64_t, NullValue> graph(stream_of({{1, 2}, {1, 3}, {2, 3}, {1, 5}, {6, 7}, {8, 9}}));
+  ConnectedComponents<NullValue> cc(5);
+  std::vector<std::string> values;
+  for (auto& ds : graph.aggregate(cc)) values.push_back(ds->toString());  // CollectSink
+  const std::vector<std::string> expected = {"1, 2, 3, 5", "6, 7", "8, 9"};
+  CHECK("ConnectedComponentsTest.test", parser(values) == expected, values.back());
+  std::printf("PASS ConnectedComponentsTest.test\n");
+}
+
+static void connected_components_test_parallel_windows() {
+  // same stream, p = 3 fold subtasks and 2 ms windows (more than one emission)
+  auto s = stream_of({{1, 2}, {1, 3}, {2, 3}, {1, 5}, {6, 7}, {8, 9}});
+  s.parallelism = 3;
+  s.timestamps = {0, 1, 2, 3, 4, 5};
+  SimpleEdgeStream<int64_t, NullValue> graph(s);
+  ConnectedComponents<NullValue> cc(2);
+  std::vector<std::string> values;
+  for (auto& ds : graph.aggregate(cc)) values.push_back(ds->toString());
+  CHECK("ConnectedComponentsTest.parallel", values.size() == 3, std::to_string(values.size()));
+  CHECK("ConnectedComponentsTest.parallel", parser(values) == std::vector<std::string>({"1, 2, 3, 5", "6, 7", "8, 9"}),
+        values.back());
+  std::printf("PASS ConnectedComponentsTest.parallel\n");
+}
+
+static void bipartite_test() {
+  SimpleEdgeStream<int64_t, NullValue> graph(stream_of({{1, 2}, {1, 3}, {1, 4}, {4, 5}, {4, 7}, {4, 9}}));
+  BipartitenessCheck<NullValue> b(500);
+  std::vector<std::string> values;
+  for (auto& c : graph.aggregate(b)) values.push_back(c->toString());
+  const std::vector<std::string> expected = {
+      "(true,{1={1=(1,true), 2=(2,false), 3=(3,false), 4=(4,false), 5=(5,true), 7=(7,true), 9=(9,true)}})"};
+  CHECK("BipartitenessCheckTest.testBipartite", values == expected, values.empty() ? "" : values[0]);
+  std::printf("PASS BipartitenessCheckTest.testBipartite\n");
+}
+
+static void non_bipartite_test() {
+  SimpleEdgeStream<int64_t, NullValue> graph(stream_of({{1, 2}, {2, 3}, {3, 1}, {4, 5}, {5, 7}, {4, 1}}));
+  BipartitenessCheck<NullValue> b(500);
+  std::vector<std::string> values;
+  for (auto& c : graph.aggregate(b)) values.push_back(c->toString());
+  CHECK("BipartitenessCheckTest.testNonBipartite", values == std::vector<std::string>({"(false,{})"}),
+        values.empty() ? "" : values[0]);
+  std::printf("PASS BipartitenessCheckTest.testNonBipartite\n");
+}
+
+static void disjoint_set_tests() {
+  DisjointSet ds;  // setup (:37-41)
+  for (int i = 0; i < 8; i++) ds.union_(i, i + 2);
+  CHECK("DisjointSetTest.testGetMatches", ds.getMatches().size() == 10, std::to_string(ds.getMatches().size()));
+  std::printf("PASS DisjointSetTest.testGetMatches\n");
+  auto root1 = ds.find(0), root2 = ds.find(1);
+  CHECK("DisjointSetTest.testFind", root1 && root2 && *root1 != *root2, "roots");
+  for (int i = 0; i < 10; i++) CHECK("DisjointSetTest.testFind", ds.find(i) == ((i % 2) == 0 ? root1 : root2), std::to_string(i));
+  CHECK("DisjointSetTest.testFind", !ds.find(1000).has_value(), "unknown vertex must be null");
+  std::printf("PASS DisjointSetTest.testFind\n");
+  DisjointSet ds2;
+  for (int i = 0; i < 8; i++) ds2.union_(i, i + 100);
+  ds2.merge(ds);
+  CHECK("DisjointSetTest.testMerge", ds2.getMatches().size() == 18, std::to_string(ds2.getMatches().size()));
+  std::set<int64_t> treeRoots;
+  for (auto& m : ds2.getMatches()) treeRoots.insert(*ds2.find(m.first));
+  CHECK("DisjointSetTest.testMerge", treeRoots.size() == 2, std::to_string(treeRoots.size()));
+  std::printf("PASS DisjointSetTest.testMerge\n");
+}
+
+static void merger_checkpoint_test() {
+  // Merger.snapshotState/restoreState (:127-135) through gs_serialize
+  auto ds = std::make_shared<DisjointSet>();
+  for (int i = 0; i < 50; ++i) ds->union_(i, (i * 7) % 50 + 100);
+  const std::string before = ds->toString();
+  auto img = ds->serialize();
+  DisjointSet restored;
+  restored.deserialize(img);
+  CHECK("Merger.checkpoint", restored.toString() == before, restored.toString());
+  Candidates c;
+  c.merge(BipartitenessCheck<>::edgeToCandidate(1, 2)).merge(BipartitenessCheck<>::edgeToCandidate(2, 3));
+  auto cimg = c.serialize();
+  Candidates c2;
+  c2.deserialize(cimg);
+  CHECK("Merger.checkpoint", c2.toString() == "(true,{1={1=(1,true), 2=(2,false), 3=(3,true)}})", c2.toString());
+  Candidates failed(false);
+  CHECK("Merger.checkpoint", failed.toString() == "(false,{})", failed.toString());
+  std::printf("PASS Merger.checkpoint\n");
+}
+
+int main() {
+  connected_components_test();
+  connected_components_test_parallel_windows();
+  bipartite_test();
+  non_bipartite_test();
+  disjoint_set_tests();
+  merger_checkpoint_test();
+  std::printf("%d failure(s)\n", failures);
+  return failures;
+}
