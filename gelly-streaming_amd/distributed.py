@@ -20,8 +20,13 @@ import torch.distributed as dist
 
 def all_gather_varlen(a, b, w, k, group=None):
     """All-gather variable-length (a[:k], b[:k], w[:k]) from every rank.
-    Returns [(a_r, b_r, w_r)] per rank (views into one gathered buffer)."""
+    Returns [(a_r, b_r, w_r)] per rank (views into one gathered buffer).
+    With the gloo backend device tensors are staged through host memory (tests
+    run several ranks on one GPU that way); with nccl (RCCL) they stay in HBM."""
     world = dist.get_world_size(group)
+    if a.is_cuda and dist.get_backend(group) == "gloo":
+        parts = all_gather_varlen(a[:k].cpu(), b[:k].cpu(), w[:k].cpu(), k, group)
+        return [(pa.to(a.device), pb.to(a.device), pw.to(a.device)) for pa, pb, pw in parts]
     dev = a.device
     cnt = torch.tensor([int(k)], dtype=torch.int64, device=dev)
     cnts = [torch.zeros_like(cnt) for _ in range(world)]

@@ -34,6 +34,6 @@ int main(int argc, char** argv) {
   }
   SimpleEdgeStream<int64_t, NullValue> edges(s);
   ConnectedComponents<NullValue> cc(mergeWindowTime);
-  for (auto& ds : edges.aggregate(cc)) std::printf("%s\n", ds->toString().c_str());
+  edges.aggregate(cc, [](const DisjointSetRef& ds) { std::printf("%s\n", ds->toString().c_str()); });
   return 0;
 }

@@ -377,12 +377,14 @@ class SummaryBulkAggregation : public SummaryAggregation<K, EV, S, T> {
 
   // run (:68-90): PartitionMapper -> keyBy(partition).timeWindow(t).fold(initial,
   // PartialAgg) -> timeWindowAll(t).reduce(combine) -> Merger -> (transform).
-  // Returns every emission in order (one per window that holds edges).
-  std::vector<T> run(const EdgeStream<K, EV>& stream) {
+  // Every emission (one per window that holds edges) is handed to `sink` at
+  // emission time (the addSink(...) of the reference tests); the running summary
+  // object is reused across windows exactly like the Merger's.
+  using Sink = std::function<void(const T&)>;
+  void run(const EdgeStream<K, EV>& stream, const Sink& sink) {
     const size_t n = stream.edges.size();
     const int p = std::max(1, stream.parallelism);
     typename Base::Merger merger(this->initialValue_, this->combineFun_, this->transientState_);
-    std::vector<T> out;
     size_t i = 0;
     while (i < n) {
       const int64_t w = window_of(stream, i);
@@ -401,9 +403,15 @@ class SummaryBulkAggregation : public SummaryAggregation<K, EV, S, T> {
         acc = acc ? this->combineFun_->reduce(acc, partial[q]) : partial[q];
       }
       S emitted = merger.flatMap(acc);
-      out.push_back(emit(emitted));
+      sink(emit(emitted));
       i = j;
     }
+  }
+  // Convenience: collect the emissions (references to live summaries; read them
+  // before the next window mutates the running summary, or use the sink form).
+  std::vector<T> run(const EdgeStream<K, EV>& stream) {
+    std::vector<T> out;
+    run(stream, [&out](const T& x) { out.push_back(x); });
     return out;
   }
 
@@ -426,6 +434,11 @@ template <typename K, typename EV>
 class SimpleEdgeStream {
  public:
   explicit SimpleEdgeStream(EdgeStream<K, EV> edges) : edges_(std::move(edges)) {}
+  template <typename S, typename T>
+  void aggregate(SummaryBulkAggregation<K, EV, S, T>& summaryAggregation,
+                 const typename SummaryBulkAggregation<K, EV, S, T>::Sink& sink) {
+    summaryAggregation.run(edges_, sink);
+  }
   template <typename S, typename T>
   std::vector<T> aggregate(SummaryBulkAggregation<K, EV, S, T>& summaryAggregation) {
     return summaryAggregation.run(edges_);

@@ -52,7 +52,7 @@ static void connected_components_test() {
   SimpleEdgeStream<int64_t, NullValue> graph(stream_of({{1, 2}, {1, 3}, {2, 3}, {1, 5}, {6, 7}, {8, 9}}));
   ConnectedComponents<NullValue> cc(5);
   std::vector<std::string> values;
-  for (auto& ds : graph.aggregate(cc)) values.push_back(ds->toString());  // CollectSink
+  graph.aggregate(cc, [&](const DisjointSetRef& ds) { values.push_back(ds->toString()); });  // CollectSink
   const std::vector<std::string> expected = {"1, 2, 3, 5", "6, 7", "8, 9"};
   CHECK("ConnectedComponentsTest.test", parser(values) == expected, values.back());
   std::printf("PASS ConnectedComponentsTest.test\n");
@@ -66,7 +66,7 @@ static void connected_components_test_parallel_windows() {
   SimpleEdgeStream<int64_t, NullValue> graph(s);
   ConnectedComponents<NullValue> cc(2);
   std::vector<std::string> values;
-  for (auto& ds : graph.aggregate(cc)) values.push_back(ds->toString());
+  graph.aggregate(cc, [&](const DisjointSetRef& ds) { values.push_back(ds->toString()); });
   CHECK("ConnectedComponentsTest.parallel", values.size() == 3, std::to_string(values.size()));
   CHECK("ConnectedComponentsTest.parallel", parser(values) == std::vector<std::string>({"1, 2, 3, 5", "6, 7", "8, 9"}),
         values.back());
@@ -77,7 +77,7 @@ static void bipartite_test() {
   SimpleEdgeStream<int64_t, NullValue> graph(stream_of({{1, 2}, {1, 3}, {1, 4}, {4, 5}, {4, 7}, {4, 9}}));
   BipartitenessCheck<NullValue> b(500);
   std::vector<std::string> values;
-  for (auto& c : graph.aggregate(b)) values.push_back(c->toString());
+  graph.aggregate(b, [&](const CandidatesRef& c) { values.push_back(c->toString()); });
   const std::vector<std::string> expected = {
       "(true,{1={1=(1,true), 2=(2,false), 3=(3,false), 4=(4,false), 5=(5,true), 7=(7,true), 9=(9,true)}})"};
   CHECK("BipartitenessCheckTest.testBipartite", values == expected, values.empty() ? "" : values[0]);
@@ -88,7 +88,7 @@ static void non_bipartite_test() {
   SimpleEdgeStream<int64_t, NullValue> graph(stream_of({{1, 2}, {2, 3}, {3, 1}, {4, 5}, {5, 7}, {4, 1}}));
   BipartitenessCheck<NullValue> b(500);
   std::vector<std::string> values;
-  for (auto& c : graph.aggregate(b)) values.push_back(c->toString());
+  graph.aggregate(b, [&](const CandidatesRef& c) { values.push_back(c->toString()); });
   CHECK("BipartitenessCheckTest.testNonBipartite", values == std::vector<std::string>({"(false,{})"}),
         values.empty() ? "" : values[0]);
   std::printf("PASS BipartitenessCheckTest.testNonBipartite\n");

@@ -1,0 +1,116 @@
+"""CPU (gloo, world_size 2 and 3): the multi-GPU combine protocol of
+gelly-streaming_amd/distributed.py. Each rank folds its share of every global
+micro-batch and exchanges its structural delta; afterwards every rank's replica
+must equal the whole stream folded by the oracle (bit-exact canonical labels).
+
+The device summary is replaced by `ModelReplica`, a CPU model of the C-ABI delta
+contract (include/gs_summary.h: gs_set_delta_tracking / gs_take_delta_device):
+new vertices as (v, v, 0), successful hooks as (root, new parent, parity)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class ModelReplica:
+    """Union-find with min-key hooking and delta recording (test model)."""
+
+    def __init__(self):
+        self.parent = {}
+        self.track = False
+        self.delta = []
+
+    def _find(self, v):
+        while self.parent[v] != v:
+            self.parent[v] = self.parent[self.parent[v]]
+            v = self.parent[v]
+        return v
+
+    def _touch(self, v):
+        if v not in self.parent:
+            self.parent[v] = v
+            if self.track:
+                self.delta.append((v, v, 0))
+
+    def fold_device(self, src, dst, n=None, w=None, stride=1):
+        s = src[:n].tolist()
+        d = dst[:n].tolist()
+        for a, b in zip(s, d):
+            self._touch(a)
+            self._touch(b)
+            ra, rb = self._find(a), self._find(b)
+            if ra == rb:
+                continue
+            hi, lo = (ra, rb) if ra > rb else (rb, ra)
+            self.parent[hi] = lo
+            if self.track:
+                self.delta.append((hi, lo, 0))
+
+    def set_delta_tracking(self, on=True):
+        self.track = bool(on)
+        self.delta = []
+
+    def take_delta_device(self, a, b, w):
+        k = len(self.delta)
+        if k:
+            arr = torch.tensor(self.delta, dtype=torch.int64)
+            a[:k] = arr[:, 0]
+            b[:k] = arr[:, 1]
+            w[:k] = arr[:, 2].to(torch.uint8)
+        self.delta = []
+        return k
+
+    def sync(self):
+        pass
+
+    def labels(self):
+        vs = sorted(self.parent)
+        return np.array(vs, np.int64), np.array([self._find(v) for v in vs], np.int64)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, src, dst, batch, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import gsamd  # noqa: F401  (registers gelly_streaming_amd)
+    from gelly_streaming_amd.distributed import DeltaExchangeFold
+
+    rep = ModelReplica()
+    x = DeltaExchangeFold(rep, 3 * batch * world + 16, torch.device("cpu"))
+    s = torch.from_numpy(src)
+    d = torch.from_numpy(dst)
+    g = batch * world
+    for o in range(0, len(src), g):  # global micro-batch: rank r folds slice r
+        lo = o + rank * batch
+        n = max(0, min(batch, len(src) - lo))
+        x.step(s[lo:], d[lo:], n)
+    v, lab = rep.labels()
+    out[rank] = (v.tolist(), lab.tolist(), x.exchanged)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_delta_exchange_gloo(oracle_mod, world):
+    src, dst = oracle_mod.rmat_edges(0x5EED0026, 12, 0, 1 << 13, True)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), src, dst, 256, out), nprocs=world, join=True)
+    ov, olab = oracle_mod.cc_labels(src, dst)
+    for r in range(world):
+        v, lab, exchanged = out[r]
+        assert v == ov.tolist(), "rank %d vertex set" % r
+        assert lab == olab.tolist(), "rank %d labels" % r
+        assert exchanged > 0
