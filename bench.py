@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-log2", type=int, default=24)
     p.add_argument("--no-profile-pass", action="store_true")
+    p.add_argument("--exchange", action="store_true",
+                   help="run the multi-GPU delta-exchange path even at one rank (overhead measurement)")
     return p.parse_args()
 
 
@@ -53,8 +55,13 @@ def main():
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if world > 1 or args.exchange:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     import gsamd as gs
     from gelly_streaming_amd.distributed import DeltaExchangeFold
@@ -67,7 +74,6 @@ def main():
 
     summ = gs.Summary("cc", device=local, capacity_hint=1 << args.scale)
     st = summ.stream
-    gs_stream = torch.cuda.ExternalStream(st, device=dev)
     src = torch.empty(per, dtype=torch.int64, device=dev)
     dst = torch.empty(per, dtype=torch.int64, device=dev)
     gs.gen_rmat(src, dst, start, per, args.scale, args.seed, True, stream=st)
@@ -76,7 +82,7 @@ def main():
     vcap = min(1 << args.scale, 2 * E) + 16
     out_v = torch.empty(vcap, dtype=torch.int64, device=dev)
     out_l = torch.empty(vcap, dtype=torch.int64, device=dev)
-    xch = DeltaExchangeFold(summ, 3 * B, dev) if world > 1 else None
+    xch = DeltaExchangeFold(summ, B, dev) if (world > 1 or args.exchange) else None
 
     nlabels = [0]
 
@@ -91,6 +97,8 @@ def main():
                 summ.fold_device(src[o:], dst[o:], n=n)
             else:
                 xch.step(src[o:], dst[o:], n)
+        if xch is not None:
+            xch.finish()
         nlabels[0] = summ.export_labels_device(out_v, out_l)  # canonical label pass (syncs)
 
     def barrier():
@@ -172,13 +180,14 @@ def main():
             "config": {"workload": "rmat%d-cc-stream" % args.scale, "scale": args.scale,
                        "edges": E, "micro_batch": B, "ids": "sparse 64-bit (scrambled)",
                        "vertices_labelled": int(nlabels[0]),
-                       "parallelism": "edge-shard x%d, per-batch delta all-gather" % world},
+                       "parallelism": "edge-shard x%d, per-batch delta all-gather" % world
+                       if xch is not None else "single GPU"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     summ.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

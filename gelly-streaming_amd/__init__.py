@@ -33,7 +33,8 @@ EXPORTED_SYMBOLS = (
     "gs_last_error", "gs_version", "gs_create", "gs_destroy", "gs_reset", "gs_fold", "gs_fold_device",
     "gs_combine", "gs_sync", "gs_num_vertices", "gs_find", "gs_export_labels", "gs_export_labels_device",
     "gs_bip_status", "gs_export_colouring", "gs_serialize", "gs_deserialize", "gs_set_delta_tracking",
-    "gs_take_delta_device", "gs_get_stream", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity",
+    "gs_take_delta_records", "gs_delta_stage", "gs_fold_records_device", "gs_fold_exchange_device",
+    "gs_get_stream", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity",
     "gs_gen_rmat", "gs_gen_er", "gs_gen_bip",
 )
 
@@ -88,7 +89,10 @@ def lib():
     L.gs_serialize.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
     L.gs_deserialize.argtypes = [_vp, _vp, _sz]
     L.gs_set_delta_tracking.argtypes = [_vp, ctypes.c_int]
-    L.gs_take_delta_device.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.POINTER(_sz)]
+    L.gs_take_delta_records.argtypes = [_vp, _vp, _sz, _vp]
+    L.gs_fold_records_device.argtypes = [_vp, _vp, _sz, ctypes.c_int]
+    L.gs_delta_stage.argtypes = [_vp, _vp, _sz]
+    L.gs_fold_exchange_device.argtypes = [_vp, _vp, _sz, _sz, ctypes.c_int]
     L.gs_get_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
     L.gs_set_profiling.argtypes = [_vp, ctypes.c_int]
     L.gs_kernel_stats.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double)]
@@ -238,11 +242,25 @@ class Summary:
     def set_delta_tracking(self, on=True):
         _check(lib().gs_set_delta_tracking(self._h, 1 if on else 0))
 
-    def take_delta_device(self, a, b, w):
-        got = _sz()
-        cap = a.numel() if hasattr(a, "numel") else len(a)
-        _check(lib().gs_take_delta_device(self._h, _ptr(a), _ptr(b), _ptr(w), cap, ctypes.byref(got)))
-        return got.value
+    def take_delta_records(self, rec, cap, count):
+        """Pack the delta since the last take into `rec` (device int64 [cap, 3]) and
+        its record count into `count` (device int64 [1]); asynchronous on self.stream."""
+        _check(lib().gs_take_delta_records(self._h, _ptr(rec), int(cap), _ptr(count)))
+
+    def delta_stage(self, send, cap):
+        """Stage the delta into `send` (device int64 [cap + 1, 3]: header row
+        {sent, queued, skip} + up to cap records; the rest stays queued);
+        asynchronous on self.stream."""
+        _check(lib().gs_delta_stage(self._h, _ptr(send), int(cap)))
+
+    def fold_exchange(self, recv, world, rows, skip_rank):
+        """Fold a gathered exchange buffer (world x rows records, row 0 of each
+        rank = header), skipping `skip_rank`'s rows."""
+        _check(lib().gs_fold_exchange_device(self._h, _ptr(recv), int(world), int(rows), int(skip_rank)))
+
+    def fold_records(self, rec, n, track=False):
+        """Fold n device records {a, b, w} (another replica's delta)."""
+        _check(lib().gs_fold_records_device(self._h, _ptr(rec), int(n), 1 if track else 0))
 
     # --- introspection
     @property

@@ -61,10 +61,13 @@ struct gs_summary {
   uint2* act = nullptr;
   uint32_t act_shard_cap = 0;
   bool track = false;
-  int64_t* da = nullptr;
-  int64_t* db = nullptr;
-  uint8_t* dw = nullptr;
+  int64_t* drec = nullptr;  // [kShards][delta_shard_cap][3]
   uint32_t delta_shard_cap = 0;
+  // exchange record queue (ping-pong): packed records not yet sent
+  int64_t* q[2] = {nullptr, nullptr};
+  unsigned long long* qn = nullptr;  // [2] device counts
+  uint64_t qcap = 0;
+  int qsel = 0;
   uint64_t delta_fill_ub = 0;  // worst-case per-shard fill since the last take
   // hook policy (DESIGN.md "Kernels"): FUSED hooks in k_fold; DEFER hooks waves
   // with <= inline_max active edges in place and hands the rest to the next
@@ -74,6 +77,7 @@ struct gs_summary {
   int ept = 1;        // edges per k_fold thread
   uint64_t epoch = 0; // k_fold launches since reset (selects the active set)
   int pending = -1;   // active set still waiting to be drained
+  bool pending_track = false;  // tracking state of the fold that deferred it
   // staging for host folds
   int64_t* d_stage = nullptr;  // [2][2][kStageChunk]
   uint8_t* d_wstage = nullptr; // [2][kStageChunk]
@@ -106,9 +110,7 @@ struct gs_summary {
     gs::Lists L;
     L.act = act;
     L.act_shard_cap = act_shard_cap;
-    L.da = da;
-    L.db = db;
-    L.dw = dw;
+    L.drec = drec;
     L.delta_shard_cap = delta_shard_cap;
     return L;
   }
@@ -215,16 +217,22 @@ int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
   return GS_OK;
 }
 
+struct ExchangeLayout {
+  uint32_t rows = 0;  // > 0: gathered exchange buffer, rows per rank
+  int skip_rank = -1;
+  const int64_t* base = nullptr;
+};
 int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
-                     size_t stride, bool check_cap = true);
+                     size_t stride, size_t w_stride, bool track, bool check_cap = true,
+                     const ExchangeLayout& xl = ExchangeLayout());
 
 // Hook the deferred active edges (DEFER mode) so the forest is complete.
 int flush_hooks(gs_summary* h) {
   if (h->pending < 0) return GS_OK;
   {
     Prof p(h, KID_HOOK);
-    gs::launch_hook(h->kind == GS_KIND_SIGNED, h->track, h->table(), h->lists(), h->pending, gs::kShards * 16,
-                    h->stream);
+    gs::launch_hook(h->kind == GS_KIND_SIGNED, h->pending_track, h->table(), h->lists(), h->pending,
+                    gs::kShards * 16, h->stream);
   }
   GS_HIP(hipGetLastError());
   h->pending = -1;
@@ -274,7 +282,7 @@ int grow(gs_summary* h, uint64_t new_cap) {
   if (rc) return rc;
   if (fail_flag) GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, h->stream));
   h->nv_ub = got;
-  rc = fold_device_impl(h, v, l, p, got, 1, /*check_cap=*/false);
+  rc = fold_device_impl(h, v, l, p, got, 1, 1, /*track=*/false, /*check_cap=*/false);
   h->track = track;
   if (rc) return rc;
   GS_HIP(hipStreamSynchronize(h->stream));
@@ -302,7 +310,7 @@ int ensure_capacity(gs_summary* h, size_t n) {
 }
 
 int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
-                     size_t stride, bool check_cap) {
+                     size_t stride, size_t w_stride, bool track, bool check_cap, const ExchangeLayout& xl) {
   if (n == 0) return GS_OK;
   if (check_cap) {
     int rc = ensure_capacity(h, n);
@@ -314,10 +322,10 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     const uint32_t per_block = 256u * (uint32_t)h->ept;
     const uint32_t blocks = (c + per_block - 1) / per_block;
     const uint32_t per_shard_edges = ((blocks + gs::kShards - 1) / gs::kShards) * per_block;
-    if (h->track) {
+    if (track) {
       h->delta_fill_ub += (uint64_t)per_shard_edges * 3;
       if (h->delta_fill_ub > h->delta_shard_cap)
-        return fail(GS_ERR_CAPACITY, "delta list full: call gs_take_delta_device after each fold of <= 2^22 edges");
+        return fail(GS_ERR_CAPACITY, "delta list full: call gs_take_delta_records after each fold of <= 2^22 edges");
     }
     const int cur = (int)(h->epoch % gs::kActSets);
     const int zero = (int)((h->epoch + 1) % gs::kActSets);
@@ -325,17 +333,19 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     const int drain = h->mode == gs_summary::DEFER ? h->pending : -1;
     {
       Prof p(h, KID_FOLD);
-      gs::launch_fold(sign, h->track, h->ept, h->table(), h->lists(), src + off * stride, dst + off * stride,
-                      w ? w + off : nullptr, c, (uint32_t)stride, cur, drain, zero, inline_max, h->stream);
+      gs::launch_fold(sign, track, h->ept, h->table(), h->lists(), src + off * stride, dst + off * stride,
+                      w ? w + off * w_stride : nullptr, c, (uint32_t)stride, (uint32_t)w_stride, cur, drain, zero,
+                      inline_max, xl.rows, xl.skip_rank, xl.base, (uint32_t)off, h->stream);
     }
     GS_HIP(hipGetLastError());
     h->epoch++;
     h->pending = h->mode == gs_summary::FUSED ? -1 : cur;
+    h->pending_track = track;
     if (h->mode == gs_summary::COMPACT) {
       const int sub = (int)std::min<uint32_t>((blocks + gs::kShards - 1) / gs::kShards, 16u);
       {
         Prof p(h, KID_HOOK);
-        gs::launch_hook(sign, h->track, h->table(), h->lists(), cur, gs::kShards * sub, h->stream);
+        gs::launch_hook(sign, track, h->table(), h->lists(), cur, gs::kShards * sub, h->stream);
       }
       GS_HIP(hipGetLastError());
       h->pending = -1;
@@ -415,9 +425,10 @@ int gs_destroy(gs_handle h) {
   (void)hipFree(h->tab);
   (void)hipFree(h->ctr);
   (void)hipFree(h->act);
-  (void)hipFree(h->da);
-  (void)hipFree(h->db);
-  (void)hipFree(h->dw);
+  (void)hipFree(h->drec);
+  (void)hipFree(h->q[0]);
+  (void)hipFree(h->q[1]);
+  (void)hipFree(h->qn);
   (void)hipFree(h->d_stage);
   (void)hipFree(h->d_wstage);
   (void)hipFree(h->d_scratch);
@@ -437,6 +448,7 @@ int gs_reset(gs_handle h) {
     gs::launch_init(h->tab, h->cap + 1, h->stream);
   }
   GS_HIP(hipGetLastError());
+  if (h->qn) GS_HIP(hipMemsetAsync(h->qn, 0, 16, h->stream));
   h->nv_ub = 0;
   h->epoch = 0;
   h->pending = -1;
@@ -463,7 +475,7 @@ static int fold_host_impl(gs_handle h, const int64_t* src, const int64_t* dst, c
       GS_HIP(hipMemcpyAsync(dwp, h->h_wstage + (size_t)b * kStageChunk, c, hipMemcpyHostToDevice, h->stream));
     }
     GS_HIP(hipEventRecord(h->stage_ev[b], h->stream));
-    int rc = fold_device_impl(h, ds, ds + kStageChunk, dwp, c, 1);
+    int rc = fold_device_impl(h, ds, ds + kStageChunk, dwp, c, 1, 1, h->track);
     if (rc) return rc;
   }
   return GS_OK;
@@ -481,7 +493,15 @@ int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const ui
   if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
   if (stride == 0) return fail(GS_ERR_INVALID, "stride must be >= 1");
   DeviceGuard g(h->device);
-  return fold_device_impl(h, src, dst, w, n, stride);
+  return fold_device_impl(h, src, dst, w, n, stride, 1, h->track);
+}
+
+int gs_fold_records_device(gs_handle h, const int64_t* rec, size_t n, int track) {
+  if (int rc = check(h)) return rc;
+  if (n && !rec) return fail(GS_ERR_INVALID, "null records");
+  if (track && !h->drec) return fail(GS_ERR_INVALID, "delta tracking was never enabled");
+  DeviceGuard g(h->device);
+  return fold_device_impl(h, rec, rec + 1, reinterpret_cast<const uint8_t*>(rec + 2), n, 3, 24, track != 0);
 }
 
 int gs_sync(gs_handle h) {
@@ -626,7 +646,7 @@ int gs_combine(gs_handle dst, gs_handle src) {
       GS_HIP(hipMemcpyPeerAsync(dl, dst->device, sl, src->device, got * 8, dst->stream));
       GS_HIP(hipMemcpyPeerAsync(dp, dst->device, sp, src->device, got, dst->stream));
     }
-    rc = fold_device_impl(dst, dv, dl, dp, got, 1);
+    rc = fold_device_impl(dst, dv, dl, dp, got, 1, 1, dst->track);
     GS_HIP(hipStreamSynchronize(dst->stream));
     if (dv != sv) {
       (void)hipFree(dv);
@@ -704,48 +724,73 @@ int gs_set_delta_tracking(gs_handle h, int on) {
   if (int rc = check(h)) return rc;
   DeviceGuard g(h->device);
   if (int rc = flush_hooks(h)) return rc;  // deferred hooks belong to the previous tracking state
-  if (on && !h->da) {
+  if (on && !h->drec) {
     // worst case between two takes: one fold chunk of kMaxChunk edges
     h->delta_shard_cap = ((kMaxChunk / 256 + gs::kShards - 1) / gs::kShards) * 256 * 3;
     const size_t m = (size_t)gs::kShards * h->delta_shard_cap;
-    GS_HIP(hipMalloc(&h->da, m * 8));
-    GS_HIP(hipMalloc(&h->db, m * 8));
-    GS_HIP(hipMalloc(&h->dw, m));
+    GS_HIP(hipMalloc(&h->drec, m * 24));
   }
   GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, gs::kShards * gs::kCtrStride * 4, h->stream));
+  if (h->qn) GS_HIP(hipMemsetAsync(h->qn, 0, 16, h->stream));
   h->delta_fill_ub = 0;
   h->track = on != 0;
   return GS_OK;
 }
 
-int gs_take_delta_device(gs_handle h, int64_t* a, int64_t* b, uint8_t* w, size_t cap, size_t* n) {
-  if (int rc = check(h)) return rc;
-  if (!n) return fail(GS_ERR_INVALID, "n is null");
-  if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
-  DeviceGuard g(h->device);
+static int ensure_queue(gs_summary* h) {
+  if (h->q[0]) return GS_OK;
+  h->qcap = (uint64_t)gs::kShards * h->delta_shard_cap;  // one full delta list
+  GS_HIP(hipMalloc(&h->q[0], h->qcap * 24));
+  GS_HIP(hipMalloc(&h->q[1], h->qcap * 24));
+  GS_HIP(hipMalloc(&h->qn, 16));
+  GS_HIP(hipMemsetAsync(h->qn, 0, 16, h->stream));
+  h->qsel = 0;
+  return GS_OK;
+}
+
+// backlog q[qsel] + fresh delta -> send rows (first cap) and q[qsel ^ 1] (the rest)
+static int stage(gs_summary* h, int64_t* send, uint64_t cap) {
   if (int rc = flush_hooks(h)) return rc;
-  std::vector<uint32_t> c(gs::kShards * gs::kCtrStride);
-  GS_HIP(hipMemcpyAsync(c.data(), h->ctr + gs::ctr_index(gs::CTR_DELTA), c.size() * 4, hipMemcpyDeviceToHost,
-                        h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
-  int rc = check_device_flags(h);
-  if (rc) return rc;
-  uint64_t total = 0;
-  uint32_t mx = 0;
-  for (int s = 0; s < gs::kShards; ++s) {
-    total += c[s * gs::kCtrStride];
-    mx = std::max(mx, c[s * gs::kCtrStride]);
-  }
-  *n = total;
-  if (total > cap) return fail(GS_ERR_TRUNCATED, "delta capacity too small");
-  if (total) {
-    const int sub = (int)std::min<uint32_t>((mx + 255) / 256, 64u);
-    gs::launch_pack(h->table(), h->lists(), a, b, w, cap, std::max(sub, 1), h->stream);
-    GS_HIP(hipGetLastError());
-  }
-  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, gs::kShards * gs::kCtrStride * 4, h->stream));
+  if (int rc = ensure_queue(h)) return rc;
+  const int a = h->qsel, b = h->qsel ^ 1;
+  gs::launch_stage(h->table(), h->lists(), h->q[a], h->qn + a, h->q[b], h->qn + b, h->qcap, send, cap, h->stream);
+  GS_HIP(hipGetLastError());
+  h->qsel = b;
   h->delta_fill_ub = 0;
   return GS_OK;
+}
+
+int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count) {
+  if (int rc = check(h)) return rc;
+  if (!count) return fail(GS_ERR_INVALID, "count is null");
+  if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
+  DeviceGuard g(h->device);
+  if (int rc = stage(h, nullptr, 0)) return rc;  // everything into the queue
+  gs::launch_copy_queue(h->q[h->qsel], h->qn + h->qsel, h->qcap, rec, cap, count, h->stream);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemsetAsync(h->qn, 0, 16, h->stream));
+  return GS_OK;
+}
+
+int gs_delta_stage(gs_handle h, int64_t* send, size_t cap) {
+  if (int rc = check(h)) return rc;
+  if (!send) return fail(GS_ERR_INVALID, "send is null");
+  if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
+  DeviceGuard g(h->device);
+  return stage(h, send, cap);
+}
+
+int gs_fold_exchange_device(gs_handle h, const int64_t* recv, size_t world, size_t rows, int skip_rank) {
+  if (int rc = check(h)) return rc;
+  if (!recv || rows == 0) return fail(GS_ERR_INVALID, "empty exchange buffer");
+  if (world * rows > 0xFFFFFFFFull) return fail(GS_ERR_INVALID, "exchange buffer too large");
+  DeviceGuard g(h->device);
+  ExchangeLayout xl;
+  xl.rows = (uint32_t)rows;
+  xl.skip_rank = skip_rank;
+  xl.base = recv;
+  return fold_device_impl(h, recv, recv + 1, reinterpret_cast<const uint8_t*>(recv + 2), world * rows, 3, 24,
+                          /*track=*/false, true, xl);
 }
 
 int gs_get_stream(gs_handle h, void** stream) {

@@ -41,6 +41,9 @@ enum CounterBlock : int {
   CTR_ERR,                       // device-side error (table overflow)
   CTR_EXPORT,                    // export append counter
   CTR_OVF,                       // delta / active list overflow
+  CTR_STAGE_N,                   // records staged by the running k_stage (u32 pair = u64)
+  CTR_STAGE_N_HI,
+  CTR_STAGE_DONE,                // k_stage block ticket
   CTR_COUNT
 };
 __host__ __device__ constexpr int ctr_index(int c) { return c * kCtrStride; }
@@ -62,9 +65,7 @@ struct Table {
 struct Lists {
   uint2* act;            // active (root<<1|parity, root) entries, [kActSets][kShards][act_shard_cap]
   uint32_t act_shard_cap;
-  int64_t* da;           // delta triples, [kShards][delta_shard_cap]
-  int64_t* db;
-  uint8_t* dw;
+  int64_t* drec;         // delta records {a, b, parity}, [kShards][delta_shard_cap][3]
   uint32_t delta_shard_cap;
 };
 
@@ -227,10 +228,10 @@ __device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, 
       if (TRACK) {
         const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_DELTA + shard)], 1u);
         if (pos < L.delta_shard_cap) {
-          const size_t o = (size_t)shard * L.delta_shard_cap + pos;
-          L.da[o] = a_lo ? kb : ka;
-          L.db[o] = a_lo ? ka : kb;
-          L.dw[o] = (uint8_t)(SIGNED ? (need & 1u) : 0u);
+          int64_t* r = L.drec + ((size_t)shard * L.delta_shard_cap + pos) * 3;
+          r[0] = a_lo ? kb : ka;
+          r[1] = a_lo ? ka : kb;
+          r[2] = (int64_t)(SIGNED ? (need & 1u) : 0u);
         } else {
           atomicOr(&t.ctr[ctr_index(CTR_OVF)], 1u);
         }

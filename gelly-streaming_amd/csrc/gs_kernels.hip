@@ -68,9 +68,14 @@ __device__ __forceinline__ void drain_set(const Table& t, const Lists& L, int se
 struct FoldArgs {
   const int64_t* src;
   const int64_t* dst;
-  const uint8_t* w;
+  const uint8_t* w;   // per edge: bit 0 = required parity (SIGNED), bit 7 = skip (padding record)
   uint32_t n;
-  uint32_t stride;
+  uint32_t stride;    // elements between consecutive src (and dst) entries
+  uint32_t w_stride;  // bytes between consecutive w entries
+  uint32_t rows;      // > 0: exchange layout, `rows` records per rank, row 0 = header {sent, ...}
+  int skip_rank;      // rank whose rows are skipped (the caller's own)
+  const int64_t* hdr; // exchange layout: start of the gathered buffer (rank r header at hdr[r * rows * 3])
+  uint32_t base;      // exchange layout: index of this launch's first record in the gathered buffer
   int cur;
   int drain;
   int zero;
@@ -92,9 +97,15 @@ __global__ __launch_bounds__(256) void k_fold(Table t, Lists L, FoldArgs a) {
     const uint32_t i = blockIdx.x * (256u * EPT) + e * 256u + threadIdx.x;
     valid[e] = i < a.n;
     act[e] = false;
+    if (valid[e] && a.rows) {  // exchange layout: per-rank header gives the live row count
+      const uint32_t ig = a.base + i, r = ig / a.rows, j = ig - r * a.rows;
+      valid[e] = j >= 1 && (int)r != a.skip_rank && (int64_t)j <= a.hdr[(size_t)r * a.rows * 3];
+    }
+    const uint32_t wi = (valid[e] && a.w) ? a.w[(size_t)i * a.w_stride] : 1u;
+    if (wi & 0x80u) valid[e] = false;
     ks[e] = valid[e] ? a.src[(size_t)i * a.stride] : 0;
     kd[e] = valid[e] ? a.dst[(size_t)i * a.stride] : 0;
-    need[e] = SIGNED ? ((valid[e] && a.w) ? (a.w[i] & 1u) : 1u) : 0u;
+    need[e] = SIGNED ? (wi & 1u) : 0u;
   }
   // all first relabel probes of the thread in flight together
   uint32_t hu[EPT], hv[EPT], l0u[EPT], l0v[EPT];
@@ -116,27 +127,20 @@ __global__ __launch_bounds__(256) void k_fold(Table t, Lists L, FoldArgs a) {
     bool nu, nv;
     const uint32_t su = lookup_resolve(t, ks[e], hu[e], k0u[e], l0u[e], lu[e], nu);
     const uint32_t sv = lookup_resolve(t, kd[e], hv[e], k0v[e], l0v[e], lv[e], nv);
-    if (nu || nv) {
-      const uint32_t cnt = (nu ? 1u : 0u) + (nv && sv != su ? 1u : 0u);
-      atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], cnt);
-      if (TRACK) {
-        const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_DELTA + shard)], cnt);
-        if (pos + cnt <= L.delta_shard_cap) {
-          const size_t o = (size_t)shard * L.delta_shard_cap + pos;
-          if (nu) {
-            L.da[o] = ks[e];
-            L.db[o] = ks[e];
-            L.dw[o] = 0;
-          }
-          if (nv && sv != su) {
-            const size_t o2 = o + (nu ? 1 : 0);
-            L.da[o2] = kd[e];
-            L.db[o2] = kd[e];
-            L.dw[o2] = 0;
-          }
-        } else {
-          atomicOr(&t.ctr[ctr_index(CTR_OVF)], 1u);
-        }
+    if (nu || nv) atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], (nu ? 1u : 0u) + (nv && sv != su ? 1u : 0u));
+    // Delta: a new vertex with an edge to another vertex is always named by a hook
+    // record (as the hooked root or as the new parent: its singleton tree can only
+    // change through a CAS on it or onto it), so only a new vertex seen through a
+    // self-loop needs a record of its own.
+    if (TRACK && nu && su == sv) {
+      const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_DELTA + shard)], 1u);
+      if (pos < L.delta_shard_cap) {
+        int64_t* r = L.drec + ((size_t)shard * L.delta_shard_cap + pos) * 3;
+        r[0] = ks[e];
+        r[1] = ks[e];
+        r[2] = 0;
+      } else {
+        atomicOr(&t.ctr[ctr_index(CTR_OVF)], 1u);
       }
     }
     ru[e] = su;
@@ -259,23 +263,119 @@ __global__ __launch_bounds__(256) void k_export(Table t, int64_t* __restrict__ o
   }
 }
 
-// Copy the sharded delta list into contiguous arrays. grid = kShards * sub.
-__global__ __launch_bounds__(256) void k_pack(Table t, Lists L, int64_t* __restrict__ oa, int64_t* __restrict__ ob,
-                                              uint8_t* __restrict__ ow, uint64_t cap_out, int sub) {
-  const int shard = blockIdx.x & (kShards - 1);
-  const int part = blockIdx.x / kShards;
-  uint64_t base = 0;
-  for (int s = 0; s < shard; ++s) base += min(t.ctr[ctr_index(CTR_DELTA + s)], L.delta_shard_cap);
-  const uint32_t cnt = min(t.ctr[ctr_index(CTR_DELTA + shard)], L.delta_shard_cap);
-  const size_t in0 = (size_t)shard * L.delta_shard_cap;
-  for (uint32_t j = part * 256u + threadIdx.x; j < cnt; j += (uint32_t)sub * 256u) {
-    const uint64_t o = base + j;
-    if (o < cap_out) {
-      oa[o] = L.da[in0 + j];
-      ob[o] = L.db[in0 + j];
-      ow[o] = L.dw[in0 + j];
-    }
+// One exchange stage, one launch. Every delta record -- first the backlog q_in
+// (qn_in records left over from the previous stage), then the sharded delta list --
+// takes a position from one counter (block-aggregated): positions < cap go to send rows 1..cap,
+// the rest to the backlog q_out. The last block to finish writes the header row
+// {sent, queued, skip}, *qn_out, and resets the counters it consumed. The receiver
+// reads `sent` from the header, so unused send rows need no padding.
+// cap == 0 with send == nullptr: everything goes to q_out (gs_take_delta_records).
+// Block-aggregated append: every thread of the block calls it (uniform control
+// flow); returns this thread's position, one global atomic per call per block.
+__device__ __forceinline__ unsigned long long block_append(bool keep, unsigned long long* counter) {
+  __shared__ uint32_t wcnt[4];
+  __shared__ unsigned long long base;
+  const unsigned long long m = __ballot(keep);
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
+  if (lane == 0) wcnt[w] = __popcll(m);
+  __syncthreads();
+  uint32_t woff = 0, tot = 0;
+  for (uint32_t q = 0; q < 4; ++q) {
+    if (q < w) woff += wcnt[q];
+    tot += wcnt[q];
   }
+  if (threadIdx.x == 0) base = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+  __syncthreads();
+  const unsigned long long pos = base + woff + rank;
+  __syncthreads();  // wcnt/base are reused by the next call
+  return pos;
+}
+
+__device__ __forceinline__ void stage_write(const Table& t, unsigned long long pos, int64_t a, int64_t b, int64_t w,
+                                            int64_t* send, uint64_t cap, int64_t* q_out, uint64_t qcap) {
+  int64_t* r;
+  if (pos < cap) {
+    r = send + (pos + 1) * 3;
+  } else if (pos - cap < qcap) {
+    r = q_out + (pos - cap) * 3;
+  } else {
+    atomicOr(&t.ctr[ctr_index(CTR_OVF)], 1u);
+    return;
+  }
+  r[0] = a;
+  r[1] = b;
+  r[2] = w;
+}
+
+// grid = kShards * kStageParts blocks of 256 threads.
+constexpr uint32_t kStageParts = 4;
+__global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* __restrict__ q_in,
+                                               unsigned long long* qn_in, int64_t* __restrict__ q_out,
+                                               unsigned long long* qn_out, uint64_t qcap, int64_t* __restrict__ send,
+                                               uint64_t cap) {
+  unsigned long long* count = (unsigned long long*)&t.ctr[ctr_index(CTR_STAGE_N)];
+  const uint64_t backlog = min((unsigned long long)*qn_in, (unsigned long long)qcap);
+  const uint64_t G = (uint64_t)gridDim.x * 256;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256; base < backlog; base += G) {
+    const uint64_t i = base + threadIdx.x;
+    const bool keep = i < backlog;
+    int64_t a = 0, b = 0, w = 0;
+    if (keep) {
+      a = q_in[i * 3];
+      b = q_in[i * 3 + 1];
+      w = q_in[i * 3 + 2];
+    }
+    const unsigned long long pos = block_append(keep, count);
+    if (keep) stage_write(t, pos, a, b, w, send, cap, q_out, qcap);
+  }
+  // delta shards: block b takes shard b % kShards, part b / kShards
+  const uint32_t s = blockIdx.x % kShards, part = blockIdx.x / kShards;
+  const uint32_t cnt = min(t.ctr[ctr_index(CTR_DELTA + s)], L.delta_shard_cap);
+  const int64_t* in = L.drec + (size_t)s * L.delta_shard_cap * 3;
+  for (uint32_t base = part * 256u; base < cnt; base += kStageParts * 256u) {
+    const uint32_t j = base + threadIdx.x;
+    const bool keep = j < cnt;
+    int64_t a = 0, b = 0, w = 0;
+    if (keep) {
+      a = in[(size_t)j * 3];
+      b = in[(size_t)j * 3 + 1];
+      w = in[(size_t)j * 3 + 2];
+    }
+    const unsigned long long pos = block_append(keep, count);
+    if (keep) stage_write(t, pos, a, b, w, send, cap, q_out, qcap);
+  }
+  // last block: header + counter resets
+  __shared__ uint32_t last;
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&t.ctr[ctr_index(CTR_STAGE_DONE)], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x < kShards) t.ctr[ctr_index(CTR_DELTA + threadIdx.x)] = 0u;
+  if (threadIdx.x == 0) {
+    const unsigned long long total = atomicAdd(count, 0ull);
+    const unsigned long long sent = total < cap ? total : cap;
+    if (send) {
+      send[0] = (int64_t)sent;
+      send[1] = (int64_t)total;
+      send[2] = 0x80;
+    }
+    *qn_out = total - sent;
+    *qn_in = 0ull;
+    atomicExch(count, 0ull);
+    atomicExch(&t.ctr[ctr_index(CTR_STAGE_DONE)], 0u);
+  }
+}
+
+// Copy the whole record queue (first cap records) and its count out.
+__global__ __launch_bounds__(256) void k_copy_queue(const int64_t* __restrict__ q, const unsigned long long* qn,
+                                                    uint64_t qcap, int64_t* __restrict__ out, uint64_t cap,
+                                                    uint64_t* count) {
+  const uint64_t total = min((unsigned long long)*qn, (unsigned long long)qcap);
+  const uint64_t n = total < cap ? total : cap;
+  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gtid == 0) *count = total;
+  for (uint64_t i = gtid; i < n * 3; i += (uint64_t)gridDim.x * blockDim.x) out[i] = q[i];
 }
 
 // Single-vertex lookup (gs_find): label and presence.
@@ -316,9 +416,10 @@ void launch_init(Slot* tab, uint64_t nslots, hipStream_t st) {
 }
 
 void launch_fold(bool sign, bool track, int ept, const Table& t, const Lists& L, const int64_t* src,
-                 const int64_t* dst, const uint8_t* w, uint32_t n, uint32_t stride, int cur, int drain, int zero,
-                 int inline_max, hipStream_t st) {
-  FoldArgs a{src, dst, w, n, stride, cur, drain, zero, inline_max};
+                 const int64_t* dst, const uint8_t* w, uint32_t n, uint32_t stride, uint32_t w_stride, int cur,
+                 int drain, int zero, int inline_max, uint32_t rows, int skip_rank, const int64_t* hdr,
+                 uint32_t base, hipStream_t st) {
+  FoldArgs a{src, dst, w, n, stride, w_stride, rows, skip_rank, hdr, base, cur, drain, zero, inline_max};
   const uint32_t per_block = 256u * (uint32_t)ept;
   const dim3 g((n + per_block - 1) / per_block), b(256);
 #define GS_FOLD(S, T, E)                                                          \
@@ -355,9 +456,15 @@ void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t*
     hipLaunchKernelGGL((k_export<false>), dim3(g), dim3(256), 0, st, t, ov, ol, op, cap_out);
 }
 
-void launch_pack(const Table& t, const Lists& L, int64_t* oa, int64_t* ob, uint8_t* ow, uint64_t cap_out, int sub,
-                 hipStream_t st) {
-  hipLaunchKernelGGL(k_pack, dim3(kShards * sub), dim3(256), 0, st, t, L, oa, ob, ow, cap_out, sub);
+void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned long long* qn_in, int64_t* q_out,
+                  unsigned long long* qn_out, uint64_t qcap, int64_t* send, uint64_t cap, hipStream_t st) {
+  hipLaunchKernelGGL(k_stage, dim3(kShards * kStageParts), dim3(256), 0, st, t, L, q_in, qn_in, q_out, qn_out, qcap,
+                     send, cap);
+}
+
+void launch_copy_queue(const int64_t* q, const unsigned long long* qn, uint64_t qcap, int64_t* out, uint64_t cap,
+                       uint64_t* count, hipStream_t st) {
+  hipLaunchKernelGGL(k_copy_queue, dim3(1024), dim3(256), 0, st, q, qn, qcap, out, cap, count);
 }
 
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st) {

@@ -13,13 +13,16 @@ void launch_init(Slot* tab, uint64_t nslots, hipStream_t st);
 // drain: active set hooked by this launch too (-1: none); zero: set whose counters
 // this launch resets (-1: none).
 void launch_fold(bool sign, bool track, int ept, const Table& t, const Lists& L, const int64_t* src,
-                 const int64_t* dst, const uint8_t* w, uint32_t n, uint32_t stride, int cur, int drain, int zero,
-                 int inline_max, hipStream_t st);
+                 const int64_t* dst, const uint8_t* w, uint32_t n, uint32_t stride, uint32_t w_stride, int cur,
+                 int drain, int zero, int inline_max, uint32_t rows, int skip_rank, const int64_t* hdr,
+                 uint32_t base, hipStream_t st);
 void launch_hook(bool sign, bool track, const Table& t, const Lists& L, int set, int blocks, hipStream_t st);
 void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out,
                    hipStream_t st);
-void launch_pack(const Table& t, const Lists& L, int64_t* oa, int64_t* ob, uint8_t* ow, uint64_t cap_out, int sub,
-                 hipStream_t st);
+void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned long long* qn_in, int64_t* q_out,
+                  unsigned long long* qn_out, uint64_t qcap, int64_t* send, uint64_t cap, hipStream_t st);
+void launch_copy_queue(const int64_t* q, const unsigned long long* qn, uint64_t qcap, int64_t* out, uint64_t cap,
+                       uint64_t* count, hipStream_t st);
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st);
 
 }  // namespace gs

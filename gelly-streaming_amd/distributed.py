@@ -5,78 +5,159 @@ This replaces the reference's gather of per-partition summaries into a
 parallelism-1 reducer (SummaryBulkAggregation.java:77-83: keyBy(partition) ->
 timeWindow fold -> timeWindowAll reduce -> Merger). Union is associative and
 commutative, so instead of shipping whole summaries to one task every rank ships
-only the STRUCTURAL DELTA its fold made (new vertices, successful hooks: at most
-one record per merged component, i.e. O(changes), not O(V)) and folds every other
-rank's delta into its replica. After each exchange all replicas describe the same
-partition, so each rank can answer queries / emit the Merger output locally.
+only the STRUCTURAL DELTA its fold made (successful hooks, plus new vertices that
+stayed roots: O(changes), not O(V)) and folds every other rank's delta into its
+replica. After each exchange all replicas describe the same partition, so any
+rank can answer queries / emit the Merger output.
 
-Collectives (RCCL over xGMI for `nccl`, gloo on CPU in tests): one all-gather of
-the per-rank delta counts, one all-gather of the padded (3 x max_count) int64
-payload. No other data-path communication.
+No host synchronisation on the per-batch path:
+  * every rank sends exactly cap + 1 rows (gs_delta_stage: a header row
+    {sent, queued, skip} + up to cap records) -- cap is agreed without
+    communication: it starts at `first_cap` and is re-derived every `retune`
+    batches from gathered headers that every rank holds identically;
+  * records past cap stay queued on the device and ride with the next exchange;
+  * the all-gather (RCCL, torch's current stream) waits on an event of the
+    summary's stream; the fold of the other ranks' rows (gs_fold_exchange_device,
+    one launch, live row counts read from the headers on the device) waits on an
+    event of the collective; batch b+1 is folded before batch b's rows are
+    applied, so the collective overlaps the next fold.
+`finish()` applies the last batch and drains any backlog in synchronous rounds.
+Folding a remote delta late is exact because union commutes.
 """
 import torch
 import torch.distributed as dist
 
-
-def all_gather_varlen(a, b, w, k, group=None):
-    """All-gather variable-length (a[:k], b[:k], w[:k]) from every rank.
-    Returns [(a_r, b_r, w_r)] per rank (views into one gathered buffer).
-    With the gloo backend device tensors are staged through host memory (tests
-    run several ranks on one GPU that way); with nccl (RCCL) they stay in HBM."""
-    world = dist.get_world_size(group)
-    if a.is_cuda and dist.get_backend(group) == "gloo":
-        parts = all_gather_varlen(a[:k].cpu(), b[:k].cpu(), w[:k].cpu(), k, group)
-        return [(pa.to(a.device), pb.to(a.device), pw.to(a.device)) for pa, pb, pw in parts]
-    dev = a.device
-    cnt = torch.tensor([int(k)], dtype=torch.int64, device=dev)
-    cnts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(cnts, cnt, group=group)
-    cnts = [int(c.item()) for c in cnts]
-    m = max(cnts)
-    if m == 0:
-        return [(a[:0], b[:0], w[:0]) for _ in range(world)]
-    payload = torch.zeros((3, m), dtype=torch.int64, device=dev)
-    if k:
-        payload[0, :k] = a[:k]
-        payload[1, :k] = b[:k]
-        payload[2, :k] = w[:k].to(torch.int64)
-    outs = [torch.empty_like(payload) for _ in range(world)]
-    dist.all_gather(outs, payload, group=group)
-    return [(o[0, :c], o[1, :c], o[2, :c].to(torch.uint8)) for o, c in zip(outs, cnts)]
+SKIP = 0x80  # wire record w bit 7: padding / header row
+HDR_LAG = 4  # a retune reads the gathered headers of the exchange HDR_LAG batches back
 
 
 class DeltaExchangeFold:
     """Drives one replica through the per-batch fold + exchange.
 
-    `summary` provides: fold_device(src, dst, n=, w=), set_delta_tracking(bool),
-    take_delta_device(a, b, w) -> count, sync(), and optionally `stream`
-    (gelly_streaming_amd.Summary does; the CPU tests plug an oracle-backed replica).
+    `summary` provides fold_device(src, dst, n=), set_delta_tracking(bool),
+    delta_stage(send, cap), fold_exchange(recv, world, rows, skip_rank), sync()
+    and `stream` (gelly_streaming_amd.Summary does; CPU tests plug a model
+    replica whose stream is None).
     """
 
-    def __init__(self, summary, delta_capacity, device, group=None):
+    def __init__(self, summary, batch, device, group=None, first_cap=None, retune=4):
         self.s = summary
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.a = torch.empty(delta_capacity, dtype=torch.int64, device=device)
-        self.b = torch.empty(delta_capacity, dtype=torch.int64, device=device)
-        self.w = torch.empty(delta_capacity, dtype=torch.uint8, device=device)
-        self.exchanged = 0  # delta records received from other ranks
+        self.dev = torch.device(device)
+        self.cuda = self.dev.type == "cuda"
+        self.nccl = self.cuda and dist.get_backend(group) == "nccl"
+        self.max_cap = 3 * int(batch)  # a fold records at most 3 per edge
+        self.first_cap = min(int(first_cap) if first_cap else int(batch), self.max_cap)
+        self.retune = int(retune)
+        rows = self.max_cap + 1
+        self.send = [torch.empty((rows, 3), dtype=torch.int64, device=self.dev) for _ in range(2)]
+        self.recv = [torch.empty((self.world * rows, 3), dtype=torch.int64, device=self.dev) for _ in range(2)]
+        self.hdr = torch.zeros((self.world, 3), dtype=torch.int64, pin_memory=self.cuda)
+        if self.cuda:
+            self.stream = torch.cuda.ExternalStream(summary.stream, device=self.dev)
+            self.ev_staged = [torch.cuda.Event() for _ in range(2)]
+            self.ev_done = [torch.cuda.Event() for _ in range(2)]
+            self.ev_hdr = torch.cuda.Event()
+        self.rows_received = 0
+        self._reset_state()
         self.s.set_delta_tracking(True)
 
-    def step(self, src, dst, n, w=None):
-        """Fold this rank's part of one global micro-batch, then combine."""
-        self.s.fold_device(src, dst, n=n, w=w)
-        k = self.s.take_delta_device(self.a, self.b, self.w)
-        self.s.sync()  # packed delta complete before the collective reads it
-        parts = all_gather_varlen(self.a, self.b, self.w, k, self.group)
-        if self.a.is_cuda:
-            torch.cuda.current_stream().synchronize()  # gathered payload complete
-        self.s.set_delta_tracking(False)  # applied deltas are not re-broadcast
-        for r, (pa, pb, pw) in enumerate(parts):
-            if r == self.rank or pa.numel() == 0:
-                continue
-            self.s.fold_device(pa, pb, n=pa.numel(), w=pw)
-            self.exchanged += pa.numel()
-        self.s.sync()  # the gathered buffers stay alive until the fold has read them
-        self.s.set_delta_tracking(True)
+    # ---------------------------------------------------------------- public
+    def step(self, src, dst, n):
+        """Fold this rank's part of one global micro-batch; exchange it
+        asynchronously and apply the previous batch's remote rows."""
+        b = self.b
+        self.b += 1
+        self.s.fold_device(src, dst, n=n)
+        self._exchange(b, self.cap, apply_now=False)
+        self._after(b)
+
+    def finish(self):
+        """Apply the last exchange and drain every rank's backlog; afterwards all
+        replicas hold the union of every rank's folds."""
+        if self.pending is not None:
+            self._apply(*self.pending)
+            self.pending = None
+        while self.b > 0:
+            remaining = self._remaining_after_last()
+            if remaining == 0:
+                break
+            b = self.b
+            self.b += 1
+            self._exchange(b, min(remaining, self.max_cap), apply_now=True)
+        self.s.sync()
+        self._reset_state()
+
+    # ---------------------------------------------------------------- internals
+    def _reset_state(self):
+        self.b = 0
+        self.cap = self.first_cap
+        self.pending = None
+        self.hdr_batch = -1
+        self.last_rows = 0
+
+    def _exchange(self, b, cap, apply_now):
+        k = b % 2
+        rows = cap + 1
+        send = self.send[k][:rows]
+        recv = self.recv[k][: self.world * rows]
+        self.s.delta_stage(send, cap)
+        if self.nccl:
+            self.ev_staged[k].record(self.stream)
+            cur = torch.cuda.current_stream(self.dev)
+            cur.wait_event(self.ev_staged[k])
+            dist.all_gather_into_tensor(recv, send, group=self.group)
+            self.ev_done[k].record(cur)
+            done = self.ev_done[k]
+            if (b + HDR_LAG) % self.retune == 0:  # headers for the retune HDR_LAG batches later
+                self.hdr.copy_(recv.view(self.world, rows, 3)[:, 0, :], non_blocking=True)
+                self.ev_hdr.record(cur)
+                self.hdr_batch = b
+        else:  # gloo: stage through host memory (CPU tests, several ranks on one GPU)
+            self.s.sync()
+            local = send.cpu()
+            parts = [torch.empty_like(local) for _ in range(self.world)]
+            dist.all_gather(parts, local, group=self.group)
+            recv.copy_(torch.cat(parts))
+            if (b + HDR_LAG) % self.retune == 0:
+                self.hdr.copy_(torch.stack([p[0] for p in parts]))
+                self.hdr_batch = b
+            done = None
+        item = (recv, done, rows)
+        if apply_now:
+            self._apply(*item)
+        else:
+            if self.pending is not None:
+                self._apply(*self.pending)
+            self.pending = item
+
+    def _after(self, b):
+        # every `retune` batches all ranks re-derive cap from the same gathered headers
+        if b % self.retune == 0 and b >= HDR_LAG and self.hdr_batch == b - HDR_LAG:
+            if self.cuda:
+                self.ev_hdr.synchronize()
+            queued = int(self.hdr[:, 1].max())
+            self.cap = int(min(self.max_cap, max(4096, queued + queued // 4 + 1024)))
+
+    def _remaining_after_last(self):
+        """Largest backlog any rank still holds after the last exchange (from its
+        gathered headers; synchronous -- only used by finish())."""
+        if self.last_rows == 0:
+            return 0
+        recv = self.recv[(self.b - 1) % 2][: self.world * self.last_rows]
+        if self.cuda:
+            torch.cuda.synchronize(self.dev)
+        h = recv.view(self.world, self.last_rows, 3)[:, 0, :].cpu()
+        return int((h[:, 1] - h[:, 0]).max())
+
+    def _apply(self, recv, done, rows):
+        self.last_rows = rows
+        if self.world == 1:
+            return
+        if done is not None:
+            self.stream.wait_event(done)  # fold behind the collective, no host sync
+        self.s.fold_exchange(recv, self.world, rows, self.rank)
+        self.rows_received += (self.world - 1) * rows
+        self.last_rows = rows

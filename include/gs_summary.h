@@ -125,14 +125,33 @@ int gs_serialize(gs_handle h, void* buf, size_t cap, size_t* len);
 int gs_deserialize(gs_handle h, const void* buf, size_t len);
 
 /* ---- streaming delta (multi-GPU combine; see DESIGN.md "Multi-GPU") ----------
- * While tracking is on, every fold records the structural changes it made as
- * (key, key2, parity) triples: each newly seen vertex as (v, v, 0) and each
- * successful hook as (root, new parent, parity). Folding another replica's delta
- * into this summary reproduces that replica's changes (union is associative and
- * commutative). gs_take_delta_device packs the delta since the previous take into
- * DEVICE arrays and clears it. */
+ * While tracking is on, every fold records the structural changes it made:
+ * each successful hook as (root, new parent, parity) and each new vertex seen
+ * only through a self-loop as (v, v, 0) (every other new vertex is named by a
+ * hook record). Folding another
+ * replica's delta into this summary reproduces that replica's changes (union is
+ * associative and commutative), which replaces shipping whole summaries to one
+ * reducer (SummaryBulkAggregation.java:77-83).
+ *
+ * Wire format: int64 records {a, b, w}, 24 bytes each; w bit 0 = parity,
+ * w bit 7 = skip (padding). gs_take_delta_records packs the delta accumulated
+ * since the previous take into DEVICE records (first `cap`) and writes the total
+ * record count to the DEVICE word *count; both complete on the handle's stream
+ * (no host synchronisation). gs_fold_records_device folds such records
+ * (track = 0: apply another replica's delta without re-recording it).
+ *
+ * gs_delta_stage is the exchange form: it fills a send buffer of cap + 1
+ * records -- row 0 = header {sent, queued, skip}, rows 1..sent = records (rows
+ * past `sent` are left untouched) -- and keeps the records past `cap` queued for
+ * the next stage, so every rank can all-gather (cap + 1) rows with a capacity
+ * agreed in advance, without a host synchronisation. gs_fold_exchange_device
+ * folds a gathered buffer of world x rows such records (each rank's header says
+ * how many of its rows are live), skipping rank `skip_rank` (the caller's own). */
 int gs_set_delta_tracking(gs_handle h, int on);
-int gs_take_delta_device(gs_handle h, int64_t* a, int64_t* b, uint8_t* w, size_t cap, size_t* n);
+int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count);
+int gs_delta_stage(gs_handle h, int64_t* send, size_t cap);
+int gs_fold_records_device(gs_handle h, const int64_t* rec, size_t n, int track);
+int gs_fold_exchange_device(gs_handle h, const int64_t* recv, size_t world, size_t rows, int skip_rank);
 
 /* ---- introspection -----------------------------------------------------------
  * The HIP stream (hipStream_t) the handle enqueues on, and per-kernel timing:

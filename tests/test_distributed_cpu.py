@@ -4,7 +4,8 @@ micro-batch and exchanges its structural delta; afterwards every rank's replica
 must equal the whole stream folded by the oracle (bit-exact canonical labels).
 
 The device summary is replaced by `ModelReplica`, a CPU model of the C-ABI delta
-contract (include/gs_summary.h: gs_set_delta_tracking / gs_take_delta_device):
+contract (include/gs_summary.h: gs_set_delta_tracking / gs_delta_stage /
+gs_fold_exchange_device):
 new vertices as (v, v, 0), successful hooks as (root, new parent, parity)."""
 import os
 import socket
@@ -17,7 +18,9 @@ import torch.multiprocessing as mp
 
 
 class ModelReplica:
-    """Union-find with min-key hooking and delta recording (test model)."""
+    """Union-find with min-key hooking and delta recording (test model of the
+    device replica: records are hooks (root, new parent, 0) and self-loop-only
+    new vertices (v, v, 0))."""
 
     def __init__(self):
         self.parent = {}
@@ -30,18 +33,20 @@ class ModelReplica:
             v = self.parent[v]
         return v
 
-    def _touch(self, v):
+    def _touch(self, v, self_loop):
         if v not in self.parent:
             self.parent[v] = v
-            if self.track:
+            # only a new vertex seen through a self-loop gets its own record; any
+            # other new vertex is named by a hook record
+            if self.track and self_loop:
                 self.delta.append((v, v, 0))
 
     def fold_device(self, src, dst, n=None, w=None, stride=1):
         s = src[:n].tolist()
         d = dst[:n].tolist()
         for a, b in zip(s, d):
-            self._touch(a)
-            self._touch(b)
+            self._touch(a, a == b)
+            self._touch(b, a == b)
             ra, rb = self._find(a), self._find(b)
             if ra == rb:
                 continue
@@ -53,16 +58,34 @@ class ModelReplica:
     def set_delta_tracking(self, on=True):
         self.track = bool(on)
         self.delta = []
+        self.queue = []
 
-    def take_delta_device(self, a, b, w):
-        k = len(self.delta)
-        if k:
-            arr = torch.tensor(self.delta, dtype=torch.int64)
-            a[:k] = arr[:, 0]
-            b[:k] = arr[:, 1]
-            w[:k] = arr[:, 2].to(torch.uint8)
+    def _pack(self):
+        self.queue += self.delta
         self.delta = []
-        return k
+
+    def delta_stage(self, send, cap):
+        """gs_delta_stage: header {sent, queued, skip}, then up to cap records."""
+        self._pack()
+        total = len(self.queue)
+        sent = min(total, cap)
+        send[0] = torch.tensor([sent, total, 0x80])
+        if sent:
+            send[1:sent + 1] = torch.tensor(self.queue[:sent], dtype=torch.int64)
+        self.queue = self.queue[sent:]
+
+    def fold_exchange(self, recv, world, rows, skip_rank):
+        saved = self.track
+        self.track = False
+        for r in range(world):
+            if r == skip_rank:
+                continue
+            block = recv[r * rows:(r + 1) * rows]
+            live = int(block[0, 0])
+            rec = block[1:live + 1]
+            rec = rec[(rec[:, 2] & 0x80) == 0]
+            self.fold_device(rec[:, 0], rec[:, 1], n=len(rec))
+        self.track = saved
 
     def sync(self):
         pass
@@ -88,7 +111,7 @@ def _worker(rank, world, port, src, dst, batch, out):
     from gelly_streaming_amd.distributed import DeltaExchangeFold
 
     rep = ModelReplica()
-    x = DeltaExchangeFold(rep, 3 * batch * world + 16, torch.device("cpu"))
+    x = DeltaExchangeFold(rep, batch, torch.device("cpu"), first_cap=max(1, batch // 16), retune=4)
     s = torch.from_numpy(src)
     d = torch.from_numpy(dst)
     g = batch * world
@@ -96,8 +119,9 @@ def _worker(rank, world, port, src, dst, batch, out):
         lo = o + rank * batch
         n = max(0, min(batch, len(src) - lo))
         x.step(s[lo:], d[lo:], n)
+    x.finish()
     v, lab = rep.labels()
-    out[rank] = (v.tolist(), lab.tolist(), x.exchanged)
+    out[rank] = (v.tolist(), lab.tolist(), x.rows_received)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -37,14 +37,15 @@ def _worker(rank, world, port, scale, nedges, batch, out):
     dst = torch.empty(nedges, dtype=torch.int64, device=dev)
     gs.gen_rmat(src, dst, 0, nedges, scale, 0x5EED0026, True)
     torch.cuda.synchronize()
-    x = DeltaExchangeFold(summ, 3 * batch, dev)
+    x = DeltaExchangeFold(summ, batch, dev, first_cap=batch // 64, retune=4)
     g = batch * world
     for o in range(0, nedges, g):
         lo = o + rank * batch
         n = max(0, min(batch, nedges - lo))
         x.step(src[lo:], dst[lo:], n)
+    x.finish()
     v, lab = summ.labels()
-    out[rank] = (v.tobytes(), lab.tobytes(), x.exchanged)
+    out[rank] = (v.tobytes(), lab.tobytes(), x.rows_received)
     summ.close()
     dist.barrier()
     dist.destroy_process_group()

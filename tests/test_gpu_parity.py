@@ -199,32 +199,79 @@ def test_serialize_roundtrip(gs, oracle_mod):
 
 
 def test_delta_exchange_reproduces_union(gs, oracle_mod):
-    # Two replicas fold disjoint halves of each batch and fold each other's delta:
-    # afterwards both equal the whole stream (the multi-GPU combine step).
+    # Two replicas fold disjoint halves of each batch and fold each other's delta
+    # records: afterwards both equal the whole stream (the multi-GPU combine step).
     import torch
     s, d = oracle_mod.rmat_edges(5, 14, 0, 1 << 16, True)
     reps = [gs.Summary("cc", capacity_hint=1 << 13) for _ in range(2)]
     for r in reps:
         r.set_delta_tracking(True)
-    cap = 3 << 16
-    bufs = [[torch.empty(cap, dtype=torch.int64, device="cuda"), torch.empty(cap, dtype=torch.int64, device="cuda"),
-             torch.empty(cap, dtype=torch.uint8, device="cuda")] for _ in range(2)]
     B = 1 << 12
+    cap = 3 * B
+    recs = [torch.empty((cap, 3), dtype=torch.int64, device="cuda") for _ in range(2)]
+    cnts = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(2)]
+    total = 0
     for i in range(0, len(s), 2 * B):
         reps[0].fold(s[i:i + B], d[i:i + B])
         reps[1].fold(s[i + B:i + 2 * B], d[i + B:i + 2 * B])
-        ns = [reps[k].take_delta_device(*bufs[k]) for k in range(2)]
-        for r in reps:
-            r.sync()
-            r.set_delta_tracking(False)  # applied deltas are not re-broadcast
         for k in range(2):
-            reps[1 - k].fold_device(bufs[k][0], bufs[k][1], n=ns[k])
-        for r in reps:
-            r.sync()
-            r.set_delta_tracking(True)
+            reps[k].take_delta_records(recs[k], cap, cnts[k])
+            reps[k].sync()
+        ns = [int(c.item()) for c in cnts]
+        assert max(ns) <= cap
+        total += sum(ns)
+        for k in range(2):
+            reps[1 - k].fold_records(recs[k], ns[k], track=False)
     for r in reps:
         _assert_cc_equal(r, oracle_mod, s, d)
         r.close()
+    # hooked new vertices are filtered: far fewer records than 2 per edge + hooks
+    assert total < len(s)
+
+
+def test_delta_stage_backlog_and_exchange_fold(gs, oracle_mod):
+    # gs_delta_stage with a small cap keeps a backlog; folding the gathered buffers
+    # (gs_fold_exchange_device) until every backlog is empty reproduces the union.
+    import torch
+    s, d = oracle_mod.rmat_edges(6, 13, 0, 1 << 15, True)
+    world, B, cap = 3, 1 << 11, 300
+    reps = [gs.Summary("cc", capacity_hint=1 << 12) for _ in range(world)]
+    for r in reps:
+        r.set_delta_tracking(True)
+    sends = [torch.empty((cap + 1, 3), dtype=torch.int64, device="cuda") for _ in range(world)]
+
+    def exchange():
+        for r in range(world):
+            reps[r].delta_stage(sends[r], cap)
+            reps[r].sync()
+        recv = torch.cat(sends)
+        for r in range(world):
+            reps[r].fold_exchange(recv, world, cap + 1, r)
+        hdr = recv.view(world, cap + 1, 3)[:, 0, :].cpu()
+        return int((hdr[:, 1] - hdr[:, 0]).max())
+
+    backlog_seen = 0
+    for i in range(0, len(s), world * B):
+        for r in range(world):
+            lo = i + r * B
+            reps[r].fold(s[lo:lo + B], d[lo:lo + B])
+        backlog_seen = max(backlog_seen, exchange())
+    while exchange() > 0:
+        pass
+    exchange()  # headers of a drained round are all empty
+    assert backlog_seen > 0  # the small cap forced a backlog
+    for r in reps:
+        _assert_cc_equal(r, oracle_mod, s, d)
+        r.close()
+
+
+def test_delta_records_skip_padding(gs, oracle_mod):
+    import torch
+    rec = torch.tensor([[1, 2, 0], [3, 4, 0x80], [5, 6, 0], [7, 7, 0x80]], dtype=torch.int64, device="cuda")
+    with gs.Summary("cc", capacity_hint=64) as a:
+        a.fold_records(rec, 4)
+        v, lab = a.labels()
+        assert v.tolist() == [1, 2, 5, 6] and lab.tolist() == [1, 1, 5, 5]
 
 
 # ------------------------------------------------------------- bipartiteness
