@@ -52,9 +52,18 @@ struct gs_summary {
   int kind = GS_KIND_CC;
   hipStream_t stream = nullptr;
   // table
-  gs::Slot* tab = nullptr;
+  gs::Slot* tab = nullptr;  // [hotcap | cap | 2 reserved]
   uint64_t cap = 0;
   int logcap = 0;
+  // hot level (gs_device.hpp): open while fewer than hot_target vertices are known;
+  // the count is read back asynchronously (pinned copy + event), never synchronously
+  uint64_t hotcap = 0;
+  int loghot = 0;
+  bool hot_open = false;
+  uint64_t hot_target = 0;
+  uint32_t* h_nv = nullptr;  // pinned copy of the new-vertex counter block
+  hipEvent_t nv_ev = nullptr;
+  bool nv_pending = false;
   uint32_t* ctr = nullptr;
   uint64_t nv_ub = 0;  // host upper bound of the vertex count
   // lists
@@ -101,9 +110,14 @@ struct gs_summary {
     gs::Table t;
     t.tab = tab;
     t.ctr = ctr;
-    t.capidx = (uint32_t)cap;
+    t.hotcap = (uint32_t)hotcap;
+    t.hotmask = hotcap ? (uint32_t)(hotcap - 1) : 0u;
+    t.hotshift = hotcap ? 64 - loghot : 0;
+    t.hot_open = hot_open ? 1 : 0;
+    t.cap = (uint32_t)cap;
     t.mask = (uint32_t)(cap - 1);
     t.shift = 64 - logcap;
+    t.r0 = (uint32_t)(hotcap + cap);
     return t;
   }
   gs::Lists lists() const {
@@ -198,7 +212,12 @@ int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
   h->cap = cap;
   h->logcap = 0;
   while ((1ull << h->logcap) < cap) ++h->logcap;
-  GS_HIP(hipMalloc(&h->tab, (cap + 1) * sizeof(gs::Slot)));
+  h->loghot = 0;
+  while (h->hotcap && (1ull << h->loghot) < h->hotcap) ++h->loghot;
+  h->hot_open = h->hotcap > 0;
+  h->hot_target = h->hotcap / 2;
+  h->nv_pending = false;
+  GS_HIP(hipMalloc(&h->tab, (h->hotcap + cap + 2) * sizeof(gs::Slot)));
   if (keep_delta) {
     GS_HIP(hipMemsetAsync(h->ctr, 0, gs::ctr_index(gs::CTR_DELTA) * 4, h->stream));
     GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 0,
@@ -208,7 +227,7 @@ int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
   }
   {
     Prof p(h, KID_INIT);
-    gs::launch_init(h->tab, cap + 1, h->stream);
+    gs::launch_init(h->tab, h->hotcap + cap + 2, h->stream);
   }
   GS_HIP(hipGetLastError());
   h->nv_ub = 0;
@@ -331,6 +350,12 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     const int zero = (int)((h->epoch + 1) % gs::kActSets);
     const int inline_max = h->mode == gs_summary::FUSED ? 64 : (h->mode == gs_summary::COMPACT ? 0 : h->inline_max);
     const int drain = h->mode == gs_summary::DEFER ? h->pending : -1;
+    if (h->hot_open && h->nv_pending && hipEventQuery(h->nv_ev) == hipSuccess) {
+      uint64_t nv = 0;
+      for (int i = 0; i < gs::kShards; ++i) nv += h->h_nv[gs::ctr_index(gs::CTR_NV + i)];
+      h->nv_pending = false;
+      if (nv >= h->hot_target) h->hot_open = false;
+    }
     {
       Prof p(h, KID_FOLD);
       gs::launch_fold(sign, track, h->ept, h->table(), h->lists(), src + off * stride, dst + off * stride,
@@ -338,6 +363,12 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
                       inline_max, xl.rows, xl.skip_rank, xl.base, (uint32_t)off, h->stream);
     }
     GS_HIP(hipGetLastError());
+    if (h->hot_open && !h->nv_pending) {  // vertex count for the next hot-level decision
+      GS_HIP(hipMemcpyAsync(h->h_nv, h->ctr + gs::ctr_index(gs::CTR_NV), gs::kShards * gs::kCtrStride * 4,
+                            hipMemcpyDeviceToHost, h->stream));
+      GS_HIP(hipEventRecord(h->nv_ev, h->stream));
+      h->nv_pending = true;
+    }
     h->epoch++;
     h->pending = h->mode == gs_summary::FUSED ? -1 : cur;
     h->pending_track = track;
@@ -384,6 +415,14 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   }
   if (const char* m = getenv("GS_INLINE_MAX")) h->inline_max = std::max(0, std::min(64, atoi(m)));
   if (const char* m = getenv("GS_EPT")) h->ept = atoi(m) == 2 ? 2 : 1;
+  // hot level (opt-in, GS_HOT_LOG2 = log2 slots): measured slower on RMAT-26 at every
+  // size from 2^16 to 2^23 slots, so it is off by default
+  {
+    if (const char* m = getenv("GS_HOT_LOG2")) {
+      const int lg = atoi(m);
+      h->hotcap = (lg > 0 && lg <= 26) ? (1ull << lg) : 0;
+    }
+  }
   uint64_t cap = next_pow2(std::max<uint64_t>(2 * std::max<uint64_t>(capacity_hint, 1), 1024));
   if (cap > kMaxCap) cap = kMaxCap;
   int rc = GS_OK;
@@ -407,6 +446,9 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   for (int i = 0; i < 2; ++i)
     if (hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming) != hipSuccess)
       return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
+  if (hipEventCreateWithFlags(&h->nv_ev, hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc(&h->h_nv, gs::kShards * gs::kCtrStride * 4, hipHostMallocDefault) != hipSuccess)
+    return bail(fail(GS_ERR_HIP, "hot-level bookkeeping allocation failed"));
   rc = alloc_table(h, cap);
   if (rc) return bail(rc);
   if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "init failed"));
@@ -422,6 +464,8 @@ int gs_destroy(gs_handle h) {
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 2; ++i)
     if (h->stage_ev[i]) (void)hipEventDestroy(h->stage_ev[i]);
+  if (h->nv_ev) (void)hipEventDestroy(h->nv_ev);
+  if (h->h_nv) (void)hipHostFree(h->h_nv);
   (void)hipFree(h->tab);
   (void)hipFree(h->ctr);
   (void)hipFree(h->act);
@@ -445,8 +489,10 @@ int gs_reset(gs_handle h) {
   GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
   {
     Prof p(h, KID_INIT);
-    gs::launch_init(h->tab, h->cap + 1, h->stream);
+    gs::launch_init(h->tab, h->hotcap + h->cap + 2, h->stream);
   }
+  h->hot_open = h->hotcap > 0;
+  h->nv_pending = false;
   GS_HIP(hipGetLastError());
   if (h->qn) GS_HIP(hipMemsetAsync(h->qn, 0, 16, h->stream));
   h->nv_ub = 0;
@@ -826,7 +872,7 @@ int gs_kernel_stats(gs_handle h, int id, uint64_t* launches, double* total_ms) {
 int gs_table_capacity(gs_handle h, uint64_t* slots) {
   if (int rc = check(h)) return rc;
   if (!slots) return fail(GS_ERR_INVALID, "slots is null");
-  *slots = h->cap;
+  *slots = h->hotcap + h->cap;
   return GS_OK;
 }
 

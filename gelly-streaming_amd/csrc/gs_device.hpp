@@ -29,7 +29,12 @@
 namespace gs {
 
 constexpr int64_t kEmpty = INT64_MIN;
+constexpr int64_t kSealed = INT64_MIN + 1;  // hot-level slot closed to inserts (the id itself lives in slot r0 + 1)
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+#ifndef GS_HOT_BUCKET
+#define GS_HOT_BUCKET 4
+#endif
+constexpr uint32_t kHotBucket = GS_HOT_BUCKET;  // hot-level bucket: slots loaded in one round trip
 constexpr int kShards = 64;      // sharded append counters (one 128-B line each)
 constexpr int kCtrStride = 32;   // u32 per counter line
 constexpr int kActSets = 3;     // active-edge lists: appended at epoch e, drained at e+1, zeroed at e+2
@@ -54,12 +59,21 @@ struct alignas(16) Slot {
   uint32_t aux;   // bit 0: reserved slot present
 };
 
+// Slot index space: [0, hotcap) hot level | [hotcap, hotcap + cap) cold level |
+// r0 = hotcap + cap (id INT64_MIN) | r0 + 1 (id INT64_MIN + 1). The hot level holds
+// the vertices inserted while it is open -- in a skewed stream the early, high-
+// degree ones -- densely enough to stay resident in the Infinity Cache.
 struct Table {
   Slot* tab;
   uint32_t* ctr;
-  uint32_t capidx;  // == cap: index of the reserved INT64_MIN slot
+  uint32_t hotcap;  // 0: no hot level
+  uint32_t hotmask;
+  int hotshift;
+  int hot_open;     // inserts may go to the hot level
+  uint32_t cap;     // cold level size (power of two)
   uint32_t mask;    // cap - 1
   int shift;        // 64 - log2(cap)
+  uint32_t r0;      // reserved slots r0 (INT64_MIN) and r0 + 1 (INT64_MIN + 1)
 };
 
 struct Lists {
@@ -72,6 +86,14 @@ struct Lists {
 __device__ __forceinline__ uint32_t hash_slot(int64_t key, int shift) {
   return (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ull) >> shift);
 }
+
+// Slot of a key's first probe: its hot bucket's first slot if there is a hot level
+// (buckets are kHotBucket aligned slots), else the cold level.
+__device__ __forceinline__ uint32_t first_probe_slot(const Table& t, int64_t key) {
+  return t.hotcap ? (hash_slot(key, t.hotshift) & ~(kHotBucket - 1)) : hash_slot(key, t.shift);
+}
+
+__device__ __forceinline__ bool is_reserved_key(int64_t key) { return key == kEmpty || key == kSealed; }
 
 __device__ __forceinline__ void load_slot(const Slot* p, int64_t& key, uint32_t& link) {
   // one 16-B load (global_load_dwordx4): key + link in the same request
@@ -87,24 +109,83 @@ __device__ __forceinline__ uint32_t load_link_fresh(const Slot* p) {
 // A key read as EMPTY for an occupied slot is a stale line: settle it at the
 // memory-side atomic unit (rare path).
 __device__ __forceinline__ int64_t settle_key(const Table& t, uint32_t s, int64_t k) {
-  if (k == kEmpty && s != t.capidx) {
+  if (k == kEmpty && s != t.r0) {
     k = (int64_t)atomicOr((unsigned long long*)&t.tab[s].key, 0ull);
   }
   return k;
 }
 
-// Insert-or-find of one id whose first probe slot h was already loaded as (k, l)
-// (callers issue both endpoints' first loads back to back so they overlap).
-// Returns the slot (dense id), the slot's observed link and whether this call
-// inserted it. Linear probing over 16-B slots (4 per 64-B line).
+// Hot level: a key lives in its bucket (kHotBucket aligned slots) or not at all.
+// The whole bucket is read at once (independent 16-B loads, one round trip) and
+// scanned in registers. While the level is open an EMPTY slot is claimed by CAS;
+// once closed, the first EMPTY slot of the bucket is sealed (CAS EMPTY -> kSealed)
+// so nothing can be inserted there later: a lookup that meets a seal, or a full
+// bucket of other keys, continues in the cold level. A key is therefore in at most
+// one level. Returns the slot, or kNoSlot to continue in the cold level.
+struct HotBucket {
+  int64_t k[kHotBucket];
+  uint32_t l[kHotBucket];
+};
+
+__device__ __forceinline__ void load_bucket(const Table& t, uint32_t b0, HotBucket& hb) {
+#pragma unroll
+  for (uint32_t i = 0; i < kHotBucket; ++i) load_slot(t.tab + b0 + i, hb.k[i], hb.l[i]);
+}
+
+// (the bucket at b0 was loaded into hb by the caller)
+__device__ __forceinline__ uint32_t hot_resolve(const Table& t, int64_t key, uint32_t b0, const HotBucket& hb,
+                                                uint32_t& link, bool& fresh) {
+  const int64_t* k = hb.k;
+  const uint32_t* l = hb.l;
+#pragma unroll
+  for (uint32_t i = 0; i < kHotBucket; ++i) {
+    if (k[i] == key) {
+      link = l[i];
+      return b0 + i;
+    }
+  }
+  for (uint32_t i = 0; i < kHotBucket; ++i) {
+    int64_t ki = k[i];
+    if (ki == kEmpty) {
+      const int64_t want = t.hot_open ? key : kSealed;
+      const unsigned long long old = atomicCAS((unsigned long long*)&t.tab[b0 + i].key, (unsigned long long)kEmpty,
+                                               (unsigned long long)want);
+      if (old == (unsigned long long)kEmpty) {
+        if (!t.hot_open) return kNoSlot;
+        fresh = true;
+        link = (b0 + i) << 1;
+        return b0 + i;
+      }
+      ki = (int64_t)old;
+      if (ki == key) {
+        link = t.tab[b0 + i].link;
+        return b0 + i;
+      }
+    }
+    if (ki == kSealed) return kNoSlot;
+  }
+  return kNoSlot;  // bucket full of other keys
+}
+
+// Insert-or-find of one id. Its first probe was already loaded by the caller
+// (callers issue both endpoints' first loads back to back so they overlap): with a
+// hot level the bucket at h into hb, else the cold slot h into (k, l). Returns the
+// slot (dense id), its observed link and whether this call inserted it.
 __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, uint32_t h, int64_t k, uint32_t l,
-                                                   uint32_t& link, bool& fresh) {
+                                                   const HotBucket& hb, uint32_t& link, bool& fresh) {
   fresh = false;
-  if (key == kEmpty) {
-    const uint32_t old = atomicOr(&t.tab[t.capidx].aux, 1u);
+  if (is_reserved_key(key)) {
+    const uint32_t r = t.r0 + (key == kSealed ? 1u : 0u);
+    const uint32_t old = atomicOr(&t.tab[r].aux, 1u);
     fresh = (old & 1u) == 0;
-    link = t.capidx << 1;  // the minimum id is always a root
-    return t.capidx;
+    link = t.tab[r].link;
+    return r;
+  }
+  if (t.hotcap) {
+    const uint32_t s = hot_resolve(t, key, h, hb, link, fresh);
+    if (s != kNoSlot) return s;
+    h = t.hotcap + hash_slot(key, t.shift);
+    load_slot(t.tab + h, k, l);
   }
   for (uint32_t probes = 0; probes <= t.mask; ++probes) {
     if (k == key) {
@@ -124,7 +205,7 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
         return h;
       }
     }
-    h = (h + 1) & t.mask;
+    h = t.hotcap + ((h - t.hotcap + 1) & t.mask);
     load_slot(t.tab + h, k, l);
   }
   atomicOr(&t.ctr[ctr_index(CTR_ERR)], 1u);
@@ -132,11 +213,41 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
 }
 
 __device__ __forceinline__ uint32_t lookup_insert(const Table& t, int64_t key, uint32_t& link, bool& fresh) {
-  const uint32_t h = hash_slot(key, t.shift);
+  const uint32_t h = first_probe_slot(t, key);
+  int64_t k = 0;
+  uint32_t l = 0;
+  HotBucket hb;
+  if (t.hotcap)
+    load_bucket(t, h, hb);
+  else
+    load_slot(t.tab + h, k, l);
+  return lookup_resolve(t, key, h, k, l, hb, link, fresh);
+}
+
+// Read-only lookup (no insert, no seal): slot or kNoSlot.
+__device__ __forceinline__ uint32_t lookup_find(const Table& t, int64_t key, uint32_t& link) {
+  if (is_reserved_key(key)) {
+    const uint32_t r = t.r0 + (key == kSealed ? 1u : 0u);
+    link = t.tab[r].link;
+    return (t.tab[r].aux & 1u) ? r : kNoSlot;
+  }
   int64_t k;
-  uint32_t l;
-  load_slot(t.tab + h, k, l);
-  return lookup_resolve(t, key, h, k, l, link, fresh);
+  if (t.hotcap) {
+    const uint32_t b0 = hash_slot(key, t.hotshift) & ~(kHotBucket - 1);
+    for (uint32_t i = 0; i < kHotBucket; ++i) {
+      load_slot(t.tab + b0 + i, k, link);
+      if (k == key) return b0 + i;
+      if (k == kEmpty || k == kSealed) break;
+    }
+  }
+  uint32_t h = t.hotcap + hash_slot(key, t.shift);
+  for (uint32_t probes = 0; probes <= t.mask; ++probes) {
+    load_slot(t.tab + h, k, link);
+    if (k == key) return h;
+    if (k == kEmpty) return kNoSlot;
+    h = t.hotcap + ((h - t.hotcap + 1) & t.mask);
+  }
+  return kNoSlot;
 }
 
 // One step of a find with path splitting. (x, lx, kx): current slot, its link and

@@ -15,12 +15,13 @@
 
 namespace gs {
 
+// slot s := {EMPTY, s << 1, 0}; the second reserved slot carries its id INT64_MIN + 1
 __global__ __launch_bounds__(256) void k_init(Slot* tab, uint64_t nslots) {
   for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
        s += (uint64_t)gridDim.x * blockDim.x) {
     uint4 v;
-    v.x = 0u;
-    v.y = 0x80000000u;  // INT64_MIN
+    v.x = (s == nslots - 1) ? 1u : 0u;
+    v.y = 0x80000000u;  // INT64_MIN (+1 for the last slot)
     v.z = (uint32_t)(s << 1);
     v.w = 0u;
     *reinterpret_cast<uint4*>(tab + s) = v;
@@ -82,8 +83,9 @@ struct FoldArgs {
   int inline_max;
 };
 
-template <bool SIGNED, bool TRACK, int EPT>
+template <bool SIGNED, bool TRACK, int EPT, bool HOT>
 __global__ __launch_bounds__(256) void k_fold(Table t, Lists L, FoldArgs a) {
+  if (!HOT) t.hotcap = 0;  // compile-time: the plain path carries no hot-level code
   if (SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0) return;
   const int shard = blockIdx.x & (kShards - 1);
   if (a.zero >= 0 && blockIdx.x == 0 && threadIdx.x < kShards)
@@ -110,13 +112,21 @@ __global__ __launch_bounds__(256) void k_fold(Table t, Lists L, FoldArgs a) {
   // all first relabel probes of the thread in flight together
   uint32_t hu[EPT], hv[EPT], l0u[EPT], l0v[EPT];
   int64_t k0u[EPT], k0v[EPT];
+  HotBucket hbu[HOT ? EPT : 1], hbv[HOT ? EPT : 1];
 #pragma unroll
   for (int e = 0; e < EPT; ++e) {
-    hu[e] = hash_slot(ks[e], t.shift);
-    hv[e] = hash_slot(kd[e], t.shift);
+    hu[e] = first_probe_slot(t, ks[e]);
+    hv[e] = first_probe_slot(t, kd[e]);
+    k0u[e] = k0v[e] = 0;
+    l0u[e] = l0v[e] = 0;
     if (valid[e]) {
-      load_slot(t.tab + hu[e], k0u[e], l0u[e]);
-      load_slot(t.tab + hv[e], k0v[e], l0v[e]);
+      if (HOT) {  // both endpoints' hot buckets in one round trip
+        load_bucket(t, hu[e], hbu[HOT ? e : 0]);
+        load_bucket(t, hv[e], hbv[HOT ? e : 0]);
+      } else {
+        load_slot(t.tab + hu[e], k0u[e], l0u[e]);
+        load_slot(t.tab + hv[e], k0v[e], l0v[e]);
+      }
     }
   }
   uint32_t ru[EPT], rv[EPT], lu[EPT], lv[EPT];
@@ -125,8 +135,8 @@ __global__ __launch_bounds__(256) void k_fold(Table t, Lists L, FoldArgs a) {
   for (int e = 0; e < EPT; ++e) {
     if (!valid[e]) continue;
     bool nu, nv;
-    const uint32_t su = lookup_resolve(t, ks[e], hu[e], k0u[e], l0u[e], lu[e], nu);
-    const uint32_t sv = lookup_resolve(t, kd[e], hv[e], k0v[e], l0v[e], lv[e], nv);
+    const uint32_t su = lookup_resolve(t, ks[e], hu[e], k0u[e], l0u[e], hbu[HOT ? e : 0], lu[e], nu);
+    const uint32_t sv = lookup_resolve(t, kd[e], hv[e], k0v[e], l0v[e], hbv[HOT ? e : 0], lv[e], nv);
     if (nu || nv) atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], (nu ? 1u : 0u) + (nv && sv != su ? 1u : 0u));
     // Delta: a new vertex with an edge to another vertex is always named by a hook
     // record (as the hooked root or as the new parent: its singleton tree can only
@@ -202,7 +212,7 @@ __global__ __launch_bounds__(256) void k_export(Table t, int64_t* __restrict__ o
   constexpr int PER = 16;
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t base_sh;
-  const uint64_t nslots = (uint64_t)t.capidx + 1;
+  const uint64_t nslots = (uint64_t)t.r0 + 2;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (uint64_t tile = (uint64_t)blockIdx.x * (256 * PER); tile < nslots; tile += (uint64_t)gridDim.x * (256 * PER)) {
     int64_t vk[PER], lk[PER];
@@ -218,7 +228,8 @@ __global__ __launch_bounds__(256) void k_export(Table t, int64_t* __restrict__ o
         int64_t k;
         uint32_t l;
         load_slot(t.tab + s, k, l);
-        const bool present = (s == t.capidx) ? ((t.tab[s].aux & 1u) != 0) : (k != kEmpty);
+        const bool present = (s >= t.r0) ? ((t.tab[s].aux & 1u) != 0)
+                                         : (k != kEmpty && !(s < t.hotcap && k == kSealed));
         if (present) {
           uint32_t r, p;
           int64_t rk;
@@ -383,23 +394,8 @@ __global__ void k_find_one(Table t, int64_t key, int64_t* out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   out[0] = 0;
   out[1] = 0;
-  uint32_t s = kNoSlot, l = 0;
-  if (key == kEmpty) {
-    if (t.tab[t.capidx].aux & 1u) s = t.capidx;
-    l = t.capidx << 1;
-  } else {
-    uint32_t h = hash_slot(key, t.shift);
-    for (uint32_t probes = 0; probes <= t.mask; ++probes) {
-      int64_t k;
-      load_slot(t.tab + h, k, l);
-      if (k == key) {
-        s = h;
-        break;
-      }
-      if (k == kEmpty) break;
-      h = (h + 1) & t.mask;
-    }
-  }
+  uint32_t l = 0;
+  const uint32_t s = lookup_find(t, key, l);
   if (s == kNoSlot) return;
   uint32_t r, p;
   int64_t rk;
@@ -422,19 +418,22 @@ void launch_fold(bool sign, bool track, int ept, const Table& t, const Lists& L,
   FoldArgs a{src, dst, w, n, stride, w_stride, rows, skip_rank, hdr, base, cur, drain, zero, inline_max};
   const uint32_t per_block = 256u * (uint32_t)ept;
   const dim3 g((n + per_block - 1) / per_block), b(256);
-#define GS_FOLD(S, T, E)                                                          \
-  if (sign == S && track == T && ept == E) {                                      \
-    hipLaunchKernelGGL((k_fold<S, T, E>), g, b, 0, st, t, L, a);                  \
+  const bool hot = t.hotcap != 0;
+#define GS_FOLD(S, T, E, H)                                                       \
+  if (sign == S && track == T && ept == E && hot == H) {                          \
+    hipLaunchKernelGGL((k_fold<S, T, E, H>), g, b, 0, st, t, L, a);               \
     return;                                                                       \
   }
-  GS_FOLD(false, false, 1)
-  GS_FOLD(false, true, 1)
-  GS_FOLD(true, false, 1)
-  GS_FOLD(true, true, 1)
-  GS_FOLD(false, false, 2)
-  GS_FOLD(false, true, 2)
-  GS_FOLD(true, false, 2)
-  GS_FOLD(true, true, 2)
+#define GS_FOLD_H(S, T, E) GS_FOLD(S, T, E, false) GS_FOLD(S, T, E, true)
+  GS_FOLD_H(false, false, 1)
+  GS_FOLD_H(false, true, 1)
+  GS_FOLD_H(true, false, 1)
+  GS_FOLD_H(true, true, 1)
+  GS_FOLD_H(false, false, 2)
+  GS_FOLD_H(false, true, 2)
+  GS_FOLD_H(true, false, 2)
+  GS_FOLD_H(true, true, 2)
+#undef GS_FOLD_H
 #undef GS_FOLD
 }
 
@@ -447,7 +446,7 @@ void launch_hook(bool sign, bool track, const Table& t, const Lists& L, int set,
 }
 
 void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, hipStream_t st) {
-  const uint64_t nslots = (uint64_t)t.capidx + 1;
+  const uint64_t nslots = (uint64_t)t.r0 + 2;
   const uint64_t tiles = (nslots + 4095) / 4096;
   const unsigned g = (unsigned)(tiles < 4096 ? tiles : 4096);
   if (sign)

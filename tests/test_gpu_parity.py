@@ -395,3 +395,36 @@ def test_hook_policies_agree(gs, oracle_mod, monkeypatch, mode, inline_max, ept)
                 c.fold(bs[i:i + 997], bd[i:i + 997])
             truth = oracle_mod.canonical_candidates_string(*oracle_mod.bip_truth(bs, bd))
             assert oracle_mod.canonical_candidates_string(*c.colouring()) == truth
+
+
+@pytest.mark.parametrize("hot_log2", ["10", "13"])
+def test_hot_level_closure_and_seals(gs, oracle_mod, monkeypatch, hot_log2):
+    # a small hot level fills up, closes (async vertex count) and gets sealed while
+    # the stream goes on: every key must still live in exactly one level
+    monkeypatch.setenv("GS_HOT_LOG2", hot_log2)
+    s, d = oracle_mod.rmat_edges(0x5EED0017, 16, 0, 1 << 19, True)
+    with gs.Summary("cc", capacity_hint=1 << 16) as ds:
+        for i in range(0, len(s), 1 << 13):
+            ds.fold(s[i:i + (1 << 13)], d[i:i + (1 << 13)])
+        _assert_cc_equal(ds, oracle_mod, s, d)
+        v, lab = ds.labels()
+        for k in range(0, len(v), max(1, len(v) // 50)):
+            assert ds.find(int(v[k])) == int(lab[k])
+        assert ds.num_vertices() == len(v)
+    with gs.Summary("signed", capacity_hint=1 << 16) as c:
+        bs, bd = oracle_mod.bip_edges(21, 14, 0, 1 << 17, [1 << 16])
+        for i in range(0, len(bs), 1 << 12):
+            c.fold(bs[i:i + (1 << 12)], bd[i:i + (1 << 12)])
+        assert c.ok() == oracle_mod.bip_truth(bs, bd)[0]
+
+
+def test_reserved_ids_with_hot_level(gs, oracle_mod, monkeypatch):
+    monkeypatch.setenv("GS_HOT_LOG2", "8")
+    ids = np.array([I64_MIN, I64_MIN + 1, I64_MIN + 2, -5, 0, 7, I64_MAX], dtype=np.int64)
+    s = np.array([ids[1], ids[2], ids[3], ids[4], ids[6], ids[0], ids[5]], dtype=np.int64)
+    d = np.array([ids[2], ids[3], ids[1], ids[5], ids[6], ids[0], ids[5]], dtype=np.int64)
+    with gs.Summary("cc", capacity_hint=1 << 16) as ds:
+        ds.fold(s, d)
+        _assert_cc_equal(ds, oracle_mod, s, d)
+        assert ds.find(I64_MIN + 1) == I64_MIN + 1
+        assert ds.find(I64_MIN) == I64_MIN
