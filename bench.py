@@ -43,7 +43,22 @@ def parse():
     p.add_argument("--no-profile-pass", action="store_true")
     p.add_argument("--exchange", action="store_true",
                    help="run the multi-GPU delta-exchange path even at one rank (overhead measurement)")
+    p.add_argument("--exchange-impl", choices=["native", "torch"], default="native",
+                   help="native: RCCL inside libgs_summary (gs_group_*); torch: torch.distributed all-gather")
     return p.parse_args()
+
+
+class NativeExchange:
+    """bench adapter: the same step/finish interface as DeltaExchangeFold."""
+
+    def __init__(self, group):
+        self.g = group
+
+    def step(self, src, dst, n):
+        self.g.fold_device(src, dst, n)
+
+    def finish(self):
+        self.g.finish()
 
 
 def main():
@@ -82,14 +97,19 @@ def main():
     vcap = min(1 << args.scale, 2 * E) + 16
     out_v = torch.empty(vcap, dtype=torch.int64, device=dev)
     out_l = torch.empty(vcap, dtype=torch.int64, device=dev)
-    xch = DeltaExchangeFold(summ, B, dev) if (world > 1 or args.exchange) else None
+    xch = None
+    if world > 1 or args.exchange:
+        if args.exchange_impl == "native":
+            uid = [gs.group_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            xch = NativeExchange(gs.Group(summ, uid[0], world, rank, B))
+        else:
+            xch = DeltaExchangeFold(summ, B, dev)
 
     nlabels = [0]
 
     def one_step():
         summ.reset()
-        if xch is not None:
-            summ.set_delta_tracking(True)
         for b in range(nbatch):
             o = b * B
             n = min(B, per - o)
@@ -180,12 +200,14 @@ def main():
             "config": {"workload": "rmat%d-cc-stream" % args.scale, "scale": args.scale,
                        "edges": E, "micro_batch": B, "ids": "sparse 64-bit (scrambled)",
                        "vertices_labelled": int(nlabels[0]),
-                       "parallelism": "edge-shard x%d, per-batch delta all-gather" % world
+                       "parallelism": ("edge-shard x%d, per-batch delta all-gather (%s)" % (world, args.exchange_impl))
                        if xch is not None else "single GPU"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    if isinstance(xch, NativeExchange):
+        xch.g.close()
     summ.close()
     if dist.is_initialized():
         dist.destroy_process_group()

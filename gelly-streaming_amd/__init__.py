@@ -36,6 +36,8 @@ EXPORTED_SYMBOLS = (
     "gs_take_delta_records", "gs_delta_stage", "gs_fold_records_device", "gs_fold_exchange_device",
     "gs_get_stream", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity",
     "gs_gen_rmat", "gs_gen_er", "gs_gen_bip",
+    "gs_group_unique_id", "gs_group_create", "gs_group_fold_device", "gs_group_finish", "gs_group_stats",
+    "gs_group_destroy",
 )
 
 
@@ -100,6 +102,12 @@ def lib():
     L.gs_gen_rmat.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, ctypes.c_int]
     L.gs_gen_er.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, ctypes.c_int]
     L.gs_gen_bip.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, _vp, _sz]
+    L.gs_group_unique_id.argtypes = [_vp]
+    L.gs_group_create.argtypes = [ctypes.POINTER(_vp), _vp, _vp, ctypes.c_int, ctypes.c_int, _sz, _sz]
+    L.gs_group_fold_device.argtypes = [_vp, _vp, _vp, _sz]
+    L.gs_group_finish.argtypes = [_vp]
+    L.gs_group_stats.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_u64)]
+    L.gs_group_destroy.argtypes = [_vp]
     _lib = L
     return L
 
@@ -282,6 +290,53 @@ class Summary:
         n = _u64()
         _check(lib().gs_table_capacity(self._h, ctypes.byref(n)))
         return n.value
+
+
+# ---------------------------------------------------------------- native multi-GPU group
+GROUP_ID_BYTES = 128
+
+
+def group_unique_id():
+    """RCCL communicator id (bytes) for Group(); create on one rank, share with all."""
+    buf = ctypes.create_string_buffer(GROUP_ID_BYTES)
+    _check(lib().gs_group_unique_id(buf))
+    return buf.raw
+
+
+class Group:
+    """Native multi-GPU combine (include/gs_group.h): per global micro-batch,
+    fold this rank's edges, all-gather the staged delta over RCCL on the
+    summary's stream, fold the other ranks' records. Collective calls."""
+
+    def __init__(self, summary, uid, nranks, rank, batch_edges, first_cap=0):
+        g = _vp()
+        buf = ctypes.create_string_buffer(bytes(uid), GROUP_ID_BYTES)
+        _check(lib().gs_group_create(ctypes.byref(g), summary.handle, buf, int(nranks), int(rank),
+                                     int(batch_edges), int(first_cap)))
+        self._g = g
+        self.summary = summary
+
+    def fold_device(self, src, dst, n):
+        _check(lib().gs_group_fold_device(self._g, _ptr(src), _ptr(dst), int(n)))
+
+    def finish(self):
+        _check(lib().gs_group_finish(self._g))
+
+    def stats(self):
+        e, s, c = _u64(), _u64(), _u64()
+        _check(lib().gs_group_stats(self._g, ctypes.byref(e), ctypes.byref(s), ctypes.byref(c)))
+        return {"exchanges": e.value, "records_sent": s.value, "cap": c.value}
+
+    def close(self):
+        if getattr(self, "_g", None):
+            lib().gs_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # ---------------------------------------------------------------- generators

@@ -877,3 +877,213 @@ int gs_table_capacity(gs_handle h, uint64_t* slots) {
 }
 
 }  // extern "C"
+
+// ============================================================================
+// Native multi-GPU group (include/gs_group.h): RCCL all-gather of staged deltas on
+// the summary's own stream. RCCL is dlopen'ed on first use (librccl.so.1; in a
+// process that already loaded torch this resolves to torch's copy).
+// ============================================================================
+#include <dlfcn.h>
+
+#include "gs_group.h"
+
+namespace {
+
+struct RcclApi {
+  void* lib = nullptr;
+  int (*getUniqueId)(void*) = nullptr;
+  int (*allGather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
+  int (*commDestroy)(void*) = nullptr;
+  const char* (*getErrorString)(int) = nullptr;
+  void* initRankSym = nullptr;  // ncclCommInitRank takes ncclUniqueId (128 B) by value: see Id128
+};
+
+struct Id128 {
+  char b[GS_GROUP_ID_BYTES];
+};
+
+RcclApi g_rccl;
+
+int rccl_load() {
+  if (g_rccl.lib) return GS_OK;
+  void* l = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!l) l = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!l) return fail(GS_ERR_HIP, std::string("cannot load RCCL: ") + dlerror());
+  g_rccl.getUniqueId = (int (*)(void*))dlsym(l, "ncclGetUniqueId");
+  g_rccl.initRankSym = dlsym(l, "ncclCommInitRank");
+  g_rccl.allGather = (int (*)(const void*, void*, size_t, int, void*, hipStream_t))dlsym(l, "ncclAllGather");
+  g_rccl.commDestroy = (int (*)(void*))dlsym(l, "ncclCommDestroy");
+  g_rccl.getErrorString = (const char* (*)(int))dlsym(l, "ncclGetErrorString");
+  if (!g_rccl.getUniqueId || !g_rccl.initRankSym || !g_rccl.allGather || !g_rccl.commDestroy)
+    return fail(GS_ERR_HIP, "RCCL is missing ncclGetUniqueId/ncclCommInitRank/ncclAllGather/ncclCommDestroy");
+  g_rccl.lib = l;
+  return GS_OK;
+}
+
+int rccl_fail(const char* what, int r) {
+  return fail(GS_ERR_HIP, std::string(what) + ": " + (g_rccl.getErrorString ? g_rccl.getErrorString(r) : "rccl error"));
+}
+
+constexpr int kNcclInt64 = 4;  // ncclInt64 (rccl.h)
+constexpr uint64_t kHdrLag = 4;  // a retune reads the headers of the exchange kHdrLag batches back
+
+}  // namespace
+
+struct gs_group {
+  gs_summary* h = nullptr;
+  void* comm = nullptr;
+  int nranks = 1, rank = 0;
+  uint64_t max_cap = 0, first_cap = 0, cap = 0, retune = 4;
+  int64_t* send = nullptr;  // [(max_cap + 1) * 3]
+  int64_t* recv = nullptr;  // [nranks * (max_cap + 1) * 3]
+  int64_t* hdr_host = nullptr;  // pinned [nranks * 3]
+  hipEvent_t hdr_ev = nullptr;
+  int64_t hdr_batch = -1;
+  uint64_t b = 0;            // exchanges since create / finish
+  uint64_t last_rows = 0;
+  uint64_t exchanges = 0;
+};
+
+namespace {
+
+// stage -> all-gather -> fold the other ranks' rows, all on the summary's stream
+int group_exchange(gs_group* g, uint64_t cap, bool keep_header) {
+  gs_summary* h = g->h;
+  const uint64_t rows = cap + 1;
+  if (int rc = stage(h, g->send, cap)) return rc;
+  const int r = g_rccl.allGather(g->send, g->recv, rows * 3, kNcclInt64, g->comm, h->stream);
+  if (r != 0) return rccl_fail("ncclAllGather", r);
+  if (keep_header) {  // rank headers (row 0 of each rank's block) -> pinned host memory
+    GS_HIP(hipMemcpy2DAsync(g->hdr_host, 24, g->recv, rows * 24, 24, g->nranks, hipMemcpyDeviceToHost, h->stream));
+    GS_HIP(hipEventRecord(g->hdr_ev, h->stream));
+    g->hdr_batch = (int64_t)g->b;
+  }
+  if (g->nranks > 1) {
+    ExchangeLayout xl;
+    xl.rows = (uint32_t)rows;
+    xl.skip_rank = g->rank;
+    xl.base = g->recv;
+    if (int rc = fold_device_impl(h, g->recv, g->recv + 1, reinterpret_cast<const uint8_t*>(g->recv + 2),
+                                  g->nranks * rows, 3, 24, /*track=*/false, true, xl))
+      return rc;
+  }
+  g->last_rows = rows;
+  g->b++;
+  g->exchanges++;
+  return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_group_unique_id(void* id) {
+  if (!id) return fail(GS_ERR_INVALID, "id is null");
+  if (int rc = rccl_load()) return rc;
+  const int r = g_rccl.getUniqueId(id);
+  return r ? rccl_fail("ncclGetUniqueId", r) : GS_OK;
+}
+
+int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, int rank, size_t batch_edges,
+                    size_t first_cap) {
+  if (!out || !id) return fail(GS_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (int rc = check(h)) return rc;
+  if (nranks < 1 || rank < 0 || rank >= nranks || batch_edges == 0) return fail(GS_ERR_INVALID, "bad group shape");
+  if (int rc = rccl_load()) return rc;
+  DeviceGuard dg(h->device);
+  if (int rc = gs_set_delta_tracking(h, 1)) return rc;
+  gs_group* g = new gs_group();
+  g->h = h;
+  g->nranks = nranks;
+  g->rank = rank;
+  g->max_cap = std::min<uint64_t>(3ull * batch_edges, (uint64_t)gs::kShards * h->delta_shard_cap);
+  g->first_cap = std::min<uint64_t>(first_cap ? first_cap : batch_edges, g->max_cap);
+  g->cap = g->first_cap;
+  if (const char* m = getenv("GS_GROUP_RETUNE")) g->retune = std::max(1, atoi(m));
+  auto bail = [&](int code) {
+    gs_group_destroy(g);
+    return code;
+  };
+  const size_t rows = g->max_cap + 1;
+  if (hipMalloc(&g->send, rows * 24) != hipSuccess || hipMalloc(&g->recv, (size_t)nranks * rows * 24) != hipSuccess ||
+      hipHostMalloc(&g->hdr_host, (size_t)nranks * 24, hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&g->hdr_ev, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(GS_ERR_HIP, "group buffer allocation failed"));
+  Id128 uid;
+  memcpy(uid.b, id, GS_GROUP_ID_BYTES);
+  typedef int (*InitRank)(void**, int, Id128, int);
+  const int r = ((InitRank)g_rccl.initRankSym)(&g->comm, nranks, uid, rank);
+  if (r != 0) return bail(rccl_fail("ncclCommInitRank", r));
+  *out = g;
+  return GS_OK;
+}
+
+int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
+  if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, /*track=*/true)) return rc;
+  const uint64_t b = g->b;
+  const bool keep = (b + kHdrLag) % g->retune == 0;
+  if (int rc = group_exchange(g, g->cap, keep)) return rc;
+  // every `retune` exchanges all ranks re-derive the capacity from the same headers
+  if (b % g->retune == 0 && b >= kHdrLag && g->hdr_batch == (int64_t)(b - kHdrLag)) {
+    GS_HIP(hipEventSynchronize(g->hdr_ev));
+    int64_t queued = 0;
+    for (int r = 0; r < g->nranks; ++r) queued = std::max(queued, g->hdr_host[r * 3 + 1]);
+    g->cap = std::min<uint64_t>(g->max_cap, std::max<uint64_t>(4096, (uint64_t)queued + (uint64_t)queued / 4 + 1024));
+  }
+  return GS_OK;
+}
+
+int gs_group_finish(gs_group_t g) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  while (g->last_rows) {
+    // headers of the last exchange -> remaining backlog on any rank (identical on every rank)
+    GS_HIP(hipMemcpy2DAsync(g->hdr_host, 24, g->recv, g->last_rows * 24, 24, g->nranks, hipMemcpyDeviceToHost,
+                            h->stream));
+    GS_HIP(hipStreamSynchronize(h->stream));
+    int64_t remaining = 0;
+    for (int r = 0; r < g->nranks; ++r) remaining = std::max(remaining, g->hdr_host[r * 3 + 1] - g->hdr_host[r * 3]);
+    if (remaining <= 0) break;
+    if (int rc = group_exchange(g, std::min<uint64_t>((uint64_t)remaining, g->max_cap), false)) return rc;
+  }
+  if (int rc = gs_sync(h)) return rc;
+  g->b = 0;
+  g->last_rows = 0;
+  g->hdr_batch = -1;
+  g->cap = g->first_cap;
+  return GS_OK;
+}
+
+int gs_group_stats(gs_group_t g, uint64_t* exchanges, uint64_t* records_sent, uint64_t* current_cap) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  uint64_t sent = 0;
+  GS_HIP(hipMemcpyAsync(&sent, h->ctr + gs::ctr_index(gs::CTR_SENT), 8, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  if (exchanges) *exchanges = g->exchanges;
+  if (records_sent) *records_sent = sent;
+  if (current_cap) *current_cap = g->cap;
+  return GS_OK;
+}
+
+int gs_group_destroy(gs_group_t g) {
+  if (!g) return GS_OK;
+  DeviceGuard dg(g->h->device);
+  (void)hipStreamSynchronize(g->h->stream);
+  if (g->comm && g_rccl.commDestroy) g_rccl.commDestroy(g->comm);
+  (void)hipFree(g->send);
+  (void)hipFree(g->recv);
+  if (g->hdr_host) (void)hipHostFree(g->hdr_host);
+  if (g->hdr_ev) (void)hipEventDestroy(g->hdr_ev);
+  delete g;
+  return GS_OK;
+}
+
+}  // extern "C"

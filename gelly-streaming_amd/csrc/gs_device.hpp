@@ -49,6 +49,7 @@ enum CounterBlock : int {
   CTR_STAGE_N,                   // records staged by the running k_stage (u32 pair = u64)
   CTR_STAGE_N_HI,
   CTR_STAGE_DONE,                // k_stage block ticket
+  CTR_SENT,                      // records sent by all stages since reset (u64)
   CTR_COUNT
 };
 __host__ __device__ constexpr int ctr_index(int c) { return c * kCtrStride; }

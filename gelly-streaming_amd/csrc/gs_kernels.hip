@@ -370,6 +370,7 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* 
       send[0] = (int64_t)sent;
       send[1] = (int64_t)total;
       send[2] = 0x80;
+      atomicAdd((unsigned long long*)&t.ctr[ctr_index(CTR_SENT)], sent);
     }
     *qn_out = total - sent;
     *qn_in = 0ull;

@@ -1,0 +1,65 @@
+/*
+ * gs_group.h -- native multi-GPU combine for the summary of include/gs_summary.h.
+ *
+ * One process (or thread) per GPU; each rank holds a replica of the global
+ * summary and folds its own shard of every global micro-batch. After its fold a
+ * rank stages its structural delta (gs_delta_stage), the ranks all-gather the
+ * staged records over RCCL (xGMI) on the summary's own HIP stream, and every rank
+ * folds the other ranks' records (gs_fold_exchange_device) -- all queued on one
+ * stream, no host synchronisation per batch. This replaces the reference's gather
+ * of per-partition summaries into one parallelism-1 reducer
+ * (SummaryBulkAggregation.java:77-83) and its Merger (SummaryAggregation.java:107-119):
+ * after gs_group_finish every replica equals the union of all ranks' folds.
+ *
+ * The per-batch collective size is agreed without communication: it starts at
+ * `first_cap` records and every `retune` batches is re-derived from gathered
+ * headers all ranks hold identically; records past it stay queued on the device
+ * and ride with the next exchange. RCCL (librccl.so.1) is loaded on first use.
+ */
+#ifndef GS_GROUP_H
+#define GS_GROUP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gs_summary.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gs_group* gs_group_t;
+
+#define GS_GROUP_ID_BYTES 128
+
+/* Create the communicator id on one rank and hand its 128 bytes to every rank
+ * (any host channel: MPI, TCP, torch.distributed, a file). */
+int gs_group_unique_id(void* id);
+
+/* Join the group as `rank` of `nranks` and bind it to summary `h` (its device and
+ * stream). `batch_edges` = maximum edges one gs_group_fold_device call folds;
+ * `first_cap` = records per rank in the first exchanges (0: batch_edges). Turns
+ * delta tracking on. Collective: every rank must call it. */
+int gs_group_create(gs_group_t* g, gs_handle h, const void* id, int nranks, int rank, size_t batch_edges,
+                    size_t first_cap);
+
+/* One global micro-batch on this rank: fold n DEVICE edges (as gs_fold_device,
+ * stride 1), exchange the delta, fold the other ranks' records. Asynchronous.
+ * Collective: every rank calls it the same number of times (n may differ,
+ * including 0). */
+int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n);
+
+/* Drain every rank's queued records (synchronous rounds) and synchronise; then all
+ * replicas are identical. Collective. */
+int gs_group_finish(gs_group_t g);
+
+/* Exchange statistics: exchanges run, records this rank has sent, the current
+ * per-rank capacity of one exchange (synchronises the stream). */
+int gs_group_stats(gs_group_t g, uint64_t* exchanges, uint64_t* records_sent, uint64_t* current_cap);
+
+int gs_group_destroy(gs_group_t g);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GS_GROUP_H */
