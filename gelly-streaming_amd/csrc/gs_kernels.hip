@@ -281,28 +281,6 @@ __global__ __launch_bounds__(256) void k_export(Table t, int64_t* __restrict__ o
 // {sent, queued, skip}, *qn_out, and resets the counters it consumed. The receiver
 // reads `sent` from the header, so unused send rows need no padding.
 // cap == 0 with send == nullptr: everything goes to q_out (gs_take_delta_records).
-// Block-aggregated append: every thread of the block calls it (uniform control
-// flow); returns this thread's position, one global atomic per call per block.
-__device__ __forceinline__ unsigned long long block_append(bool keep, unsigned long long* counter) {
-  __shared__ uint32_t wcnt[4];
-  __shared__ unsigned long long base;
-  const unsigned long long m = __ballot(keep);
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
-  if (lane == 0) wcnt[w] = __popcll(m);
-  __syncthreads();
-  uint32_t woff = 0, tot = 0;
-  for (uint32_t q = 0; q < 4; ++q) {
-    if (q < w) woff += wcnt[q];
-    tot += wcnt[q];
-  }
-  if (threadIdx.x == 0) base = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
-  __syncthreads();
-  const unsigned long long pos = base + woff + rank;
-  __syncthreads();  // wcnt/base are reused by the next call
-  return pos;
-}
-
 __device__ __forceinline__ void stage_write(const Table& t, unsigned long long pos, int64_t a, int64_t b, int64_t w,
                                             int64_t* send, uint64_t cap, int64_t* q_out, uint64_t qcap) {
   int64_t* r;
@@ -319,44 +297,51 @@ __device__ __forceinline__ void stage_write(const Table& t, unsigned long long p
   r[2] = w;
 }
 
-// grid = kShards * kStageParts blocks of 256 threads.
-constexpr uint32_t kStageParts = 4;
+// grid = kShards blocks: block s copies backlog slice s and delta shard s to
+// deterministic positions (backlog first, then shards in order: a prefix of the
+// 64 shard counts, no append atomics); the last block (64-way ticket) resets the
+// counters the others read.
 __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* __restrict__ q_in,
                                                unsigned long long* qn_in, int64_t* __restrict__ q_out,
                                                unsigned long long* qn_out, uint64_t qcap, int64_t* __restrict__ send,
                                                uint64_t cap) {
-  unsigned long long* count = (unsigned long long*)&t.ctr[ctr_index(CTR_STAGE_N)];
+  __shared__ uint32_t cnt[kShards];
+  __shared__ uint64_t off_sh, total_sh;
+  const uint32_t s = blockIdx.x;
   const uint64_t backlog = min((unsigned long long)*qn_in, (unsigned long long)qcap);
-  const uint64_t G = (uint64_t)gridDim.x * 256;
-  for (uint64_t base = (uint64_t)blockIdx.x * 256; base < backlog; base += G) {
-    const uint64_t i = base + threadIdx.x;
-    const bool keep = i < backlog;
-    int64_t a = 0, b = 0, w = 0;
-    if (keep) {
-      a = q_in[i * 3];
-      b = q_in[i * 3 + 1];
-      w = q_in[i * 3 + 2];
+  if (threadIdx.x < kShards) cnt[threadIdx.x] = min(t.ctr[ctr_index(CTR_DELTA + threadIdx.x)], L.delta_shard_cap);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t off = backlog, tot = backlog;
+    for (uint32_t q = 0; q < kShards; ++q) {
+      if (q < s) off += cnt[q];
+      tot += cnt[q];
     }
-    const unsigned long long pos = block_append(keep, count);
-    if (keep) stage_write(t, pos, a, b, w, send, cap, q_out, qcap);
+    off_sh = off;
+    total_sh = tot;
   }
-  // delta shards: block b takes shard b % kShards, part b / kShards
-  const uint32_t s = blockIdx.x % kShards, part = blockIdx.x / kShards;
-  const uint32_t cnt = min(t.ctr[ctr_index(CTR_DELTA + s)], L.delta_shard_cap);
+  __syncthreads();
+  const uint64_t total = total_sh;
+  // backlog slice s
+  const uint64_t per = (backlog + kShards - 1) / kShards;
+  const uint64_t b0 = (uint64_t)s * per, b1 = min(backlog, b0 + per);
+  for (uint64_t i = b0 + threadIdx.x; i < b1; i += 256) stage_write(t, i, q_in[i * 3], q_in[i * 3 + 1], q_in[i * 3 + 2], send, cap, q_out, qcap);
+  // delta shard s
   const int64_t* in = L.drec + (size_t)s * L.delta_shard_cap * 3;
-  for (uint32_t base = part * 256u; base < cnt; base += kStageParts * 256u) {
-    const uint32_t j = base + threadIdx.x;
-    const bool keep = j < cnt;
-    int64_t a = 0, b = 0, w = 0;
-    if (keep) {
-      a = in[(size_t)j * 3];
-      b = in[(size_t)j * 3 + 1];
-      w = in[(size_t)j * 3 + 2];
+  const uint64_t off = off_sh;
+  for (uint32_t j = threadIdx.x; j < cnt[s]; j += 256)
+    stage_write(t, off + j, in[(size_t)j * 3], in[(size_t)j * 3 + 1], in[(size_t)j * 3 + 2], send, cap, q_out, qcap);
+  if (s == 0 && threadIdx.x == 0) {
+    const uint64_t sent = total < cap ? total : cap;
+    if (send) {
+      send[0] = (int64_t)sent;
+      send[1] = (int64_t)total;
+      send[2] = 0x80;
+      atomicAdd((unsigned long long*)&t.ctr[ctr_index(CTR_SENT)], (unsigned long long)sent);
     }
-    const unsigned long long pos = block_append(keep, count);
-    if (keep) stage_write(t, pos, a, b, w, send, cap, q_out, qcap);
+    *qn_out = total - sent;
   }
-  // last block: header + counter resets
+  // the last block resets what every block has read
   __shared__ uint32_t last;
   __syncthreads();
   if (threadIdx.x == 0) last = atomicAdd(&t.ctr[ctr_index(CTR_STAGE_DONE)], 1u) == gridDim.x - 1;
@@ -364,17 +349,7 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* 
   if (!last) return;
   if (threadIdx.x < kShards) t.ctr[ctr_index(CTR_DELTA + threadIdx.x)] = 0u;
   if (threadIdx.x == 0) {
-    const unsigned long long total = atomicAdd(count, 0ull);
-    const unsigned long long sent = total < cap ? total : cap;
-    if (send) {
-      send[0] = (int64_t)sent;
-      send[1] = (int64_t)total;
-      send[2] = 0x80;
-      atomicAdd((unsigned long long*)&t.ctr[ctr_index(CTR_SENT)], sent);
-    }
-    *qn_out = total - sent;
     *qn_in = 0ull;
-    atomicExch(count, 0ull);
     atomicExch(&t.ctr[ctr_index(CTR_STAGE_DONE)], 0u);
   }
 }
@@ -458,8 +433,7 @@ void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t*
 
 void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned long long* qn_in, int64_t* q_out,
                   unsigned long long* qn_out, uint64_t qcap, int64_t* send, uint64_t cap, hipStream_t st) {
-  hipLaunchKernelGGL(k_stage, dim3(kShards * kStageParts), dim3(256), 0, st, t, L, q_in, qn_in, q_out, qn_out, qcap,
-                     send, cap);
+  hipLaunchKernelGGL(k_stage, dim3(kShards), dim3(256), 0, st, t, L, q_in, qn_in, q_out, qn_out, qcap, send, cap);
 }
 
 void launch_copy_queue(const int64_t* q, const unsigned long long* qn, uint64_t qcap, int64_t* out, uint64_t cap,
