@@ -158,14 +158,18 @@ def main():
         edges_per_launch = per / max(nf, 1) if world == 1 else B  # own-shard launches dominate
         achieved = BYTES_PER_EDGE_SPARSE * edges_per_launch / (fold_avg_ms * 1e-3) / 1e9
         traffic = None
+        traffic_gbs = None
         pmc = os.path.join(ROOT, "profiles", "pmc_fold_traffic.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc):  # PMC bytes per launch from the committed rocprofv3 passes
             with open(pmc) as f:
                 pm = json.load(f)
             if pm.get("workload") == "rmat%d-cc-stream" % args.scale and pm.get("batch") == B:
-                traffic = pm.get("hbm_bytes_per_launch")
+                traffic = int(pm.get("hbm_bytes_per_launch"))
+                traffic_gbs = round(traffic / (fold_avg_ms * 1e-3) / 1e9, 1)
         roof = {"kernel": "k_fold", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_gbs": traffic_gbs,
+                "traffic_frac": round(traffic_gbs / HBM_PEAK_GBS, 4) if traffic_gbs else None,
                 "bytes_per_edge": BYTES_PER_EDGE_SPARSE, "edges_per_launch": int(edges_per_launch),
                 "fold_avg_us": round(fold_avg_ms * 1e3, 2), "fold_launches": int(nf),
                 "hook_avg_us": round(hook_ms * 1e3 / max(nh, 1), 2), "hook_launches": int(nh),

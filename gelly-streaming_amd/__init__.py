@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "gs_combine", "gs_sync", "gs_num_vertices", "gs_find", "gs_export_labels", "gs_export_labels_device",
     "gs_bip_status", "gs_export_colouring", "gs_serialize", "gs_deserialize", "gs_set_delta_tracking",
     "gs_take_delta_records", "gs_delta_stage", "gs_fold_records_device", "gs_fold_exchange_device",
-    "gs_get_stream", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity",
+    "gs_get_stream", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity", "gs_counters",
     "gs_gen_rmat", "gs_gen_er", "gs_gen_bip",
     "gs_group_unique_id", "gs_group_create", "gs_group_fold_device", "gs_group_finish", "gs_group_stats",
     "gs_group_destroy",
@@ -99,6 +99,7 @@ def lib():
     L.gs_set_profiling.argtypes = [_vp, ctypes.c_int]
     L.gs_kernel_stats.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double)]
     L.gs_table_capacity.argtypes = [_vp, ctypes.POINTER(_u64)]
+    L.gs_counters.argtypes = [_vp, ctypes.POINTER(_u64)]
     L.gs_gen_rmat.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, ctypes.c_int]
     L.gs_gen_er.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, ctypes.c_int]
     L.gs_gen_bip.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, _vp, _sz]
@@ -285,6 +286,14 @@ class Summary:
         ms = ctypes.c_double()
         _check(lib().gs_kernel_stats(self._h, KERNEL_IDS[name], ctypes.byref(n), ctypes.byref(ms)))
         return n.value, ms.value
+
+    def counters(self):
+        """Device counters (gs_counters): vertices, failed, err, ovf, sent,
+        hooks / hook iterations / failed CASes (debug build only)."""
+        a = (_u64 * 8)()
+        _check(lib().gs_counters(self._h, a))
+        keys = ("vertices", "failed", "err", "ovf", "sent", "hooks", "hook_iters", "cas_fail")
+        return dict(zip(keys, list(a)))
 
     def table_capacity(self):
         n = _u64()

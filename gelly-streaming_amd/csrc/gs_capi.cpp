@@ -869,6 +869,28 @@ int gs_kernel_stats(gs_handle h, int id, uint64_t* launches, double* total_ms) {
   return GS_OK;
 }
 
+int gs_counters(gs_handle h, uint64_t* out8) {
+  if (int rc = check(h)) return rc;
+  if (!out8) return fail(GS_ERR_INVALID, "out is null");
+  DeviceGuard g(h->device);
+  if (int rc = flush_hooks(h)) return rc;
+  std::vector<uint32_t> c(gs::CTR_COUNT * gs::kCtrStride);
+  GS_HIP(hipMemcpyAsync(c.data(), h->ctr, c.size() * 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  uint64_t nv = 0;
+  for (int i = 0; i < gs::kShards; ++i) nv += c[gs::ctr_index(gs::CTR_NV + i)];
+  auto u64 = [&](int idx) { return (uint64_t)c[gs::ctr_index(idx)] | ((uint64_t)c[gs::ctr_index(idx) + 1] << 32); };
+  out8[0] = nv;
+  out8[1] = c[gs::ctr_index(gs::CTR_FAIL)];
+  out8[2] = c[gs::ctr_index(gs::CTR_ERR)];
+  out8[3] = c[gs::ctr_index(gs::CTR_OVF)];
+  out8[4] = u64(gs::CTR_SENT);
+  out8[5] = c[gs::ctr_index(gs::CTR_DBG_HOOKS)];
+  out8[6] = c[gs::ctr_index(gs::CTR_DBG_ITERS)];
+  out8[7] = c[gs::ctr_index(gs::CTR_DBG_CASFAIL)];
+  return GS_OK;
+}
+
 int gs_table_capacity(gs_handle h, uint64_t* slots) {
   if (int rc = check(h)) return rc;
   if (!slots) return fail(GS_ERR_INVALID, "slots is null");

@@ -50,6 +50,9 @@ enum CounterBlock : int {
   CTR_STAGE_N_HI,
   CTR_STAGE_DONE,                // k_stage block ticket
   CTR_SENT,                      // records sent by all stages since reset (u64)
+  CTR_DBG_HOOKS,                 // debug build (-DGS_DEBUG_COUNTERS): hook calls,
+  CTR_DBG_ITERS,                 //   hook-loop iterations,
+  CTR_DBG_CASFAIL,               //   failed hook CASes
   CTR_COUNT
 };
 __host__ __device__ constexpr int ctr_index(int c) { return c * kCtrStride; }
@@ -317,10 +320,18 @@ __device__ __forceinline__ void find_root(const Table& t, uint32_t x, uint32_t l
 // Hook loop: make a and b one set with colour(a) ^ colour(b) == need (SIGNED).
 // The larger-key root is hooked under the smaller key, so every root is the
 // minimum id of its tree (the canonical label) at all times.
+#ifdef GS_DEBUG_COUNTERS
+#define GS_DBG(c) atomicAdd(&t.ctr[ctr_index(c)], 1u)
+#else
+#define GS_DBG(c) ((void)0)
+#endif
+
 template <bool SIGNED, bool TRACK>
 __device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, uint32_t a, uint32_t la, int64_t ka,
                                      uint32_t b, uint32_t lb, int64_t kb, uint32_t need) {
+  GS_DBG(CTR_DBG_HOOKS);
   while (true) {
+    GS_DBG(CTR_DBG_ITERS);
     uint32_t pa = 0, pb = 0;
     find_root2<true>(t, a, la, ka, pa, b, lb, kb, pb);
     la = a << 1;
@@ -351,6 +362,7 @@ __device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, 
       return;
     }
     // hi was hooked meanwhile: continue that side from its live link
+    GS_DBG(CTR_DBG_CASFAIL);
     if (a_lo)
       lb = old;
     else

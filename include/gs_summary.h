@@ -163,6 +163,12 @@ int gs_set_profiling(gs_handle h, int on);
 int gs_kernel_stats(gs_handle h, int id, uint64_t* launches, double* total_ms);
 int gs_table_capacity(gs_handle h, uint64_t* slots);
 
+/* Device counters (synchronises): out[0] vertices, [1] bipartiteness failed,
+ * [2] table-overflow error, [3] list overflow, [4] records sent by exchanges,
+ * [5] hook calls, [6] hook-loop iterations, [7] failed hook CASes -- [5..7] only
+ * count in the debug build (make -C gelly-streaming_amd debug). */
+int gs_counters(gs_handle h, uint64_t* out8);
+
 #ifdef __cplusplus
 }
 #endif
