@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-log2", type=int, default=24)
     p.add_argument("--no-profile-pass", action="store_true")
+    p.add_argument("--pipeline", type=int, default=3,
+                   help="pipelined windows at N=1 (gs_set_pipelining depth; 1 = strictly in order)")
     p.add_argument("--exchange", action="store_true",
                    help="run the multi-GPU delta-exchange path even at one rank (overhead measurement)")
     p.add_argument("--exchange-impl", choices=["native", "torch"], default="native",
@@ -106,6 +108,8 @@ def main():
         else:
             xch = DeltaExchangeFold(summ, B, dev)
 
+    if xch is None and args.pipeline > 1:
+        summ.set_pipelining(args.pipeline)
     nlabels = [0]
 
     def one_step():

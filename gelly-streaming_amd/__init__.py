@@ -16,6 +16,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libgs_summary.so")
+if os.environ.get("GS_LIB_VARIANT"):  # experiment builds (Makefile target `variant`)
+    LIB_PATH = os.path.join(_HERE, "lib_" + os.environ["GS_LIB_VARIANT"], "libgs_summary.so")
 
 KIND_CC = 0
 KIND_SIGNED = 1
@@ -34,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "gs_combine", "gs_sync", "gs_num_vertices", "gs_find", "gs_export_labels", "gs_export_labels_device",
     "gs_bip_status", "gs_export_colouring", "gs_serialize", "gs_deserialize", "gs_set_delta_tracking",
     "gs_take_delta_records", "gs_delta_stage", "gs_fold_records_device", "gs_fold_exchange_device",
-    "gs_get_stream", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity", "gs_counters",
+    "gs_get_stream", "gs_set_pipelining", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity", "gs_counters",
     "gs_gen_rmat", "gs_gen_er", "gs_gen_bip",
     "gs_group_unique_id", "gs_group_create", "gs_group_fold_device", "gs_group_finish", "gs_group_stats",
     "gs_group_destroy",
@@ -97,6 +99,7 @@ def lib():
     L.gs_fold_exchange_device.argtypes = [_vp, _vp, _sz, _sz, ctypes.c_int]
     L.gs_get_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
     L.gs_set_profiling.argtypes = [_vp, ctypes.c_int]
+    L.gs_set_pipelining.argtypes = [_vp, ctypes.c_int]
     L.gs_kernel_stats.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double)]
     L.gs_table_capacity.argtypes = [_vp, ctypes.POINTER(_u64)]
     L.gs_counters.argtypes = [_vp, ctypes.POINTER(_u64)]
@@ -280,6 +283,11 @@ class Summary:
 
     def set_profiling(self, on=True):
         _check(lib().gs_set_profiling(self._h, 1 if on else 0))
+
+    def set_pipelining(self, depth=2):
+        """gs_set_pipelining: depth 2 lets consecutive device folds overlap on the
+        device (pipelined windows); any read orders behind them."""
+        _check(lib().gs_set_pipelining(self._h, int(depth)))
 
     def kernel_stats(self, name):
         n = _u64()

@@ -95,6 +95,16 @@ struct gs_summary {
   hipEvent_t stage_ev[2] = {nullptr, nullptr};
   int stage_next = 0;
   int64_t* d_scratch = nullptr;  // small scratch (find_one)
+  // pipelined folds (gs_set_pipelining): consecutive device folds alternate over
+  // two lane streams so that fold b+1 may start while fold b drains; every other
+  // entry point joins the lanes onto `stream` first (join_lanes).
+  int pipe_depth = 1;
+  static constexpr int kLanes = 4;
+  hipStream_t lane[kLanes] = {};
+  hipEvent_t lane_ev[kLanes] = {};
+  hipEvent_t main_ev = nullptr;
+  int lane_next = 0;
+  bool lanes_dirty = false;
   // profiling
   bool profiling = false;
   struct Pending {
@@ -187,6 +197,17 @@ void drain_profile(gs_summary* h) {
   h->prof_pending.clear();
 }
 
+// Order the handle's stream behind every fold still running on a lane.
+int join_lanes(gs_summary* h) {
+  if (!h->lanes_dirty) return GS_OK;
+  for (int i = 0; i < h->pipe_depth; ++i) {
+    GS_HIP(hipEventRecord(h->lane_ev[i], h->lane[i]));
+    GS_HIP(hipStreamWaitEvent(h->stream, h->lane_ev[i], 0));
+  }
+  h->lanes_dirty = false;
+  return GS_OK;
+}
+
 int check_device_flags(gs_summary* h) {
   uint32_t flags[2] = {0, 0};
   GS_HIP(hipMemcpyAsync(&flags[0], h->ctr + gs::ctr_index(gs::CTR_ERR), 4, hipMemcpyDeviceToHost, h->stream));
@@ -198,6 +219,7 @@ int check_device_flags(gs_summary* h) {
 }
 
 int read_nv(gs_summary* h, uint64_t* nv) {
+  if (int rc = join_lanes(h)) return rc;
   std::vector<uint32_t> c(gs::CTR_COUNT * gs::kCtrStride);
   GS_HIP(hipMemcpyAsync(c.data(), h->ctr, c.size() * 4, hipMemcpyDeviceToHost, h->stream));
   GS_HIP(hipStreamSynchronize(h->stream));
@@ -243,7 +265,7 @@ struct ExchangeLayout {
 };
 int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
                      size_t stride, size_t w_stride, bool track, bool check_cap = true,
-                     const ExchangeLayout& xl = ExchangeLayout());
+                     const ExchangeLayout& xl = ExchangeLayout(), bool allow_pipe = false);
 
 // Hook the deferred active edges (DEFER mode) so the forest is complete.
 int flush_hooks(gs_summary* h) {
@@ -260,6 +282,7 @@ int flush_hooks(gs_summary* h) {
 
 // Export every (vertex, label, parity) into device arrays; returns count.
 int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n) {
+  if (int rc = join_lanes(h)) return rc;
   if (int rc = flush_hooks(h)) return rc;
   GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, h->stream));
   {
@@ -329,16 +352,25 @@ int ensure_capacity(gs_summary* h, size_t n) {
 }
 
 int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
-                     size_t stride, size_t w_stride, bool track, bool check_cap, const ExchangeLayout& xl) {
+                     size_t stride, size_t w_stride, bool track, bool check_cap, const ExchangeLayout& xl,
+                     bool allow_pipe) {
   if (n == 0) return GS_OK;
   if (check_cap) {
     int rc = ensure_capacity(h, n);
     if (rc) return rc;
   }
+  // Pipelined: plain fused folds (no delta tracking, no exchange layout, no hot
+  // level, not profiling) may overlap the previous fold. Union is associative and
+  // commutative, so the forest after both is the same; readers join the lanes.
+  const bool pipe = allow_pipe && h->pipe_depth > 1 && h->mode == gs_summary::FUSED && !track && xl.rows == 0 &&
+                    h->hotcap == 0 && !h->profiling;
+  if (!pipe) {
+    if (int rc = join_lanes(h)) return rc;
+  }
   const bool sign = h->kind == GS_KIND_SIGNED;
   for (size_t off = 0; off < n; off += kMaxChunk) {
     const uint32_t c = (uint32_t)std::min<size_t>(kMaxChunk, n - off);
-    const uint32_t per_block = 256u * (uint32_t)h->ept;
+    const uint32_t per_block = gs::kFoldBS * (uint32_t)h->ept;
     const uint32_t blocks = (c + per_block - 1) / per_block;
     const uint32_t per_shard_edges = ((blocks + gs::kShards - 1) / gs::kShards) * per_block;
     if (track) {
@@ -356,11 +388,19 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       h->nv_pending = false;
       if (nv >= h->hot_target) h->hot_open = false;
     }
+    hipStream_t st = h->stream;
+    if (pipe) {  // the lane waits for the caller's work on the handle stream, not for the other lane
+      GS_HIP(hipEventRecord(h->main_ev, h->stream));
+      st = h->lane[h->lane_next];
+      h->lane_next = (h->lane_next + 1) % h->pipe_depth;
+      GS_HIP(hipStreamWaitEvent(st, h->main_ev, 0));
+      h->lanes_dirty = true;
+    }
     {
       Prof p(h, KID_FOLD);
       gs::launch_fold(sign, track, h->ept, h->table(), h->lists(), src + off * stride, dst + off * stride,
                       w ? w + off * w_stride : nullptr, c, (uint32_t)stride, (uint32_t)w_stride, cur, drain, zero,
-                      inline_max, xl.rows, xl.skip_rank, xl.base, (uint32_t)off, h->stream);
+                      inline_max, xl.rows, xl.skip_rank, xl.base, (uint32_t)off, st);
     }
     GS_HIP(hipGetLastError());
     if (h->hot_open && !h->nv_pending) {  // vertex count for the next hot-level decision
@@ -446,6 +486,12 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   for (int i = 0; i < 2; ++i)
     if (hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming) != hipSuccess)
       return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
+  for (int i = 0; i < gs_summary::kLanes; ++i)
+    if (hipStreamCreateWithFlags(&h->lane[i], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->lane_ev[i], hipEventDisableTiming) != hipSuccess)
+      return bail(fail(GS_ERR_HIP, "lane stream creation failed"));
+  if (hipEventCreateWithFlags(&h->main_ev, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
   if (hipEventCreateWithFlags(&h->nv_ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(&h->h_nv, gs::kShards * gs::kCtrStride * 4, hipHostMallocDefault) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hot-level bookkeeping allocation failed"));
@@ -459,8 +505,14 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
 int gs_destroy(gs_handle h) {
   if (!h) return GS_OK;
   DeviceGuard g(h->device);
+  (void)join_lanes(h);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   drain_profile(h);
+  for (int i = 0; i < gs_summary::kLanes; ++i) {
+    if (h->lane_ev[i]) (void)hipEventDestroy(h->lane_ev[i]);
+    if (h->lane[i]) (void)hipStreamDestroy(h->lane[i]);
+  }
+  if (h->main_ev) (void)hipEventDestroy(h->main_ev);
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 2; ++i)
     if (h->stage_ev[i]) (void)hipEventDestroy(h->stage_ev[i]);
@@ -486,6 +538,7 @@ int gs_destroy(gs_handle h) {
 int gs_reset(gs_handle h) {
   if (int rc = check(h)) return rc;
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
   {
     Prof p(h, KID_INIT);
@@ -531,6 +584,7 @@ int gs_fold(gs_handle h, const int64_t* src, const int64_t* dst, size_t n) {
   if (int rc = check(h)) return rc;
   if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   return fold_host_impl(h, src, dst, nullptr, n);
 }
 
@@ -539,7 +593,7 @@ int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const ui
   if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
   if (stride == 0) return fail(GS_ERR_INVALID, "stride must be >= 1");
   DeviceGuard g(h->device);
-  return fold_device_impl(h, src, dst, w, n, stride, 1, h->track);
+  return fold_device_impl(h, src, dst, w, n, stride, 1, h->track, true, ExchangeLayout(), /*allow_pipe=*/true);
 }
 
 int gs_fold_records_device(gs_handle h, const int64_t* rec, size_t n, int track) {
@@ -547,12 +601,14 @@ int gs_fold_records_device(gs_handle h, const int64_t* rec, size_t n, int track)
   if (n && !rec) return fail(GS_ERR_INVALID, "null records");
   if (track && !h->drec) return fail(GS_ERR_INVALID, "delta tracking was never enabled");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   return fold_device_impl(h, rec, rec + 1, reinterpret_cast<const uint8_t*>(rec + 2), n, 3, 24, track != 0);
 }
 
 int gs_sync(gs_handle h) {
   if (int rc = check(h)) return rc;
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   if (int rc = flush_hooks(h)) return rc;
   GS_HIP(hipStreamSynchronize(h->stream));
   return check_device_flags(h);
@@ -562,6 +618,7 @@ int gs_num_vertices(gs_handle h, uint64_t* n) {
   if (int rc = check(h)) return rc;
   if (!n) return fail(GS_ERR_INVALID, "n is null");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   int rc = read_nv(h, n);
   if (rc) return rc;
   return check_device_flags(h);
@@ -571,6 +628,7 @@ int gs_find(gs_handle h, int64_t v, int64_t* label, int* found) {
   if (int rc = check(h)) return rc;
   if (!label || !found) return fail(GS_ERR_INVALID, "null output");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   if (int rc = flush_hooks(h)) return rc;
   gs::launch_find_one(h->table(), v, h->d_scratch, h->stream);
   GS_HIP(hipGetLastError());
@@ -586,6 +644,7 @@ int gs_export_labels_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* pa
   if (int rc = check(h)) return rc;
   if (!n) return fail(GS_ERR_INVALID, "n is null");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   return export_device_impl(h, v, label, parity, cap, n);
 }
 
@@ -620,6 +679,7 @@ int gs_export_labels(gs_handle h, int64_t* v, int64_t* label, size_t cap, size_t
   if (int rc = check(h)) return rc;
   if (!n) return fail(GS_ERR_INVALID, "n is null");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   return export_host(h, v, label, nullptr, cap, n);
 }
 
@@ -627,6 +687,7 @@ int gs_bip_status(gs_handle h, int* ok) {
   if (int rc = check(h)) return rc;
   if (!ok) return fail(GS_ERR_INVALID, "ok is null");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   if (int rc = flush_hooks(h)) return rc;
   uint32_t f = 0;
   GS_HIP(hipMemcpyAsync(&f, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream));
@@ -646,6 +707,7 @@ int gs_export_colouring(gs_handle h, int64_t* comp, int64_t* v, uint8_t* sign, s
     return GS_OK;
   }
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   rc = export_host(h, v, comp, sign, cap, n);
   if (rc) return rc;
   if (sign)
@@ -665,6 +727,7 @@ int gs_combine(gs_handle dst, gs_handle src) {
   uint32_t sfail = 0;
   {
     DeviceGuard g(src->device);
+    if (int rc_ = join_lanes(src)) return rc_;
     int rc = read_nv(src, &nv);
     if (rc) return rc;
     GS_HIP(hipMemcpyAsync(&sfail, src->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, src->stream));
@@ -678,6 +741,7 @@ int gs_combine(gs_handle dst, gs_handle src) {
     }
   }
   DeviceGuard g(dst->device);
+  if (int rc_ = join_lanes(dst)) return rc_;
   int rc = GS_OK;
   if (sfail) {
     GS_HIP(hipMemsetAsync(dst->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, dst->stream));
@@ -711,6 +775,7 @@ int gs_serialize(gs_handle h, void* buf, size_t cap, size_t* len) {
   if (int rc = check(h)) return rc;
   if (!len) return fail(GS_ERR_INVALID, "len is null");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   uint64_t nv = 0;
   int rc = read_nv(h, &nv);
   if (rc) return rc;
@@ -754,6 +819,7 @@ int gs_deserialize(gs_handle h, const void* buf, size_t len) {
   int rc = gs_reset(h);
   if (rc) return rc;
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   if (!hdr[2]) {
     GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, h->stream));
     return gs_sync(h);
@@ -769,6 +835,7 @@ int gs_deserialize(gs_handle h, const void* buf, size_t len) {
 int gs_set_delta_tracking(gs_handle h, int on) {
   if (int rc = check(h)) return rc;
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   if (int rc = flush_hooks(h)) return rc;  // deferred hooks belong to the previous tracking state
   if (on && !h->drec) {
     // worst case between two takes: one fold chunk of kMaxChunk edges
@@ -811,6 +878,7 @@ int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count
   if (!count) return fail(GS_ERR_INVALID, "count is null");
   if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   if (int rc = stage(h, nullptr, 0)) return rc;  // everything into the queue
   gs::launch_copy_queue(h->q[h->qsel], h->qn + h->qsel, h->qcap, rec, cap, count, h->stream);
   GS_HIP(hipGetLastError());
@@ -823,6 +891,7 @@ int gs_delta_stage(gs_handle h, int64_t* send, size_t cap) {
   if (!send) return fail(GS_ERR_INVALID, "send is null");
   if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   return stage(h, send, cap);
 }
 
@@ -831,6 +900,7 @@ int gs_fold_exchange_device(gs_handle h, const int64_t* recv, size_t world, size
   if (!recv || rows == 0) return fail(GS_ERR_INVALID, "empty exchange buffer");
   if (world * rows > 0xFFFFFFFFull) return fail(GS_ERR_INVALID, "exchange buffer too large");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   ExchangeLayout xl;
   xl.rows = (uint32_t)rows;
   xl.skip_rank = skip_rank;
@@ -842,6 +912,10 @@ int gs_fold_exchange_device(gs_handle h, const int64_t* recv, size_t world, size
 int gs_get_stream(gs_handle h, void** stream) {
   if (int rc = check(h)) return rc;
   if (!stream) return fail(GS_ERR_INVALID, "stream is null");
+  {
+    DeviceGuard g(h->device);
+    if (int rc_ = join_lanes(h)) return rc_;
+  }
   *stream = (void*)h->stream;
   return GS_OK;
 }
@@ -849,6 +923,7 @@ int gs_get_stream(gs_handle h, void** stream) {
 int gs_set_profiling(gs_handle h, int on) {
   if (int rc = check(h)) return rc;
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   (void)hipStreamSynchronize(h->stream);
   drain_profile(h);
   h->profiling = on != 0;
@@ -863,6 +938,7 @@ int gs_kernel_stats(gs_handle h, int id, uint64_t* launches, double* total_ms) {
   if (int rc = check(h)) return rc;
   if (id < 0 || id >= KID_N || !launches || !total_ms) return fail(GS_ERR_INVALID, "bad kernel id");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   drain_profile(h);
   *launches = h->launches[id];
   *total_ms = h->total_ms[id];
@@ -873,6 +949,7 @@ int gs_counters(gs_handle h, uint64_t* out8) {
   if (int rc = check(h)) return rc;
   if (!out8) return fail(GS_ERR_INVALID, "out is null");
   DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
   if (int rc = flush_hooks(h)) return rc;
   std::vector<uint32_t> c(gs::CTR_COUNT * gs::kCtrStride);
   GS_HIP(hipMemcpyAsync(c.data(), h->ctr, c.size() * 4, hipMemcpyDeviceToHost, h->stream));
@@ -888,6 +965,16 @@ int gs_counters(gs_handle h, uint64_t* out8) {
   out8[5] = c[gs::ctr_index(gs::CTR_DBG_HOOKS)];
   out8[6] = c[gs::ctr_index(gs::CTR_DBG_ITERS)];
   out8[7] = c[gs::ctr_index(gs::CTR_DBG_CASFAIL)];
+  return GS_OK;
+}
+
+int gs_set_pipelining(gs_handle h, int depth) {
+  if (int rc = check(h)) return rc;
+  if (depth < 1 || depth > gs_summary::kLanes) return fail(GS_ERR_INVALID, "pipelining depth must be 1..4");
+  DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
+  h->pipe_depth = depth;
+  h->lane_next = 0;
   return GS_OK;
 }
 

@@ -35,6 +35,10 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 #define GS_HOT_BUCKET 4
 #endif
 constexpr uint32_t kHotBucket = GS_HOT_BUCKET;  // hot-level bucket: slots loaded in one round trip
+#ifndef GS_FOLD_BS
+#define GS_FOLD_BS 256
+#endif
+constexpr uint32_t kFoldBS = GS_FOLD_BS;  // k_fold threads per block
 constexpr int kShards = 64;      // sharded append counters (one 128-B line each)
 constexpr int kCtrStride = 32;   // u32 per counter line
 constexpr int kActSets = 3;     // active-edge lists: appended at epoch e, drained at e+1, zeroed at e+2
@@ -56,6 +60,20 @@ enum CounterBlock : int {
   CTR_COUNT
 };
 __host__ __device__ constexpr int ctr_index(int c) { return c * kCtrStride; }
+
+#ifdef GS_DIAG_WAVES
+// Diagnostic build only (tools/diag_fold.hip): per-thread event counts of k_fold
+// {find steps, hook iterations, failed hook CASes, probe steps, key settles}.
+constexpr uint32_t kDiagThreads = 1u << 22;
+extern __device__ uint32_t gs_diag_cnt[kDiagThreads * 5];
+#define GS_DIAG(k)                                                              \
+  do {                                                                          \
+    const uint32_t dtid_ = blockIdx.x * blockDim.x + threadIdx.x;               \
+    if (dtid_ < kDiagThreads) gs_diag_cnt[dtid_ * 5 + (k)]++;                   \
+  } while (0)
+#else
+#define GS_DIAG(k) ((void)0)
+#endif
 
 struct alignas(16) Slot {
   int64_t key;
@@ -114,6 +132,7 @@ __device__ __forceinline__ uint32_t load_link_fresh(const Slot* p) {
 // memory-side atomic unit (rare path).
 __device__ __forceinline__ int64_t settle_key(const Table& t, uint32_t s, int64_t k) {
   if (k == kEmpty && s != t.r0) {
+    GS_DIAG(4);
     k = (int64_t)atomicOr((unsigned long long*)&t.tab[s].key, 0ull);
   }
   return k;
@@ -192,6 +211,7 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
     load_slot(t.tab + h, k, l);
   }
   for (uint32_t probes = 0; probes <= t.mask; ++probes) {
+    GS_DIAG(3);
     if (k == key) {
       link = l;
       return h;
@@ -260,6 +280,7 @@ __device__ __forceinline__ uint32_t lookup_find(const Table& t, int64_t key, uin
 // non-root forever and the grandparent is an ancestor: a benign race).
 __device__ __forceinline__ void find_step(const Table& t, uint32_t& x, uint32_t& lx, int64_t& kx, uint32_t& acc,
                                           bool& done, int64_t kp, uint32_t lp) {
+  GS_DIAG(0);
   const uint32_t p = lx >> 1;
   const uint32_t gp = lp >> 1;
   acc ^= lx & 1u;
@@ -332,6 +353,7 @@ __device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, 
   GS_DBG(CTR_DBG_HOOKS);
   while (true) {
     GS_DBG(CTR_DBG_ITERS);
+    GS_DIAG(1);
     uint32_t pa = 0, pb = 0;
     find_root2<true>(t, a, la, ka, pa, b, lb, kb, pb);
     la = a << 1;
@@ -363,6 +385,7 @@ __device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, 
     }
     // hi was hooked meanwhile: continue that side from its live link
     GS_DBG(CTR_DBG_CASFAIL);
+    GS_DIAG(2);
     if (a_lo)
       lb = old;
     else

@@ -15,6 +15,25 @@
 
 namespace gs {
 
+#ifdef GS_DIAG_WAVES
+// Diagnostic build only (tools/diag_fold.hip): per-wave {start, end, block, xcc}
+// of k_fold in 100 MHz wall-clock ticks.
+constexpr uint32_t kDiagWaves = 1u << 16;
+__device__ uint64_t gs_diag_waves[kDiagWaves * 2];
+__device__ uint32_t gs_diag_meta[kDiagWaves];
+__device__ uint32_t gs_diag_cnt[kDiagThreads * 5];
+void diag_copy(uint64_t* w, uint32_t* m, size_t nw, uint32_t* cnt, size_t nt) {
+  (void)hipMemcpyFromSymbol(w, HIP_SYMBOL(gs_diag_waves), nw * 16);
+  (void)hipMemcpyFromSymbol(m, HIP_SYMBOL(gs_diag_meta), nw * 4);
+  if (cnt) (void)hipMemcpyFromSymbol(cnt, HIP_SYMBOL(gs_diag_cnt), nt * 20);
+}
+void diag_clear(size_t nt) {
+  static uint32_t* z = nullptr;
+  if (!z) z = (uint32_t*)calloc(kDiagThreads * 5, 4);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(gs_diag_cnt), z, nt * 20);
+}
+#endif
+
 // slot s := {EMPTY, s << 1, 0}; the second reserved slot carries its id INT64_MIN + 1
 __global__ __launch_bounds__(256) void k_init(Slot* tab, uint64_t nslots) {
   for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
@@ -53,10 +72,10 @@ __device__ __forceinline__ void drain_set(const Table& t, const Lists& L, int se
   const uint32_t G = gridDim.x;
   if (G >= (uint32_t)kShards) {
     const uint32_t nparts = G / kShards, part = blockIdx.x / kShards;
-    if (part < nparts) drain_entries<SIGNED, TRACK>(t, L, set, blockIdx.x % kShards, part * 256u + threadIdx.x, nparts * 256u);
+    if (part < nparts) drain_entries<SIGNED, TRACK>(t, L, set, blockIdx.x % kShards, part * blockDim.x + threadIdx.x, nparts * blockDim.x);
   } else {
     for (uint32_t s = blockIdx.x; s < (uint32_t)kShards; s += G)
-      drain_entries<SIGNED, TRACK>(t, L, set, (int)s, threadIdx.x, 256u);
+      drain_entries<SIGNED, TRACK>(t, L, set, (int)s, threadIdx.x, blockDim.x);
   }
 }
 
@@ -84,8 +103,22 @@ struct FoldArgs {
 };
 
 template <bool SIGNED, bool TRACK, int EPT, bool HOT>
-__global__ __launch_bounds__(256) void k_fold(Table t, Lists L, FoldArgs a) {
+__global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Lists L, FoldArgs a) {
   if (!HOT) t.hotcap = 0;  // compile-time: the plain path carries no hot-level code
+#ifdef GS_DIAG_WAVES
+  const uint64_t diag_t0 = wall_clock64();
+  struct DiagEnd {
+    uint64_t t0;
+    __device__ ~DiagEnd() {
+      const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
+      if ((threadIdx.x & 63u) == 0 && w < kDiagWaves) {
+        gs_diag_waves[2 * w] = t0;
+        gs_diag_waves[2 * w + 1] = wall_clock64();
+        gs_diag_meta[w] = (blockIdx.x << 4) | (__builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 15u);
+      }
+    }
+  } diag_end{diag_t0};
+#endif
   if (SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0) return;
   const int shard = blockIdx.x & (kShards - 1);
   if (a.zero >= 0 && blockIdx.x == 0 && threadIdx.x < kShards)
@@ -96,7 +129,7 @@ __global__ __launch_bounds__(256) void k_fold(Table t, Lists L, FoldArgs a) {
   uint32_t need[EPT];
 #pragma unroll
   for (int e = 0; e < EPT; ++e) {
-    const uint32_t i = blockIdx.x * (256u * EPT) + e * 256u + threadIdx.x;
+    const uint32_t i = blockIdx.x * (kFoldBS * EPT) + e * kFoldBS + threadIdx.x;
     valid[e] = i < a.n;
     act[e] = false;
     if (valid[e] && a.rows) {  // exchange layout: per-rank header gives the live row count
@@ -105,8 +138,13 @@ __global__ __launch_bounds__(256) void k_fold(Table t, Lists L, FoldArgs a) {
     }
     const uint32_t wi = (valid[e] && a.w) ? a.w[(size_t)i * a.w_stride] : 1u;
     if (wi & 0x80u) valid[e] = false;
+#ifdef GS_NT_EDGES
+    ks[e] = valid[e] ? __builtin_nontemporal_load(&a.src[(size_t)i * a.stride]) : 0;
+    kd[e] = valid[e] ? __builtin_nontemporal_load(&a.dst[(size_t)i * a.stride]) : 0;
+#else
     ks[e] = valid[e] ? a.src[(size_t)i * a.stride] : 0;
     kd[e] = valid[e] ? a.dst[(size_t)i * a.stride] : 0;
+#endif
     need[e] = SIGNED ? (wi & 1u) : 0u;
   }
   // all first relabel probes of the thread in flight together
@@ -392,12 +430,13 @@ void launch_fold(bool sign, bool track, int ept, const Table& t, const Lists& L,
                  int drain, int zero, int inline_max, uint32_t rows, int skip_rank, const int64_t* hdr,
                  uint32_t base, hipStream_t st) {
   FoldArgs a{src, dst, w, n, stride, w_stride, rows, skip_rank, hdr, base, cur, drain, zero, inline_max};
-  const uint32_t per_block = 256u * (uint32_t)ept;
-  const dim3 g((n + per_block - 1) / per_block), b(256);
+  const uint32_t per_block = kFoldBS * (uint32_t)ept;
+  const dim3 g((n + per_block - 1) / per_block), b(kFoldBS);
   const bool hot = t.hotcap != 0;
+  static const size_t lds = getenv("GS_FOLD_LDS") ? (size_t)atoi(getenv("GS_FOLD_LDS")) : 0;  // occupancy experiment
 #define GS_FOLD(S, T, E, H)                                                       \
   if (sign == S && track == T && ept == E && hot == H) {                          \
-    hipLaunchKernelGGL((k_fold<S, T, E, H>), g, b, 0, st, t, L, a);               \
+    hipLaunchKernelGGL((k_fold<S, T, E, H>), g, b, lds, st, t, L, a);             \
     return;                                                                       \
   }
 #define GS_FOLD_H(S, T, E) GS_FOLD(S, T, E, false) GS_FOLD(S, T, E, true)

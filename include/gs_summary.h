@@ -82,6 +82,17 @@ int gs_fold(gs_handle h, const int64_t* src, const int64_t* dst, size_t n);
  * caller guarantees the inputs are complete before work on the handle's stream. */
 int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n, size_t stride);
 
+/* Pipelined windows: with depth d (1..4), up to d consecutive gs_fold_device calls
+ * may run concurrently on the device (fold b+1 starts while fold b drains), the way Flink
+ * runs the window fold of window w+1 while the Merger still handles window w
+ * (SummaryBulkAggregation.java:77-90 is a pipelined dataflow). Union is associative
+ * and commutative, so the forest after the folds is the same; every other call on
+ * the handle (reads, exports, combine, serialize, sync, gs_get_stream) first orders
+ * the handle's stream behind all pending folds. Device buffers passed to a
+ * pipelined fold must stay valid until that next call. Applies to plain folds
+ * (no delta tracking, hot level off, profiling off); depth 1 (default) = in order. */
+int gs_set_pipelining(gs_handle h, int depth);
+
 /* Merge summary `src` into `dst` (either may be on any device; `src` is unchanged).
  * Replaces CombineCC.reduce -> DisjointSet.merge (ConnectedComponents.java:116-126,
  * DisjointSet.java:127-131) and combineFunction.reduce -> Candidates.merge

@@ -176,6 +176,45 @@ def test_rmat20_config2_full(gs, oracle_mod):
         _assert_cc_equal(ds, oracle_mod, hs, hd)
 
 
+@pytest.mark.parametrize("hint", [1 << 18, 64])
+def test_pipelined_folds_match_ordered(gs, oracle_mod, hint):
+    # gs_set_pipelining(2): consecutive device folds overlap on two lane streams; the
+    # labels (and the growth path from a tiny hint) must match the oracle exactly.
+    import torch
+    n, b = 1 << 20, 1 << 15
+    s = torch.empty(n, dtype=torch.int64, device="cuda")
+    d = torch.empty(n, dtype=torch.int64, device="cuda")
+    gs.gen_rmat(s, d, 0, n, 18, 0x5EED0018, True)
+    torch.cuda.synchronize()
+    hs, hd = s.cpu().numpy(), d.cpu().numpy()
+    with gs.Summary("cc", capacity_hint=hint) as ds:
+        ds.set_pipelining(2)
+        for i in range(0, n, b):
+            ds.fold_device(s[i:], d[i:], n=b)
+            if i == n // 2:
+                assert ds.num_vertices() > 0  # a read in the middle joins the lanes
+        _assert_cc_equal(ds, oracle_mod, hs, hd)
+        ds.reset()
+        for i in range(0, n // 4, b):
+            ds.fold_device(s[i:], d[i:], n=b)
+        _assert_cc_equal(ds, oracle_mod, hs[:n // 4], hd[:n // 4])
+
+
+def test_pipelined_signed_folds(gs, oracle_mod):
+    s, d = oracle_mod.rmat_edges(0x5EED0B1C, 14, 0, 1 << 16, True)
+    import torch
+    ts = torch.from_numpy(s).cuda()
+    td = torch.from_numpy(d).cuda()
+    with gs.Summary("signed", capacity_hint=1 << 14) as a, gs.Summary("signed", capacity_hint=1 << 14) as b:
+        a.set_pipelining(2)
+        for i in range(0, len(s), 1 << 12):
+            a.fold_device(ts[i:], td[i:], n=1 << 12)
+            b.fold_device(ts[i:], td[i:], n=1 << 12)
+        ca, cb = a.colouring(), b.colouring()
+        assert ca[0] == cb[0]
+        assert all(np.array_equal(x, y) for x, y in zip(ca[1:], cb[1:]))
+
+
 # ------------------------------------------------------------- combine / serialize / delta
 def test_combine_equals_whole(gs, oracle_mod):
     s, d = oracle_mod.rmat_edges(3, 14, 0, 1 << 16, True)
