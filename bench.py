@@ -34,6 +34,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--workload", choices=["rmat-cc", "bip", "er-latency"], default="rmat-cc",
+                   help="rmat-cc: BASELINE config 3 (the headline line); bip: config 4 (bipartiteness, "
+                        "2x2^19 vertices, 2^24 edges); er-latency: config 5 (ER G(2^22, 2^26), 2^16-edge windows, "
+                        "per-window latency)")
     p.add_argument("--scale", type=int, default=26)
     p.add_argument("--edge-factor", type=int, default=16)
     p.add_argument("--log-batch", type=int, default=20)
@@ -63,8 +67,121 @@ class NativeExchange:
         self.g.finish()
 
 
+def bench_bip(args):
+    """BASELINE config 4: random bipartite stream, sides of 2^19 vertices, E = 2^24, 2^20-edge
+    windows, signed (parity) union-find. Throughput on the clean stream (nothing skipped: a failed
+    verdict would short-circuit the fold); verdict check on the odd-cycle variant (edges injected at
+    E/8, E/4, E/2, 3E/4): the verdict must flip in the window of the first conflicting edge."""
+    import gsamd as gs
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    logside, E, B, seed = 19, 1 << 24, 1 << 20, 0x5EED0B1B
+    summ = gs.Summary("signed", device=0, capacity_hint=1 << 20)
+    src = torch.empty(E, dtype=torch.int64, device=dev)
+    dst = torch.empty(E, dtype=torch.int64, device=dev)
+    gs.gen_bip(src, dst, 0, E, logside, seed, [], stream=summ.stream)
+    summ.sync()
+    if args.pipeline > 1:
+        summ.set_pipelining(args.pipeline)
+    ok = [True]
+
+    def one_step():
+        summ.reset()
+        for o in range(0, E, B):
+            summ.fold_device(src[o:], dst[o:], n=min(B, E - o))
+        ok[0] = summ.ok()  # the verdict read joins every pending fold
+
+    for _ in range(args.warmup):
+        one_step()
+    summ.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    summ.sync()
+    el = time.perf_counter() - t0
+    # odd-cycle variant: verdict per window against the parity union-find truth
+    inject = [E // 8, E // 4, E // 2, 3 * E // 4]
+    gs.gen_bip(src, dst, 0, E, logside, seed, inject, stream=summ.stream)
+    summ.reset()
+    flip = None
+    for o in range(0, E, B):
+        summ.fold_device(src[o:], dst[o:], n=B)
+        if flip is None and not summ.ok():
+            flip = o // B
+    import oracle  # checker only
+    first = oracle.bip_first_failure(src.cpu().numpy(), dst.cpu().numpy())
+    expect = None if first < 0 else first // B
+    line = {"metric": "edges/sec for streaming bipartiteness (config 4)", "value": round(E * args.steps / el, 1),
+            "unit": "edges/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": "bip-config4", "side_vertices": 1 << logside, "edges": E, "micro_batch": B,
+                       "clean_stream_bipartite": bool(ok[0]), "odd_cycle_flip_window": flip,
+                       "odd_cycle_flip_window_truth": expect, "verdict_parity": flip == expect}}
+    print(json.dumps(line), flush=True)
+    summ.close()
+
+
+def bench_er_latency(args):
+    """BASELINE config 5: Erdos-Renyi G(n = 2^22, m = 2^26), 1024 windows of 2^16 edges. Per
+    window: fold (delta tracking on) + delta export into device memory (the records the
+    Merger/combine consumes) + completion; host steady-clock latency per window, p50/p99."""
+    import gsamd as gs
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    logn, E, B, seed = 22, 1 << 26, 1 << 16, 0x5EED00E5
+    summ = gs.Summary("cc", device=0, capacity_hint=1 << logn)
+    src = torch.empty(E, dtype=torch.int64, device=dev)
+    dst = torch.empty(E, dtype=torch.int64, device=dev)
+    gs.gen_er(src, dst, 0, E, logn, seed, True, stream=summ.stream)
+    summ.set_delta_tracking(True)
+    cap = 3 * B + 16
+    rec = torch.empty(cap * 3, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    summ.sync()
+    lat = []
+    nrec = torch.zeros(1, dtype=torch.int64, device=dev)
+    for step in range(args.warmup + 1):
+        summ.reset()
+        lat = []
+        nrec.zero_()
+        for o in range(0, E, B):
+            t0 = time.perf_counter()
+            summ.fold_device(src[o:], dst[o:], n=B)
+            summ.take_delta_records(rec, cap, cnt)
+            summ.sync()
+            lat.append(time.perf_counter() - t0)
+            nrec.add_(cnt)  # outside the timed window (torch's stream, after the sync)
+    nrec = int(nrec.item())
+    lat = np.array(lat) * 1e6
+    tot = lat.sum() * 1e-6
+    import oracle  # CPU baseline leg only: the 1-thread restatement on the first 64 windows
+    nw = 64
+    cl = oracle.cpu_window_latency_cc(src[:nw * B].cpu().numpy(), dst[:nw * B].cpu().numpy(), B) * 1e6
+    cpu = {"value": round(float(np.percentile(cl, 50)), 2), "unit": "us", "cores": 1, "kind": "port",
+           "p99_us": round(float(np.percentile(cl, 99)), 2),
+           "sample": "first %d windows of the same stream, DisjointSet.union per edge + CombineCC/Merger per "
+                     "window (oracle/gs_oracle.cpp), 1 thread, %.1f s" % (nw, cl.sum() * 1e-6)}
+    line = {"metric": "per-window latency p50 (us) for streaming CC on ER (config 5)",
+            "value": round(float(np.percentile(lat, 50)), 2), "unit": "us", "n_gpus": 1, "steps": 1,
+            "warmup": args.warmup, "ms_per_step": round(tot * 1e3, 3), "higher_is_better": False,
+            "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": "er-latency-config5", "n": 1 << logn, "edges": E, "micro_batch": B,
+                       "windows": E // B, "p50_us": round(float(np.percentile(lat, 50)), 2),
+                       "p99_us": round(float(np.percentile(lat, 99)), 2), "max_us": round(float(lat.max()), 2),
+                       "edges_per_s": round(E / tot, 1), "delta_records": nrec,
+                       "per_window": "fold + delta export to device + completion (host steady clock)"},
+            "cpu_baseline": cpu}
+    print(json.dumps(line), flush=True)
+    summ.close()
+
+
 def main():
     args = parse()
+    if args.workload == "bip":
+        return bench_bip(args)
+    if args.workload == "er-latency":
+        return bench_er_latency(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -62,6 +62,7 @@ struct gs_summary {
   bool hot_open = false;
   uint64_t hot_target = 0;
   uint32_t* h_nv = nullptr;  // pinned copy of the new-vertex counter block
+  uint32_t* h_flags = nullptr;  // pinned: error / overflow flags
   hipEvent_t nv_ev = nullptr;
   bool nv_pending = false;
   uint32_t* ctr = nullptr;
@@ -208,13 +209,15 @@ int join_lanes(gs_summary* h) {
   return GS_OK;
 }
 
+// Error flags, read with ONE host synchronisation (pinned copies queued behind the
+// handle's work, then a single stream sync).
 int check_device_flags(gs_summary* h) {
-  uint32_t flags[2] = {0, 0};
-  GS_HIP(hipMemcpyAsync(&flags[0], h->ctr + gs::ctr_index(gs::CTR_ERR), 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipMemcpyAsync(&flags[1], h->ctr + gs::ctr_index(gs::CTR_OVF), 4, hipMemcpyDeviceToHost, h->stream));
+  uint32_t* f = h->h_flags;
+  GS_HIP(hipMemcpyAsync(&f[0], h->ctr + gs::ctr_index(gs::CTR_ERR), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipMemcpyAsync(&f[1], h->ctr + gs::ctr_index(gs::CTR_OVF), 4, hipMemcpyDeviceToHost, h->stream));
   GS_HIP(hipStreamSynchronize(h->stream));
-  if (flags[0]) return fail(GS_ERR_CAPACITY, "vertex table overflow (device probe limit)");
-  if (flags[1]) return fail(GS_ERR_CAPACITY, "delta/active list overflow: take the delta after each fold");
+  if (f[0]) return fail(GS_ERR_CAPACITY, "vertex table overflow (device probe limit)");
+  if (f[1]) return fail(GS_ERR_CAPACITY, "delta/active list overflow: take the delta after each fold");
   return GS_OK;
 }
 
@@ -493,7 +496,8 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   if (hipEventCreateWithFlags(&h->main_ev, hipEventDisableTiming) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
   if (hipEventCreateWithFlags(&h->nv_ev, hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc(&h->h_nv, gs::kShards * gs::kCtrStride * 4, hipHostMallocDefault) != hipSuccess)
+      hipHostMalloc(&h->h_nv, gs::kShards * gs::kCtrStride * 4, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&h->h_flags, 16, hipHostMallocDefault) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hot-level bookkeeping allocation failed"));
   rc = alloc_table(h, cap);
   if (rc) return bail(rc);
@@ -518,6 +522,7 @@ int gs_destroy(gs_handle h) {
     if (h->stage_ev[i]) (void)hipEventDestroy(h->stage_ev[i]);
   if (h->nv_ev) (void)hipEventDestroy(h->nv_ev);
   if (h->h_nv) (void)hipHostFree(h->h_nv);
+  if (h->h_flags) (void)hipHostFree(h->h_flags);
   (void)hipFree(h->tab);
   (void)hipFree(h->ctr);
   (void)hipFree(h->act);
@@ -610,8 +615,7 @@ int gs_sync(gs_handle h) {
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
   if (int rc = flush_hooks(h)) return rc;
-  GS_HIP(hipStreamSynchronize(h->stream));
-  return check_device_flags(h);
+  return check_device_flags(h);  // its one stream sync completes all queued work
 }
 
 int gs_num_vertices(gs_handle h, uint64_t* n) {
@@ -879,10 +883,15 @@ int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count
   if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  if (int rc = stage(h, nullptr, 0)) return rc;  // everything into the queue
-  gs::launch_copy_queue(h->q[h->qsel], h->qn + h->qsel, h->qcap, rec, cap, count, h->stream);
+  // one launch: backlog + fresh delta straight into rec (first cap), total -> *count
+  if (int rc = flush_hooks(h)) return rc;
+  if (int rc = ensure_queue(h)) return rc;
+  const int a = h->qsel, b = h->qsel ^ 1;
+  gs::launch_stage(h->table(), h->lists(), h->q[a], h->qn + a, h->q[b], h->qn + b, h->qcap, rec, cap, h->stream,
+                   reinterpret_cast<unsigned long long*>(count));
   GS_HIP(hipGetLastError());
-  GS_HIP(hipMemsetAsync(h->qn, 0, 16, h->stream));
+  h->qsel = b;
+  h->delta_fill_ub = 0;
   return GS_OK;
 }
 

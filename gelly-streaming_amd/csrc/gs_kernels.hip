@@ -320,10 +320,12 @@ __global__ __launch_bounds__(256) void k_export(Table t, int64_t* __restrict__ o
 // reads `sent` from the header, so unused send rows need no padding.
 // cap == 0 with send == nullptr: everything goes to q_out (gs_take_delta_records).
 __device__ __forceinline__ void stage_write(const Table& t, unsigned long long pos, int64_t a, int64_t b, int64_t w,
-                                            int64_t* send, uint64_t cap, int64_t* q_out, uint64_t qcap) {
+                                            int64_t* send, uint64_t cap, int64_t* q_out, uint64_t qcap, bool plain) {
   int64_t* r;
   if (pos < cap) {
-    r = send + (pos + 1) * 3;
+    r = send + (pos + (plain ? 0 : 1)) * 3;
+  } else if (plain) {
+    return;  // take: records past cap are dropped (the caller sees the total count)
   } else if (pos - cap < qcap) {
     r = q_out + (pos - cap) * 3;
   } else {
@@ -342,7 +344,8 @@ __device__ __forceinline__ void stage_write(const Table& t, unsigned long long p
 __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* __restrict__ q_in,
                                                unsigned long long* qn_in, int64_t* __restrict__ q_out,
                                                unsigned long long* qn_out, uint64_t qcap, int64_t* __restrict__ send,
-                                               uint64_t cap) {
+                                               uint64_t cap, unsigned long long* count_out) {
+  const bool plain = count_out != nullptr;  // take: rows from 0, no header, total -> *count_out
   __shared__ uint32_t cnt[kShards];
   __shared__ uint64_t off_sh, total_sh;
   const uint32_t s = blockIdx.x;
@@ -363,13 +366,17 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* 
   // backlog slice s
   const uint64_t per = (backlog + kShards - 1) / kShards;
   const uint64_t b0 = (uint64_t)s * per, b1 = min(backlog, b0 + per);
-  for (uint64_t i = b0 + threadIdx.x; i < b1; i += 256) stage_write(t, i, q_in[i * 3], q_in[i * 3 + 1], q_in[i * 3 + 2], send, cap, q_out, qcap);
+  for (uint64_t i = b0 + threadIdx.x; i < b1; i += 256) stage_write(t, i, q_in[i * 3], q_in[i * 3 + 1], q_in[i * 3 + 2], send, cap, q_out, qcap, plain);
   // delta shard s
   const int64_t* in = L.drec + (size_t)s * L.delta_shard_cap * 3;
   const uint64_t off = off_sh;
   for (uint32_t j = threadIdx.x; j < cnt[s]; j += 256)
-    stage_write(t, off + j, in[(size_t)j * 3], in[(size_t)j * 3 + 1], in[(size_t)j * 3 + 2], send, cap, q_out, qcap);
-  if (s == 0 && threadIdx.x == 0) {
+    stage_write(t, off + j, in[(size_t)j * 3], in[(size_t)j * 3 + 1], in[(size_t)j * 3 + 2], send, cap, q_out, qcap,
+                plain);
+  if (s == 0 && threadIdx.x == 0 && plain) {
+    *count_out = total;
+    *qn_out = 0ull;
+  } else if (s == 0 && threadIdx.x == 0) {
     const uint64_t sent = total < cap ? total : cap;
     if (send) {
       send[0] = (int64_t)sent;
@@ -390,17 +397,6 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* 
     *qn_in = 0ull;
     atomicExch(&t.ctr[ctr_index(CTR_STAGE_DONE)], 0u);
   }
-}
-
-// Copy the whole record queue (first cap records) and its count out.
-__global__ __launch_bounds__(256) void k_copy_queue(const int64_t* __restrict__ q, const unsigned long long* qn,
-                                                    uint64_t qcap, int64_t* __restrict__ out, uint64_t cap,
-                                                    uint64_t* count) {
-  const uint64_t total = min((unsigned long long)*qn, (unsigned long long)qcap);
-  const uint64_t n = total < cap ? total : cap;
-  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gtid == 0) *count = total;
-  for (uint64_t i = gtid; i < n * 3; i += (uint64_t)gridDim.x * blockDim.x) out[i] = q[i];
 }
 
 // Single-vertex lookup (gs_find): label and presence.
@@ -471,13 +467,10 @@ void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t*
 }
 
 void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned long long* qn_in, int64_t* q_out,
-                  unsigned long long* qn_out, uint64_t qcap, int64_t* send, uint64_t cap, hipStream_t st) {
-  hipLaunchKernelGGL(k_stage, dim3(kShards), dim3(256), 0, st, t, L, q_in, qn_in, q_out, qn_out, qcap, send, cap);
-}
-
-void launch_copy_queue(const int64_t* q, const unsigned long long* qn, uint64_t qcap, int64_t* out, uint64_t cap,
-                       uint64_t* count, hipStream_t st) {
-  hipLaunchKernelGGL(k_copy_queue, dim3(1024), dim3(256), 0, st, q, qn, qcap, out, cap, count);
+                  unsigned long long* qn_out, uint64_t qcap, int64_t* send, uint64_t cap, hipStream_t st,
+                  unsigned long long* count_out) {
+  hipLaunchKernelGGL(k_stage, dim3(kShards), dim3(256), 0, st, t, L, q_in, qn_in, q_out, qn_out, qcap, send, cap,
+                     count_out);
 }
 
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st) {

@@ -20,9 +20,8 @@ void launch_hook(bool sign, bool track, const Table& t, const Lists& L, int set,
 void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out,
                    hipStream_t st);
 void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned long long* qn_in, int64_t* q_out,
-                  unsigned long long* qn_out, uint64_t qcap, int64_t* send, uint64_t cap, hipStream_t st);
-void launch_copy_queue(const int64_t* q, const unsigned long long* qn, uint64_t qcap, int64_t* out, uint64_t cap,
-                       uint64_t* count, hipStream_t st);
+                  unsigned long long* qn_out, uint64_t qcap, int64_t* send, uint64_t cap, hipStream_t st,
+                  unsigned long long* count_out = nullptr);
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st);
 
 }  // namespace gs

@@ -51,6 +51,9 @@ def lib():
         L.or_cpu_baseline_cc.restype = ctypes.c_double
         L.or_cpu_baseline_cc_threads.argtypes = [_i64p, _i64p, _sz, _sz, ctypes.c_int]
         L.or_cpu_baseline_cc_threads.restype = ctypes.c_double
+        L.or_cpu_window_latency_cc.argtypes = [_i64p, _i64p, _sz, _sz,
+                                               np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")]
+        L.or_cpu_window_latency_cc.restype = None
         L.or_cpu_baseline_bip.argtypes = [_i64p, _i64p, _sz]
         L.or_cpu_baseline_bip.restype = ctypes.c_double
         _lib = L
@@ -155,6 +158,14 @@ def cpu_baseline_cc(src, dst, window, threads=1):
     if threads <= 1:
         return lib().or_cpu_baseline_cc(src, dst, len(src), window)
     return lib().or_cpu_baseline_cc_threads(src, dst, len(src), window, threads)
+
+
+def cpu_window_latency_cc(src, dst, window):
+    """Seconds per window (fold + CombineCC/Merger) of the 1-thread restatement."""
+    src, dst = _arr(src), _arr(dst)
+    out = np.zeros((len(src) + window - 1) // window, np.float64)
+    lib().or_cpu_window_latency_cc(src, dst, len(src), window, out)
+    return out
 
 
 def cpu_baseline_bip(src, dst):

@@ -647,6 +647,23 @@ double or_cpu_baseline_cc_threads(const int64_t* src, const int64_t* dst, size_t
   return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// Per-window latency of the 1-thread restatement (config 5 CPU leg): window fold +
+// CombineCC into the running summary (the Merger), seconds per window into out[].
+void or_cpu_window_latency_cc(const int64_t* src, const int64_t* dst, size_t n, size_t window, double* out) {
+  DisjointSet summary;
+  size_t w = 0;
+  for (size_t i = 0; i < n; i += window, ++w) {
+    auto t0 = std::chrono::steady_clock::now();
+    size_t j = std::min(n, i + window);
+    DisjointSet part;
+    for (size_t k = i; k < j; ++k) part.unite(src[k], dst[k]);
+    DisjointSet r;
+    combine_cc(part, summary, &r);
+    summary = std::move(r);
+    out[w] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+}
+
 // Quirk-exact Candidates fold of a prefix, one window, p = 1; returns wall seconds.
 double or_cpu_baseline_bip(const int64_t* src, const int64_t* dst, size_t n) {
   auto t0 = std::chrono::steady_clock::now();
