@@ -34,7 +34,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--workload", choices=["rmat-cc", "bip", "er-latency"], default="rmat-cc",
+    p.add_argument("--workload", choices=["rmat-cc", "bip", "er-latency", "ingest"], default="rmat-cc",
                    help="rmat-cc: BASELINE config 3 (the headline line); bip: config 4 (bipartiteness, "
                         "2x2^19 vertices, 2^24 edges); er-latency: config 5 (ER G(2^22, 2^26), 2^16-edge windows, "
                         "per-window latency)")
@@ -176,8 +176,65 @@ def bench_er_latency(args):
     summ.close()
 
 
+def bench_ingest(args):
+    """Text edge ingest: 2^24 RMAT-26 edges as "src dst\\n" text
+    (sparse 64-bit ids, ~640 MB). Device leg: text resident in HBM -> gs_parse_edges_device
+    (count pass + parse pass) -> int64 src/dst. Host leg: gs_fold_text from host memory
+    (pinned staging over PCIe, parse, fold) into a CC summary."""
+    import gsamd as gs
+    import oracle  # input formatting + CPU baseline leg only
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    E = 1 << 24
+    src = torch.empty(E, dtype=torch.int64, device=dev)
+    dst = torch.empty(E, dtype=torch.int64, device=dev)
+    gs.gen_rmat(src, dst, 0, E, 26, 0x5EED0026, True)
+    torch.cuda.synchronize()
+    hs, hd = src.cpu().numpy(), dst.cpu().numpy()
+    text_h = oracle.format_edges(hs, hd, 0)
+    text = torch.from_numpy(text_h).to(dev)
+    ps = torch.empty(E, dtype=torch.int64, device=dev)
+    pd = torch.empty(E, dtype=torch.int64, device=dev)
+    for _ in range(args.warmup):
+        gs.parse_edges_device(text, ps, pd)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n, bad = gs.parse_edges_device(text, ps, pd)
+    el = (time.perf_counter() - t0) / args.steps
+    ok = n == E and bad == -1 and bool(torch.equal(ps, src)) and bool(torch.equal(pd, dst))
+    nbytes = int(text.numel())
+    alg = nbytes + 16 * E  # text read once + int64 pair written per edge
+    with gs.Summary("cc", device=0, capacity_hint=1 << 26) as summ:
+        th = bytes(text_h)
+        t1 = time.perf_counter()
+        nf = summ.fold_text(th)
+        summ.sync()
+        host_el = time.perf_counter() - t1
+    m = 1 << 20
+    sample = bytes(text_h[: int(np.searchsorted(np.cumsum(text_h == 10), m)) + 1])
+    c0 = time.perf_counter()
+    oracle.parse_edges(sample, 0)
+    cpu_el = time.perf_counter() - c0
+    line = {"metric": "text edge ingest: edges/sec parsed from device-resident text", "value": round(E / el, 1),
+            "unit": "edges/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el * 1e3, 3), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "ingest-rmat26-text", "edges": E, "text_bytes": nbytes, "parity": ok,
+                       "text_GBps": round(nbytes / el / 1e9, 1),
+                       "host_fold_text_edges_per_s": round(nf / host_el, 1),
+                       "host_fold_text_GBps": round(nbytes / host_el / 1e9, 2)},
+            "roofline": {"kernel": "k_count_lines + k_parse", "bound": "hbm", "achieved": round(alg / el / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / el / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": None, "note": "algorithmic bytes = text + 16 B/edge; wall time incl. sync"},
+            "cpu_baseline": {"value": round(m / cpu_el, 1), "unit": "edges/s", "cores": 1, "kind": "port",
+                             "sample": "first 2^20 lines, split + Long.parseLong restatement (oracle/gs_oracle.cpp)"}}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.workload == "ingest":
+        return bench_ingest(args)
     if args.workload == "bip":
         return bench_bip(args)
     if args.workload == "er-latency":

@@ -27,6 +27,10 @@ GS_ERR_INVALID = -1
 GS_ERR_HIP = -2
 GS_ERR_CAPACITY = -3
 GS_ERR_TRUNCATED = -4
+GS_ERR_PARSE = -5
+
+SEP_WHITESPACE = 0  # split("\\s") (ConnectedComponentsExample.java:113)
+SEP_TAB = 1         # split("\\t") (BipartitenessCheckExample.java:101)
 
 KERNEL_IDS = {"fold": 0, "hook": 1, "export": 2, "init": 3}
 
@@ -38,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "gs_take_delta_records", "gs_delta_stage", "gs_fold_records_device", "gs_fold_exchange_device",
     "gs_get_stream", "gs_set_pipelining", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity", "gs_counters",
     "gs_gen_rmat", "gs_gen_er", "gs_gen_bip",
+    "gs_parse_edges_device", "gs_fold_text",
     "gs_group_unique_id", "gs_group_create", "gs_group_fold_device", "gs_group_finish", "gs_group_stats",
     "gs_group_destroy",
 )
@@ -106,6 +111,9 @@ def lib():
     L.gs_gen_rmat.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, ctypes.c_int]
     L.gs_gen_er.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, ctypes.c_int]
     L.gs_gen_bip.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, _vp, _sz]
+    L.gs_parse_edges_device.argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp, _vp, _sz, ctypes.POINTER(_u64),
+                                        ctypes.POINTER(_i64)]
+    L.gs_fold_text.argtypes = [_vp, ctypes.c_char_p, _sz, ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(_i64)]
     L.gs_group_unique_id.argtypes = [_vp]
     L.gs_group_create.argtypes = [ctypes.POINTER(_vp), _vp, _vp, ctypes.c_int, ctypes.c_int, _sz, _sz]
     L.gs_group_fold_device.argtypes = [_vp, _vp, _vp, _sz]
@@ -284,6 +292,16 @@ class Summary:
     def set_profiling(self, on=True):
         _check(lib().gs_set_profiling(self._h, 1 if on else 0))
 
+    def fold_text(self, text, sep=SEP_WHITESPACE):
+        """gs_fold_text: parse edge lines from host bytes (reference source-map
+        semantics, include/gs_ingest.h) and fold them. Returns the edge count;
+        raises GSError(GS_ERR_PARSE) naming the first malformed line."""
+        text = bytes(text)
+        n = _u64()
+        bad = _i64(-1)
+        _check(lib().gs_fold_text(self._h, text, len(text), int(sep), ctypes.byref(n), ctypes.byref(bad)))
+        return n.value
+
     def set_pipelining(self, depth=2):
         """gs_set_pipelining: depth 2 lets consecutive device folds overlap on the
         device (pipelined windows); any read orders behind them."""
@@ -357,6 +375,21 @@ class Group:
 
 
 # ---------------------------------------------------------------- generators
+def parse_edges_device(text, src, dst, sep=SEP_WHITESPACE, stream=None):
+    """gs_parse_edges_device: device uint8 text -> device int64 src/dst. Returns
+    (n_lines, bad_line); bad_line = first malformed line or -1 (no exception for a
+    malformed line or a short output: the caller compares n_lines with capacity)."""
+    n = _u64()
+    bad = _i64(-1)
+    ln = text.numel() if hasattr(text, "numel") else len(text)
+    cap = src.numel() if hasattr(src, "numel") else len(src)
+    rc = lib().gs_parse_edges_device(stream, _ptr(text), ln, int(sep), _ptr(src), _ptr(dst), cap, ctypes.byref(n),
+                                     ctypes.byref(bad))
+    if rc not in (GS_OK, GS_ERR_PARSE, GS_ERR_TRUNCATED):
+        raise GSError(rc, "gs_parse_edges_device failed")
+    return n.value, bad.value
+
+
 def gen_rmat(src, dst, start, count, scale, seed, scramble=True, stream=None):
     rc = lib().gs_gen_rmat(stream, _ptr(src), _ptr(dst), start, count, scale, seed, 1 if scramble else 0)
     if rc:

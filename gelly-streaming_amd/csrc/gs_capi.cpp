@@ -11,8 +11,11 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
+#include "gs_ingest.h"
+#include "gs_ingest.hpp"
 #include "gs_kernels.hpp"
 #include "gs_summary.h"
 
@@ -99,6 +102,15 @@ struct gs_summary {
   // pipelined folds (gs_set_pipelining): consecutive device folds alternate over
   // two lane streams so that fold b+1 may start while fold b drains; every other
   // entry point joins the lanes onto `stream` first (join_lanes).
+  // text ingest (gs_fold_text): pinned + device text chunks, parsed edges, scratch
+  char* h_text = nullptr;  // pinned [2][kTextChunk]
+  uint64_t* h_tres = nullptr;  // pinned [2][2] parse results
+  hipEvent_t text_ev[2] = {nullptr, nullptr};
+  char* d_text = nullptr;
+  int64_t* d_tsrc = nullptr;
+  int64_t* d_tdst = nullptr;
+  void* d_tscratch = nullptr;
+  gs::ParseScratch tscratch;
   int pipe_depth = 1;
   static constexpr int kLanes = 4;
   hipStream_t lane[kLanes] = {};
@@ -523,6 +535,14 @@ int gs_destroy(gs_handle h) {
   if (h->nv_ev) (void)hipEventDestroy(h->nv_ev);
   if (h->h_nv) (void)hipHostFree(h->h_nv);
   if (h->h_flags) (void)hipHostFree(h->h_flags);
+  if (h->h_text) (void)hipHostFree(h->h_text);
+  if (h->h_tres) (void)hipHostFree(h->h_tres);
+  for (int i = 0; i < 2; ++i)
+    if (h->text_ev[i]) (void)hipEventDestroy(h->text_ev[i]);
+  (void)hipFree(h->d_text);
+  (void)hipFree(h->d_tsrc);
+  (void)hipFree(h->d_tdst);
+  (void)hipFree(h->d_tscratch);
   (void)hipFree(h->tab);
   (void)hipFree(h->ctr);
   (void)hipFree(h->act);
@@ -974,6 +994,95 @@ int gs_counters(gs_handle h, uint64_t* out8) {
   out8[5] = c[gs::ctr_index(gs::CTR_DBG_HOOKS)];
   out8[6] = c[gs::ctr_index(gs::CTR_DBG_ITERS)];
   out8[7] = c[gs::ctr_index(gs::CTR_DBG_CASFAIL)];
+  return GS_OK;
+}
+
+// ---- text ingest (include/gs_ingest.h) ----
+namespace {
+constexpr size_t kTextChunk = 16u << 20;  // bytes of text per parse + fold
+}
+
+// Copy into pinned staging with a few threads (one core's memcpy is far below PCIe).
+static void staged_copy(char* dst, const char* src, size_t n) {
+  const int nt = n >= (4u << 20) ? 8 : 1;
+  if (nt == 1) {
+    memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) {
+    const size_t a = n * t / nt, b = n * (t + 1) / nt;
+    th.emplace_back([=] { memcpy(dst + a, src + a, b - a); });
+  }
+  for (auto& x : th) x.join();
+}
+
+// End of the chunk that starts at off: after the last '\n' within kTextChunk bytes
+// (the whole rest when it fits); 0 = a single line longer than a chunk.
+static size_t chunk_end(const char* text, size_t len, size_t off) {
+  if (len - off <= kTextChunk) return len;
+  size_t end = off + kTextChunk;
+  while (end > off && text[end - 1] != '\n') --end;
+  return end == off ? 0 : end;
+}
+
+int gs_fold_text(gs_handle h, const char* text, size_t len, int sep, uint64_t* n_edges, int64_t* bad_line) {
+  if (int rc = check(h)) return rc;
+  if (!n_edges || !bad_line || (len && !text)) return fail(GS_ERR_INVALID, "null argument");
+  if (sep != GS_SEP_WHITESPACE && sep != GS_SEP_TAB) return fail(GS_ERR_INVALID, "unknown separator");
+  DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
+  *n_edges = 0;
+  *bad_line = -1;
+  const size_t max_lines = kTextChunk / 2 + 2;  // every line has >= 1 byte + '\n'
+  if (!h->h_text) {
+    size_t cub = 0;
+    const size_t sb = gs::parse_scratch_bytes(kTextChunk, &cub);
+    GS_HIP(hipHostMalloc(&h->h_text, 2 * kTextChunk, hipHostMallocDefault));
+    GS_HIP(hipHostMalloc(&h->h_tres, 4 * sizeof(uint64_t), hipHostMallocDefault));
+    GS_HIP(hipMalloc(&h->d_text, 2 * kTextChunk));
+    GS_HIP(hipMalloc(&h->d_tsrc, max_lines * 8));
+    GS_HIP(hipMalloc(&h->d_tdst, max_lines * 8));
+    GS_HIP(hipMalloc(&h->d_tscratch, sb));
+    for (int i = 0; i < 2; ++i) GS_HIP(hipEventCreateWithFlags(&h->text_ev[i], hipEventDisableTiming));
+    gs::parse_scratch_init(h->tscratch, h->d_tscratch, kTextChunk);
+  }
+  // Double-buffered: while chunk k is copied to the device, parsed and folded, the
+  // host copies chunk k+1 into the other pinned buffer.
+  auto enqueue = [&](int b, size_t c) -> int {
+    char* dt = h->d_text + (size_t)b * kTextChunk;
+    GS_HIP(hipMemcpyAsync(dt, h->h_text + (size_t)b * kTextChunk, c, hipMemcpyHostToDevice, h->stream));
+    if (gs::parse_text_enqueue(h->stream, dt, c, sep, h->d_tsrc, h->d_tdst, max_lines, h->tscratch))
+      return fail(GS_ERR_HIP, "text parse launch failed");
+    GS_HIP(hipMemcpyAsync(h->h_tres + 2 * b, h->tscratch.res, 16, hipMemcpyDeviceToHost, h->stream));
+    GS_HIP(hipEventRecord(h->text_ev[b], h->stream));
+    return GS_OK;
+  };
+  if (len == 0) return GS_OK;
+  size_t end = chunk_end(text, len, 0);
+  if (!end) return fail(GS_ERR_INVALID, "a line is longer than the 16 MiB ingest chunk");
+  staged_copy(h->h_text, text, end);
+  if (int rc = enqueue(0, end)) return rc;
+  uint64_t line0 = 0;
+  for (int b = 0;; b ^= 1) {
+    // host: the next chunk into the other pinned buffer (its previous H2D is done:
+    // that chunk's event was waited for in the previous iteration)
+    const size_t noff = end, nend = noff < len ? chunk_end(text, len, noff) : noff;
+    if (noff < len && !nend) return fail(GS_ERR_INVALID, "a line is longer than the 16 MiB ingest chunk");
+    if (noff < len) staged_copy(h->h_text + (size_t)(b ^ 1) * kTextChunk, text + noff, nend - noff);
+    GS_HIP(hipEventSynchronize(h->text_ev[b]));
+    const uint64_t nl = h->h_tres[2 * b], bad = h->h_tres[2 * b + 1];
+    if (bad != ~0ull) {
+      *bad_line = (int64_t)(line0 + bad);
+      return fail(GS_ERR_PARSE, "malformed edge line " + std::to_string(*bad_line));
+    }
+    if (int rc = fold_device_impl(h, h->d_tsrc, h->d_tdst, nullptr, nl, 1, 1, h->track)) return rc;
+    *n_edges += nl;
+    line0 += nl;
+    if (noff >= len) break;
+    if (int rc = enqueue(b ^ 1, nend - noff)) return rc;  // stream order: after this chunk's fold
+    end = nend;
+  }
   return GS_OK;
 }
 

@@ -1,0 +1,277 @@
+// gs_ingest.hip -- text edge-file parsing on the GPU (include/gs_ingest.h).
+//
+// Replaces the reference's source map `s.split("\\s")` / `s.split("\\t")` +
+// Long.parseLong(fields[0..1]) over env.readTextFile lines
+// (ConnectedComponentsExample.java:109-118, BipartitenessCheckExample.java:97-106).
+//
+// Two launches + one scan, all HBM-streaming:
+//   k_count_lines : per 4 KiB tile, the number of '\n' (coalesced 16-B loads)
+//   exclusive scan of the tile counts (hipcub) -> '\n' before each tile
+//   k_parse       : per tile, the tile (+ 512 B of the next) is staged in LDS; every
+//                   thread owns 16 bytes, finds the line starts in them (byte after a
+//                   '\n'), numbers each line from the tile prefix + a block scan, and
+//                   parses it from LDS (global memory past the overhang) with the
+//                   Java split/parseLong rules; malformed lines -> atomicMin(bad).
+#include <hipcub/hipcub.hpp>
+
+#include "gs_ingest.h"
+#include "gs_ingest.hpp"
+
+namespace gs {
+
+constexpr uint32_t kTile = 8192;   // bytes per parse block (32 per thread in the start scan)
+constexpr uint32_t kOver = 512;    // bytes of the next tile staged for lines crossing the end
+
+__device__ __forceinline__ bool is_sep(uint8_t c, int sep) {
+  // Java regex \s = [ \t\n\x0B\f\r]; \t = tab only
+  return sep == GS_SEP_TAB ? c == '\t' : (c == ' ' || (c >= '\t' && c <= '\r'));
+}
+
+__global__ __launch_bounds__(256) void k_count_lines(const uint8_t* __restrict__ text, uint64_t len,
+                                                     uint64_t* __restrict__ tile_cnt, bool aligned) {
+  __shared__ uint32_t wsum[4];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t h = 0; h < kTile / 4096; ++h) {  // 16 B per thread per 4 KiB slice: coalesced
+    const uint64_t p = t0 + h * 4096u + threadIdx.x * 16u;
+    if (aligned && p + 16 <= len) {
+      const uint4 v = *reinterpret_cast<const uint4*>(text + p);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) c += ((w[k] >> (8 * b)) & 0xFFu) == '\n';
+    } else {
+      for (uint64_t q = p; q < p + 16 && q < len; ++q) c += text[q] == '\n';
+    }
+  }
+  // block sum
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = (uint64_t)wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+constexpr uint32_t kLds0 = 16;  // LDS offset of byte t0 (byte t0 - 1 sits at kLds0 - 1)
+
+struct LineBuf {
+  const uint8_t* lds;
+  const uint8_t* text;
+  uint64_t t0, len, staged_end;  // bytes [t0, staged_end) are staged in LDS
+  // byte q, or '\n' past the end of the text (the last line needs no terminator)
+  __device__ __forceinline__ uint8_t at(uint64_t q) const {
+    if (q < staged_end) return lds[kLds0 + (q - t0)];
+    return q < len ? text[q] : (uint8_t)'\n';
+  }
+};
+
+enum { kFieldBad = 0, kFieldSep = 1, kFieldEol = 2 };
+
+// Long.parseLong on the field starting at q: optional sign, >= 1 ASCII digit, int64
+// range; the field must end at a separator or at the end of the line ('\n', end of
+// text, or a '\r' right before either: Flink drops it). One byte read per step.
+__device__ __forceinline__ int parse_long(const LineBuf& b, uint64_t& q, int sep, int64_t& out) {
+  uint8_t c = b.at(q);
+  const bool neg = c == '-';
+  if (neg || c == '+') c = b.at(++q);
+  // magnitude m <= 2^63 (negative) or 2^63 - 1: below kCut every next digit fits
+  // without a check; at kCut only a last digit <= 8 / 7 fits (Long.parseLong range)
+  constexpr uint64_t kCut = 922337203685477580ull;  // (2^63 - 1) / 10
+  const uint32_t last_ok = neg ? 8u : 7u;
+  uint64_t m = 0;
+  int digits = 0;
+  uint32_t d = (uint32_t)c - '0';
+  while (d <= 9u) {
+    if (m >= kCut && (m > kCut || d > last_ok)) return kFieldBad;
+    m = (m << 3) + (m << 1) + d;
+    ++digits;
+    c = b.at(++q);
+    d = (uint32_t)c - '0';
+  }
+  if (digits == 0) return kFieldBad;
+  out = neg ? (int64_t)(0ull - m) : (int64_t)m;
+  if (c == '\n') return kFieldEol;
+  if (c == '\r' && b.at(q + 1) == '\n') return kFieldEol;
+  return is_sep(c, sep) ? kFieldSep : kFieldBad;  // e.g. "12a"
+}
+
+__global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text, uint64_t len, int sep,
+                                               const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
+                                               int64_t* __restrict__ dst, uint64_t cap,
+                                               unsigned long long* __restrict__ bad, bool aligned) {
+  constexpr uint32_t kSeg = kTile / 256;  // bytes per thread in the line-start scan
+  __shared__ __align__(16) uint8_t lds[kLds0 + kTile + kOver];
+  __shared__ uint16_t starts[kTile];
+  __shared__ uint32_t wsum[4];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  const uint64_t staged_end = min(len, t0 + kTile + kOver);
+  // stage [t0, staged_end) at lds[kLds0..] with 16-B stores; lds[kLds0 - 1] = byte t0 - 1.
+  // Every thread's global loads are issued before any is waited for.
+  if (threadIdx.x == 0) lds[kLds0 - 1] = t0 == 0 ? (uint8_t)'\n' : text[t0 - 1];
+  constexpr uint32_t kStage = (kTile + kOver + 4095) / 4096;
+  uint4 v[kStage];
+  bool full[kStage];
+#pragma unroll
+  for (uint32_t r = 0; r < kStage; ++r) {
+    const uint64_t i = r * 4096u + threadIdx.x * 16u;
+    full[r] = aligned && i < kTile + kOver && t0 + i + 16 <= staged_end;
+    if (full[r]) v[r] = *reinterpret_cast<const uint4*>(text + t0 + i);
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < kStage; ++r) {
+    const uint64_t i = r * 4096u + threadIdx.x * 16u;
+    if (full[r]) {
+      *reinterpret_cast<uint4*>(lds + kLds0 + i) = v[r];
+    } else if (i < kTile + kOver) {
+      for (uint64_t q = t0 + i; q < t0 + i + 16 && q < staged_end; ++q) lds[kLds0 + (q - t0)] = text[q];
+    }
+  }
+  __syncthreads();
+  // (1) line starts of the tile (byte p - 1 is '\n', or p == 0), compacted into LDS
+  //     in order with a block scan, so that lane i then parses line i in lockstep.
+  //     Each thread tests its 32-byte segment in registers (two ds_read_b128).
+  static_assert(kSeg == 32, "one 32-bit mask per thread");
+  const uint32_t seg = threadIdx.x * kSeg;
+  const uint64_t tile_end = min(len, t0 + kTile);
+  const uint4 w0 = *reinterpret_cast<const uint4*>(lds + kLds0 + seg);
+  const uint4 w1 = *reinterpret_cast<const uint4*>(lds + kLds0 + seg + 16);
+  const uint32_t ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+  uint32_t nl = 0;  // bit j: byte seg + j is '\n'
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) nl |= (((ww[k] >> (8 * bb)) & 0xFFu) == '\n' ? 1u : 0u) << (4 * k + bb);
+  uint32_t mine = (nl << 1) | (lds[kLds0 - 1 + seg] == '\n' ? 1u : 0u);  // bit j: a line starts at seg + j
+  const uint64_t valid = t0 + seg >= tile_end ? 0 : min<uint64_t>(kSeg, tile_end - (t0 + seg));
+  if (valid < 32) mine &= (1u << valid) - 1u;
+  const uint32_t c = __popc(mine);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  uint32_t wbase = 0, total = 0;
+  for (int q = 0; q < 4; ++q) {
+    if (q < wid) wbase += wsum[q];
+    total += wsum[q];
+  }
+  uint32_t k = wbase + (x - c);
+  while (mine) {
+    const uint32_t j = __ffs(mine) - 1;
+    mine &= mine - 1;
+    starts[k++] = (uint16_t)(seg + j);
+  }
+  __syncthreads();
+  // (2) the k-th start follows k '\n' of the tile if a line starts at t0, else k + 1
+  const uint64_t line0 = tile_pre[blockIdx.x] + (lds[kLds0 - 1] == '\n' ? 0u : 1u);
+  const LineBuf b{lds, text, t0, len, staged_end};
+  for (uint32_t i = threadIdx.x; i < total; i += 256u) {
+    const uint64_t line = line0 + i;
+    uint64_t q = t0 + starts[i];
+    int64_t a = 0, d = 0;
+    // two fields: the first must end at a separator (else fields[1] does not exist)
+    bool ok = parse_long(b, q, sep, a) == kFieldSep;
+    if (ok) {
+      ++q;
+      ok = parse_long(b, q, sep, d) != kFieldBad;
+    }
+    if (!ok) {
+      atomicMin(bad, (unsigned long long)line);
+    } else if (line < cap) {
+      src[line] = a;
+      dst[line] = d;
+    }
+  }
+}
+
+// {line count, first malformed line (~0: none)} of a parsed text
+__global__ void k_parse_result(const uint64_t* tile_pre, const uint64_t* tile_cnt, uint64_t tiles,
+                               const uint8_t* text, uint64_t len, const unsigned long long* bad, uint64_t* res) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  res[0] = tile_pre[tiles - 1] + tile_cnt[tiles - 1] + (text[len - 1] != '\n' ? 1u : 0u);  // a last line may lack '\n'
+  res[1] = *bad;
+}
+
+int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, int64_t* src, int64_t* dst, size_t cap,
+                       ParseScratch& s) {
+  if (len == 0) return hipMemsetAsync(s.res, 0xFF, 16, st) == hipSuccess &&
+                        hipMemsetAsync(s.res, 0, 8, st) == hipSuccess ? 0 : -1;
+  const uint64_t tiles = (len + kTile - 1) / kTile;
+  if (tiles > s.tiles_cap) return -1;
+  const bool aligned = ((uintptr_t)text & 15u) == 0;
+  const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
+  hipLaunchKernelGGL(k_count_lines, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, s.tile_cnt, aligned);
+  size_t tmp = s.cub_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(s.cub_tmp, tmp, s.tile_cnt, s.tile_pre, (int)tiles, st) != hipSuccess)
+    return -1;
+  if (hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_parse, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, s.tile_pre, src, dst,
+                     (uint64_t)cap, s.bad, aligned);
+  hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
+                     s.bad, s.res);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int parse_text(hipStream_t st, const char* text, size_t len, int sep, int64_t* src, int64_t* dst, size_t cap,
+               ParseScratch& s, uint64_t* n_lines, int64_t* bad_line) {
+  *n_lines = 0;
+  *bad_line = -1;
+  if (parse_text_enqueue(st, text, len, sep, src, dst, cap, s)) return -1;
+  uint64_t res[2];
+  if (hipMemcpyAsync(res, s.res, 16, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
+  if (hipStreamSynchronize(st) != hipSuccess) return -1;
+  *n_lines = res[0];
+  *bad_line = res[1] == ~0ull ? -1 : (int64_t)res[1];
+  return 0;
+}
+
+size_t parse_scratch_bytes(size_t max_len, size_t* cub_bytes) {
+  const uint64_t tiles = (max_len + kTile - 1) / kTile + 1;
+  size_t tmp = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (uint64_t*)nullptr, (uint64_t*)nullptr, (int)tiles);
+  *cub_bytes = tmp;
+  return tiles * 16 + 48 + tmp + 256;
+}
+
+int parse_scratch_init(ParseScratch& s, void* mem, size_t max_len) {
+  size_t cub = 0;
+  parse_scratch_bytes(max_len, &cub);
+  const uint64_t tiles = (max_len + kTile - 1) / kTile + 1;
+  uint8_t* p = static_cast<uint8_t*>(mem);
+  s.tile_cnt = reinterpret_cast<uint64_t*>(p);
+  s.tile_pre = s.tile_cnt + tiles;
+  s.bad = reinterpret_cast<unsigned long long*>(s.tile_pre + tiles);
+  s.res = reinterpret_cast<uint64_t*>(s.bad + 2);
+  s.cub_tmp = reinterpret_cast<void*>(((uintptr_t)(s.res + 4) + 255) & ~(uintptr_t)255);
+  s.cub_bytes = cub;
+  s.tiles_cap = tiles;
+  return 0;
+}
+
+}  // namespace gs
+
+extern "C" int gs_parse_edges_device(void* stream, const char* text, size_t len, int sep, int64_t* src, int64_t* dst,
+                                     size_t cap, uint64_t* n_lines, int64_t* bad_line) {
+  if (!n_lines || !bad_line || (len && !text)) return GS_ERR_INVALID;
+  if (sep != GS_SEP_WHITESPACE && sep != GS_SEP_TAB) return GS_ERR_INVALID;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  size_t cub = 0;
+  const size_t bytes = gs::parse_scratch_bytes(len, &cub);
+  void* mem = nullptr;
+  if (hipMallocAsync(&mem, bytes, st) != hipSuccess) return GS_ERR_HIP;
+  gs::ParseScratch s;
+  gs::parse_scratch_init(s, mem, len);
+  const int rc = gs::parse_text(st, text, len, sep, src, dst, cap, s, n_lines, bad_line);
+  (void)hipFreeAsync(mem, st);
+  (void)hipStreamSynchronize(st);
+  if (rc) return GS_ERR_HIP;
+  if (*bad_line >= 0) return GS_ERR_PARSE;
+  if (*n_lines > cap) return GS_ERR_TRUNCATED;
+  return GS_OK;
+}

@@ -54,6 +54,10 @@ def lib():
         L.or_cpu_window_latency_cc.argtypes = [_i64p, _i64p, _sz, _sz,
                                                np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")]
         L.or_cpu_window_latency_cc.restype = None
+        L.or_format_edges.argtypes = [_i64p, _i64p, _sz, ctypes.c_int, _u8p, _sz]
+        L.or_format_edges.restype = _sz
+        L.or_parse_edges.argtypes = [ctypes.c_char_p, _sz, ctypes.c_int, _i64p, _i64p, _sz,
+                                     ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64)]
         L.or_cpu_baseline_bip.argtypes = [_i64p, _i64p, _sz]
         L.or_cpu_baseline_bip.restype = ctypes.c_double
         _lib = L
@@ -158,6 +162,27 @@ def cpu_baseline_cc(src, dst, window, threads=1):
     if threads <= 1:
         return lib().or_cpu_baseline_cc(src, dst, len(src), window)
     return lib().or_cpu_baseline_cc_threads(src, dst, len(src), window, threads)
+
+
+def format_edges(src, dst, sep=0):
+    """Edge-list text ("src<sep>dst\\n" per edge) as a numpy uint8 array (test/bench input)."""
+    src, dst = _arr(src), _arr(dst)
+    out = np.empty(42 * len(src) + 1, np.uint8)
+    n = lib().or_format_edges(src, dst, len(src), sep, out, len(out))
+    return out[:n]
+
+
+def parse_edges(text, sep=0):
+    """Reference source-map semantics (split + Long.parseLong per readTextFile line):
+    (src, dst, n_lines, bad_line); bad_line = first malformed line or -1."""
+    text = bytes(text)
+    cap = text.count(b"\n") + 1
+    src = np.zeros(cap, np.int64)
+    dst = np.zeros(cap, np.int64)
+    n = ctypes.c_uint64(0)
+    bad = ctypes.c_int64(-1)
+    lib().or_parse_edges(text, len(text), sep, src, dst, cap, ctypes.byref(n), ctypes.byref(bad))
+    return src[:n.value], dst[:n.value], int(n.value), int(bad.value)
 
 
 def cpu_window_latency_cc(src, dst, window):

@@ -664,6 +664,96 @@ void or_cpu_window_latency_cc(const int64_t* src, const int64_t* dst, size_t n, 
   }
 }
 
+// ---------------- text edge ingest (include/gs_ingest.h) ----------------
+// Restatement of the reference's source map, per line of env.readTextFile:
+//   String[] fields = s.split("\\s" or "\\t"); Long.parseLong(fields[0]); Long.parseLong(fields[1])
+// (ConnectedComponentsExample.java:109-118, BipartitenessCheckExample.java:97-106), with
+// Java 8 String.split semantics (a leading empty field is kept, trailing empty fields are
+// removed, no match -> the whole line) and Long.parseLong semantics (optional sign,
+// >= 1 digit, int64 range), and Flink TextInputFormat line handling ('\n' delimiter, a
+// trailing '\r' dropped, no record after a final '\n').
+static bool java_is_sep(char c, int sep) {
+  if (sep == 1) return c == '\t';
+  return c == ' ' || c == '\t' || c == '\n' || c == '\x0B' || c == '\f' || c == '\r';
+}
+static std::vector<std::string> java_split(const std::string& s, int sep) {
+  std::vector<std::string> out;
+  size_t start = 0;
+  bool matched = false;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (java_is_sep(s[i], sep)) {
+      out.push_back(s.substr(start, i - start));
+      start = i + 1;
+      matched = true;
+    }
+  }
+  if (!matched) return {s};
+  out.push_back(s.substr(start));
+  while (!out.empty() && out.back().empty()) out.pop_back();  // limit 0: trailing empties removed
+  return out;
+}
+static bool java_parse_long(const std::string& f, int64_t* v) {
+  if (f.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (f[0] == '-' || f[0] == '+') {
+    neg = f[0] == '-';
+    if (f.size() == 1) return false;
+    i = 1;
+  }
+  // magnitude in unsigned arithmetic, range-checked against 2^63 (neg) / 2^63 - 1
+  const unsigned long long lim = neg ? (1ull << 63) : (1ull << 63) - 1;
+  unsigned long long m = 0;
+  for (; i < f.size(); ++i) {
+    if (f[i] < '0' || f[i] > '9') return false;
+    const unsigned d = (unsigned)(f[i] - '0');
+    if (m > (lim - d) / 10) return false;
+    m = m * 10 + d;
+  }
+  *v = neg ? (int64_t)(0ull - m) : (int64_t)m;
+  return true;
+}
+
+// Test/bench input generator: "src<sep>dst\n" lines (sep 0 = ' ', 1 = '\t'); returns bytes
+// written (0 if cap is too small).
+size_t or_format_edges(const int64_t* src, const int64_t* dst, size_t n, int sep, char* out, size_t cap) {
+  size_t w = 0;
+  char tmp[48];
+  for (size_t i = 0; i < n; ++i) {
+    int k = snprintf(tmp, sizeof tmp, "%lld%c%lld\n", (long long)src[i], sep == 1 ? '\t' : ' ', (long long)dst[i]);
+    if (w + (size_t)k > cap) return 0;
+    memcpy(out + w, tmp, (size_t)k);
+    w += (size_t)k;
+  }
+  return w;
+}
+
+int or_parse_edges(const char* text, size_t len, int sep, int64_t* src, int64_t* dst, size_t cap, uint64_t* n_lines,
+                   int64_t* bad_line) {
+  *n_lines = 0;
+  *bad_line = -1;
+  size_t pos = 0;
+  uint64_t line = 0;
+  while (pos < len) {
+    size_t e = pos;
+    while (e < len && text[e] != '\n') ++e;
+    std::string s(text + pos, e - pos);
+    if (!s.empty() && s.back() == '\r') s.pop_back();
+    std::vector<std::string> f = java_split(s, sep);
+    int64_t a = 0, b = 0;
+    const bool ok = f.size() >= 2 && java_parse_long(f[0], &a) && java_parse_long(f[1], &b);
+    if (!ok && *bad_line < 0) *bad_line = (int64_t)line;
+    if (ok && line < cap) {
+      src[line] = a;
+      dst[line] = b;
+    }
+    ++line;
+    pos = e + 1;  // past the '\n' (a final '\n' yields no further record)
+  }
+  *n_lines = line;
+  return *bad_line >= 0 ? -5 : 0;
+}
+
 // Quirk-exact Candidates fold of a prefix, one window, p = 1; returns wall seconds.
 double or_cpu_baseline_bip(const int64_t* src, const int64_t* dst, size_t n) {
   auto t0 = std::chrono::steady_clock::now();

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared_symbols():
     names = set()
-    for h in ("gs_summary.h", "gs_gen.h", "gs_group.h"):
+    for h in ("gs_summary.h", "gs_gen.h", "gs_group.h", "gs_ingest.h"):
         with open(os.path.join(ROOT, "include", h)) as f:
             text = f.read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)

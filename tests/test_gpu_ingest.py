@@ -1,0 +1,106 @@
+"""GPU parity of the text edge ingest (include/gs_ingest.h) against the oracle's
+restatement of the reference's source map (split + Long.parseLong per line,
+ConnectedComponentsExample.java:109-118, BipartitenessCheckExample.java:97-106)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+I64_MIN = -(1 << 63)
+I64_MAX = (1 << 63) - 1
+
+
+def _random_text(rng, nlines, sep):
+    s = b"\t" if sep == 1 else b" "
+    seps = [b" ", b"\t", b"\x0b", b"\x0c"] if sep == 0 else [b"\t"]
+    good_vals = [0, 1, -1, 7, I64_MAX, I64_MIN, 123456789012345678]
+    lines = []
+    for i in range(nlines):
+        r = rng.random()
+        a = int(rng.choice(good_vals)) if rng.random() < 0.2 else int(rng.integers(-(10 ** 12), 10 ** 12))
+        b = int(rng.integers(-(10 ** 18), 10 ** 18))
+        sp = seps[int(rng.integers(len(seps)))]
+        if r < 0.80:
+            ln = b"%d%s%d" % (a, sp, b)
+        elif r < 0.85:
+            ln = b"+%d%s%d" % (abs(a), sp, b)
+        elif r < 0.88:
+            ln = b"%d%s%d%s%s" % (a, sp, b, s, b"x" * int(rng.integers(1, 700)))  # long ignored 3rd field
+        elif r < 0.91:
+            ln = b"%d%s%d\r" % (a, sp, b)
+        elif r < 0.93:
+            ln = b"%d%s%d%s" % (a, sp, b, sp)  # trailing separator
+        else:  # malformed variants
+            bad = [b"", b"%d" % a, s + b"%d%s%d" % (a, s, b), b"%d%s%s%d" % (a, s, s, b), b"%da%s%d" % (a, s, b),
+                   b"9223372036854775808%s1" % s, b"-%s5" % s, b"1%s-9223372036854775809" % s]
+            ln = bad[int(rng.integers(len(bad)))]
+        lines.append(ln)
+    text = b"\n".join(lines)
+    if rng.random() < 0.5:
+        text += b"\n"
+    return text
+
+
+def _gpu_parse(gs, text, sep, offset=0):
+    import torch
+    buf = torch.zeros(len(text) + offset, dtype=torch.uint8, device="cuda")
+    if text:
+        buf[offset:] = torch.frombuffer(bytearray(text), dtype=torch.uint8).cuda()
+    view = buf[offset:]
+    cap = text.count(b"\n") + 1
+    src = torch.zeros(cap, dtype=torch.int64, device="cuda")
+    dst = torch.zeros(cap, dtype=torch.int64, device="cuda")
+    n, bad = gs.parse_edges_device(view, src, dst, sep)
+    torch.cuda.synchronize()
+    return src.cpu().numpy()[:n], dst.cpu().numpy()[:n], n, bad
+
+
+@pytest.mark.parametrize("sep", [0, 1])
+@pytest.mark.parametrize("seed,nlines,offset", [(1, 50, 0), (2, 20000, 0), (3, 150000, 0), (4, 30000, 1),
+                                                (5, 30000, 7)])
+def test_parse_matches_oracle(gs, oracle_mod, sep, seed, nlines, offset):
+    rng = np.random.default_rng(seed)
+    text = _random_text(rng, nlines, sep)
+    es, ed, en, eb = oracle_mod.parse_edges(text, sep)
+    s, d, n, b = _gpu_parse(gs, text, sep, offset)
+    assert (n, b) == (en, eb)
+    assert np.array_equal(s, es) and np.array_equal(d, ed)
+
+
+@pytest.mark.parametrize("text", [b"", b"\n", b"1 2", b"1 2\n", b"1 2\n\n", b"\n1 2", b"1 2\r", b"1 2\r\n3 4\r\n",
+                                  b"-9223372036854775808 9223372036854775807\n"])
+def test_parse_edge_cases(gs, oracle_mod, text):
+    for sep in (0, 1):
+        es, ed, en, eb = oracle_mod.parse_edges(text, sep)
+        s, d, n, b = _gpu_parse(gs, text, sep)
+        assert (n, b) == (en, eb), (text, sep)
+        assert np.array_equal(s, es) and np.array_equal(d, ed)
+
+
+def test_fold_text_rmat_chunks_and_malformed(gs, oracle_mod):
+    # > 16 MiB of text: several ingest chunks, each cut at a line boundary
+    s, d = oracle_mod.rmat_edges(0x5EED0016, 16, 0, 1 << 20, True)
+    text = b"\n".join(b"%d %d" % (a, b) for a, b in zip(s.tolist(), d.tolist())) + b"\n"
+    assert len(text) > (16 << 20)
+    with gs.Summary("cc", capacity_hint=1 << 16) as ds:
+        assert ds.fold_text(text) == len(s)
+        v, lab = ds.labels()
+        ov, olab = oracle_mod.cc_labels(s, d)
+        assert np.array_equal(v, ov) and np.array_equal(lab, olab)
+    # a malformed line deep in the stream: GS_ERR_PARSE naming its line index
+    lines = text.split(b"\n")
+    k = 700001
+    lines[k] = b"12 x"
+    bad_text = b"\n".join(lines)
+    with gs.Summary("cc", capacity_hint=1 << 16) as ds:
+        with pytest.raises(gs.GSError) as e:
+            ds.fold_text(bad_text)
+        assert e.value.code == gs.GS_ERR_PARSE and str(k) in str(e.value)
+    # tab-separated (BipartitenessCheckExample format) into a signed summary
+    b0, b1 = oracle_mod.bip_edges(0x5EED0B1B, 12, 0, 1 << 14, [])
+    tsv = b"\n".join(b"%d\t%d" % (a, b) for a, b in zip(b0.tolist(), b1.tolist()))
+    with gs.Summary("signed", capacity_hint=1 << 13) as c, gs.Summary("signed", capacity_hint=1 << 13) as ref:
+        assert c.fold_text(tsv, gs.SEP_TAB) == len(b0)
+        ref.fold(b0, b1)
+        ca, cb = c.colouring(), ref.colouring()
+        assert ca[0] == cb[0] and all(np.array_equal(x, y) for x, y in zip(ca[1:], cb[1:]))

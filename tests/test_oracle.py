@@ -179,3 +179,56 @@ def test_cpu_baseline_runs(oracle_mod):
     assert oracle_mod.cpu_baseline_cc(s, d, 1 << 12) > 0
     assert oracle_mod.cpu_baseline_cc(s, d, 1 << 12, threads=2) > 0
     assert oracle_mod.cpu_baseline_bip(s[:256], d[:256]) > 0
+
+
+# ------------------------------------------------------------- text ingest semantics
+# Expected values follow the Java 8 / Flink 1.8 behaviour of the reference's source map
+# (ConnectedComponentsExample.java:109-118: split("\\s"); BipartitenessCheckExample.java:97-106:
+# split("\\t"); Long.parseLong on fields 0 and 1; readTextFile lines). No fixture in the
+# reference exercises it (parity pinned to the Java specification, not to reference data).
+PARSE_CASES = [
+    # text, sep, n_lines, bad_line, src, dst   (src/dst of the well-formed lines, in order)
+    (b"1 2\n3 4", 0, 2, -1, [1, 3], [2, 4]),
+    (b"1 2\n3 4\n", 0, 2, -1, [1, 3], [2, 4]),                 # no record after the final newline
+    (b"1\t2\r\n-5 +6 extra\n", 0, 2, -1, [1, -5], [2, 6]),     # CRLF, signs, ignored 3rd field
+    (b"1\t2\r\n", 1, 1, -1, [1], [2]),                         # tab mode: trailing CR dropped by Flink
+    (b"1 2\n", 1, 1, 0, [], []),                                 # tab mode: one field
+    (b" 1 2\n", 0, 1, 0, [], []),                                # leading separator: fields[0] == ""
+    (b"1  2\n", 0, 1, 0, [], []),                                # doubled separator: fields[1] == ""
+    (b"1 2 \n", 0, 1, -1, [1], [2]),                             # trailing empty fields removed
+    (b"1\x0b2\n3\x0c4\n", 0, 2, -1, [1, 3], [2, 4]),              # \s includes VT and FF
+    (b"9223372036854775807 -9223372036854775808\n", 0, 1, -1, [9223372036854775807], [-9223372036854775808]),
+    (b"9223372036854775808 1\n", 0, 1, 0, [], []),               # overflow
+    (b"12a 3\n", 0, 1, 0, [], []),
+    (b"- 3\n", 0, 1, 0, [], []),
+    (b"+ 3\n", 0, 1, 0, [], []),
+    (b"1\n", 0, 1, 0, [], []),                                   # one field
+    (b"", 0, 0, -1, [], []),
+    (b"\n", 0, 1, 0, [], []),                                    # an empty line is a record -> throws
+    (b"1 2\n\n3 4\n", 0, 3, 1, [1, 3], [2, 4]),
+]
+
+
+@pytest.mark.parametrize("case", PARSE_CASES, ids=[repr(c[0])[:30] for c in PARSE_CASES])
+def test_parse_edges_java_semantics(oracle_mod, case):
+    text, sep, n, bad, es, ed = case
+    s, d, nl, b = oracle_mod.parse_edges(text, sep)
+    assert (nl, b) == (n, bad)
+    good = [i for i in range(nl) if not _malformed(text, sep, i)]
+    assert s[good].tolist() == es and d[good].tolist() == ed
+
+
+def _malformed(text, sep, i):
+    line = text.split(b"\n")[i]
+    if line.endswith(b"\r"):
+        line = line[:-1]
+    import re
+    parts = re.split(rb"[ \t\n\x0b\x0c\r]" if sep == 0 else rb"\t", line)
+    while len(parts) > 1 and parts[-1] == b"":
+        parts.pop()
+    if len(parts) < 2:
+        return True
+    for f in parts[:2]:
+        if not re.fullmatch(rb"[+-]?[0-9]+", f) or not (-(1 << 63) <= int(f) < (1 << 63)):
+            return True
+    return False
