@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "gs_gen_rmat", "gs_gen_er", "gs_gen_bip",
     "gs_parse_edges_device", "gs_fold_text",
     "gs_group_unique_id", "gs_group_create", "gs_group_fold_device", "gs_group_finish", "gs_group_stats",
-    "gs_group_destroy",
+    "gs_group_destroy", "gs_group_tree_combine", "gs_combine_exported_device",
 )
 
 
@@ -120,6 +120,8 @@ def lib():
     L.gs_group_finish.argtypes = [_vp]
     L.gs_group_stats.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_u64)]
     L.gs_group_destroy.argtypes = [_vp]
+    L.gs_group_tree_combine.argtypes = [_vp]
+    L.gs_combine_exported_device.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.c_int]
     _lib = L
     return L
 
@@ -221,6 +223,12 @@ class Summary:
         _check(lib().gs_export_labels(self._h, v.ctypes.data, lab.ctypes.data, n, ctypes.byref(got)))
         o = np.argsort(v[: got.value], kind="stable")
         return v[: got.value][o], lab[: got.value][o]
+
+    def combine_exported_device(self, v, label, parity, n, failed=False):
+        """Fold another summary's exported (v, label, parity) DEVICE arrays into this
+        one and AND the verdict with `not failed` (gs_combine_exported_device)."""
+        _check(lib().gs_combine_exported_device(self._h, _ptr(v), _ptr(label), _ptr(parity), int(n),
+                                                int(bool(failed))))
 
     def export_labels_device(self, v, label, parity=None):
         got = _sz()
@@ -356,6 +364,11 @@ class Group:
 
     def finish(self):
         _check(lib().gs_group_finish(self._g))
+
+    def tree_combine(self):
+        """Binomial-tree combine of per-rank partial summaries onto rank 0
+        (gs_group_tree_combine; SummaryTreeReduce). Collective, synchronous."""
+        _check(lib().gs_group_tree_combine(self._g))
 
     def stats(self):
         e, s, c = _u64(), _u64(), _u64()

@@ -794,6 +794,20 @@ int gs_combine(gs_handle dst, gs_handle src) {
   return rc;
 }
 
+int gs_combine_exported_device(gs_handle h, const int64_t* v, const int64_t* label, const uint8_t* parity, size_t n,
+                               int failed) {
+  if (int rc = check(h)) return rc;
+  if (n && (!v || !label)) return fail(GS_ERR_INVALID, "null arrays");
+  if (n && h->kind == GS_KIND_SIGNED && !parity) return fail(GS_ERR_INVALID, "a signed summary needs parity");
+  DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
+  if (failed) {  // the verdict is the AND (BipartitenessCheck.combineFunction -> Candidates.merge :79-81)
+    GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, h->stream));
+    return GS_OK;
+  }
+  return fold_device_impl(h, v, label, parity, n, 1, 1, h->track);
+}
+
 // Serialized image: u32 magic 'GSS1', u32 kind, u32 ok, u32 0, u64 n, int64 v[n], int64 label[n], u8 parity[n]
 int gs_serialize(gs_handle h, void* buf, size_t cap, size_t* len) {
   if (int rc = check(h)) return rc;
@@ -1121,6 +1135,10 @@ struct RcclApi {
   int (*getUniqueId)(void*) = nullptr;
   int (*allGather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
   int (*commDestroy)(void*) = nullptr;
+  int (*send)(const void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  int (*recv)(void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  int (*groupStart)() = nullptr;
+  int (*groupEnd)() = nullptr;
   const char* (*getErrorString)(int) = nullptr;
   void* initRankSym = nullptr;  // ncclCommInitRank takes ncclUniqueId (128 B) by value: see Id128
 };
@@ -1141,6 +1159,10 @@ int rccl_load() {
   g_rccl.allGather = (int (*)(const void*, void*, size_t, int, void*, hipStream_t))dlsym(l, "ncclAllGather");
   g_rccl.commDestroy = (int (*)(void*))dlsym(l, "ncclCommDestroy");
   g_rccl.getErrorString = (const char* (*)(int))dlsym(l, "ncclGetErrorString");
+  g_rccl.send = (int (*)(const void*, size_t, int, int, void*, hipStream_t))dlsym(l, "ncclSend");
+  g_rccl.recv = (int (*)(void*, size_t, int, int, void*, hipStream_t))dlsym(l, "ncclRecv");
+  g_rccl.groupStart = (int (*)())dlsym(l, "ncclGroupStart");
+  g_rccl.groupEnd = (int (*)())dlsym(l, "ncclGroupEnd");
   if (!g_rccl.getUniqueId || !g_rccl.initRankSym || !g_rccl.allGather || !g_rccl.commDestroy)
     return fail(GS_ERR_HIP, "RCCL is missing ncclGetUniqueId/ncclCommInitRank/ncclAllGather/ncclCommDestroy");
   g_rccl.lib = l;
@@ -1152,6 +1174,7 @@ int rccl_fail(const char* what, int r) {
 }
 
 constexpr int kNcclInt64 = 4;  // ncclInt64 (rccl.h)
+constexpr int kNcclUint8 = 1;  // ncclUint8 (rccl.h)
 constexpr uint64_t kHdrLag = 4;  // a retune reads the headers of the exchange kHdrLag batches back
 
 }  // namespace
@@ -1216,10 +1239,12 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   if (!out || !id) return fail(GS_ERR_INVALID, "null argument");
   *out = nullptr;
   if (int rc = check(h)) return rc;
-  if (nranks < 1 || rank < 0 || rank >= nranks || batch_edges == 0) return fail(GS_ERR_INVALID, "bad group shape");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(GS_ERR_INVALID, "bad group shape");
   if (int rc = rccl_load()) return rc;
   DeviceGuard dg(h->device);
-  if (int rc = gs_set_delta_tracking(h, 1)) return rc;
+  const bool exchange = batch_edges != 0;  // 0: tree-combine-only group
+  if (exchange)
+    if (int rc = gs_set_delta_tracking(h, 1)) return rc;
   gs_group* g = new gs_group();
   g->h = h;
   g->nranks = nranks;
@@ -1233,9 +1258,9 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
     return code;
   };
   const size_t rows = g->max_cap + 1;
-  if (hipMalloc(&g->send, rows * 24) != hipSuccess || hipMalloc(&g->recv, (size_t)nranks * rows * 24) != hipSuccess ||
+  if (exchange && (hipMalloc(&g->send, rows * 24) != hipSuccess || hipMalloc(&g->recv, (size_t)nranks * rows * 24) != hipSuccess ||
       hipHostMalloc(&g->hdr_host, (size_t)nranks * 24, hipHostMallocDefault) != hipSuccess ||
-      hipEventCreateWithFlags(&g->hdr_ev, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&g->hdr_ev, hipEventDisableTiming) != hipSuccess))
     return bail(fail(GS_ERR_HIP, "group buffer allocation failed"));
   Id128 uid;
   memcpy(uid.b, id, GS_GROUP_ID_BYTES);
@@ -1250,6 +1275,7 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   if (!g) return fail(GS_ERR_INVALID, "null group");
   gs_summary* h = g->h;
   DeviceGuard dg(h->device);
+  if (!g->send) return fail(GS_ERR_INVALID, "tree-combine-only group (created with batch_edges 0)");
   if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
   if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, /*track=*/true)) return rc;
   const uint64_t b = g->b;
@@ -1285,6 +1311,109 @@ int gs_group_finish(gs_group_t g) {
   g->hdr_batch = -1;
   g->cap = g->first_cap;
   return GS_OK;
+}
+
+namespace {
+
+// device arrays of one exported summary (v, label, parity), freed on scope exit
+struct ExportedArrays {
+  int64_t* v = nullptr;
+  int64_t* l = nullptr;
+  uint8_t* p = nullptr;
+  int alloc(size_t n) {
+    if (!n) return GS_OK;
+    GS_HIP(hipMalloc(&v, n * 8));
+    GS_HIP(hipMalloc(&l, n * 8));
+    GS_HIP(hipMalloc(&p, n));
+    return GS_OK;
+  }
+  ~ExportedArrays() {
+    (void)hipFree(v);
+    (void)hipFree(l);
+    (void)hipFree(p);
+  }
+};
+
+// one tree edge, sending side: header {count, failed}, then the three arrays
+int tree_send(gs_group* g, int peer, int64_t* hdr) {
+  gs_summary* h = g->h;
+  uint64_t nv = 0;
+  if (int rc = read_nv(h, &nv)) return rc;
+  ExportedArrays a;
+  if (int rc = a.alloc(nv + 1)) return rc;
+  size_t got = 0;
+  if (int rc = export_device_impl(h, a.v, a.l, a.p, nv + 1, &got)) return rc;
+  uint32_t failed = 0;
+  GS_HIP(hipMemcpyAsync(&failed, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  const int64_t hv[2] = {(int64_t)got, (int64_t)((failed & 0xff) != 0)};
+  GS_HIP(hipMemcpyAsync(hdr, hv, 16, hipMemcpyHostToDevice, h->stream));
+  int r = g_rccl.send(hdr, 2, kNcclInt64, peer, g->comm, h->stream);
+  if (r) return rccl_fail("ncclSend", r);
+  if (got) {
+    g_rccl.groupStart();
+    r = g_rccl.send(a.v, got, kNcclInt64, peer, g->comm, h->stream);
+    if (!r) r = g_rccl.send(a.l, got, kNcclInt64, peer, g->comm, h->stream);
+    if (!r) r = g_rccl.send(a.p, got, kNcclUint8, peer, g->comm, h->stream);
+    const int e = g_rccl.groupEnd();
+    if (r || e) return rccl_fail("ncclSend", r ? r : e);
+  }
+  GS_HIP(hipStreamSynchronize(h->stream));  // the arrays are freed on return
+  return GS_OK;
+}
+
+// one tree edge, receiving side: fold the peer's exported summary into this one
+int tree_recv(gs_group* g, int peer, int64_t* hdr) {
+  gs_summary* h = g->h;
+  int r = g_rccl.recv(hdr, 2, kNcclInt64, peer, g->comm, h->stream);
+  if (r) return rccl_fail("ncclRecv", r);
+  int64_t hv[2] = {0, 0};
+  GS_HIP(hipMemcpyAsync(hv, hdr, 16, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  const size_t got = (size_t)hv[0];
+  ExportedArrays a;
+  if (int rc = a.alloc(got)) return rc;
+  if (got) {
+    g_rccl.groupStart();
+    r = g_rccl.recv(a.v, got, kNcclInt64, peer, g->comm, h->stream);
+    if (!r) r = g_rccl.recv(a.l, got, kNcclInt64, peer, g->comm, h->stream);
+    if (!r) r = g_rccl.recv(a.p, got, kNcclUint8, peer, g->comm, h->stream);
+    const int e = g_rccl.groupEnd();
+    if (r || e) return rccl_fail("ncclRecv", r ? r : e);
+  }
+  const bool track = h->track;
+  h->track = false;  // a bulk combine is not a structural delta of this rank's own fold
+  const int rc = gs_combine_exported_device(h, a.v, a.l, a.p, got, (int)hv[1]);
+  h->track = track;
+  if (rc) return rc;
+  GS_HIP(hipStreamSynchronize(h->stream));
+  return GS_OK;
+}
+
+}  // namespace
+
+int gs_group_tree_combine(gs_group_t g) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  if (!g_rccl.send || !g_rccl.recv || !g_rccl.groupStart || !g_rccl.groupEnd)
+    return fail(GS_ERR_HIP, "RCCL is missing ncclSend/ncclRecv/ncclGroupStart/ncclGroupEnd");
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  if (int rc = join_lanes(h)) return rc;
+  int64_t* hdr = nullptr;  // device {count, failed}
+  GS_HIP(hipMalloc(&hdr, 16));
+  int rc = GS_OK;
+  // binomial tree (SummaryTreeReduce.enhance pairs partitions by f0/2, :107): at level l
+  // rank r with r mod 2^(l+1) == 2^l sends to r - 2^l and leaves the tree
+  for (int step = 1; step < g->nranks && rc == GS_OK; step <<= 1) {
+    const int pos = g->rank % (2 * step);
+    if (pos == step) {
+      rc = tree_send(g, g->rank - step, hdr);
+      break;
+    }
+    if (pos == 0 && g->rank + step < g->nranks) rc = tree_recv(g, g->rank + step, hdr);
+  }
+  (void)hipFree(hdr);
+  return rc;
 }
 
 int gs_group_stats(gs_group_t g, uint64_t* exchanges, uint64_t* records_sent, uint64_t* current_cap) {

@@ -161,3 +161,65 @@ class DeltaExchangeFold:
         self.s.fold_exchange(recv, self.world, rows, self.rank)
         self.rows_received += (self.world - 1) * rows
         self.last_rows = rows
+
+
+def tree_combine(summary, group=None):
+    """Binomial-tree combine of PER-RANK PARTIAL summaries onto rank 0: the
+    reference's SummaryTreeReduce / ConnectedComponentsTree
+    (SummaryTreeReduce.java:68-123; `enhance` pairs partitions by f0/2 at :107 and
+    reduces level by level) over torch.distributed point-to-point. At level l, rank
+    r with r mod 2^(l+1) == 2^l sends its exported summary -- header
+    {count, failed}, then (v, label, parity) -- to r - 2^l, which folds it as
+    union(v, label) with the required parity (DisjointSet.merge, DisjointSet.java:127-131;
+    Candidates.merge for the signed kind, verdict ANDed: Candidates.java:79-81).
+    Same schedule as the native gs_group_tree_combine (include/gs_group.h).
+
+    `summary` provides num_vertices(), ok(), export_labels_device(v, label, parity)
+    -> count, combine_exported_device(v, label, parity, n, failed) and sync()
+    (gelly_streaming_amd.Summary does; CPU tests plug a model). With gloo the
+    payload is staged through host memory. Collective; returns True on the rank
+    that holds the combined summary (rank 0)."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    nccl = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
+    wire = dev
+
+    def peer(r):
+        return dist.get_global_rank(group, r) if group is not None else r
+
+    xdev = getattr(summary, "device", dev)
+    xdev = torch.device("cuda", xdev) if isinstance(xdev, int) else torch.device(xdev)
+
+    step = 1
+    while step < world:
+        pos = rank % (2 * step)
+        if pos == step:
+            n = summary.num_vertices()
+            cap = n + 1
+            v = torch.empty(cap, dtype=torch.int64, device=xdev)
+            lab = torch.empty(cap, dtype=torch.int64, device=xdev)
+            par = torch.empty(cap, dtype=torch.uint8, device=xdev)
+            got = summary.export_labels_device(v, lab, par)
+            hdr = torch.tensor([got, 0 if summary.ok() else 1], dtype=torch.int64, device=wire)
+            dist.send(hdr, peer(rank - step), group=group)
+            if got:
+                for t in (v[:got], lab[:got], par[:got]):
+                    dist.send(t.to(wire).contiguous(), peer(rank - step), group=group)
+            return False
+        if pos == 0 and rank + step < world:
+            src = peer(rank + step)
+            hdr = torch.empty(2, dtype=torch.int64, device=wire)
+            dist.recv(hdr, src, group=group)
+            got, failed = int(hdr[0]), bool(hdr[1])
+            bufs = [torch.empty(got, dtype=dt, device=wire) for dt in (torch.int64, torch.int64, torch.uint8)]
+            for t in bufs:
+                if got:
+                    dist.recv(t, src, group=group)
+            v, lab, par = (t.to(xdev) for t in bufs)
+            if xdev.type == "cuda":
+                torch.cuda.current_stream(xdev).synchronize()  # the summary's stream reads them next
+            summary.combine_exported_device(v, lab, par, got, failed)
+            summary.sync()
+        step <<= 1
+    return rank == 0

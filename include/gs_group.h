@@ -39,7 +39,9 @@ int gs_group_unique_id(void* id);
 /* Join the group as `rank` of `nranks` and bind it to summary `h` (its device and
  * stream). `batch_edges` = maximum edges one gs_group_fold_device call folds;
  * `first_cap` = records per rank in the first exchanges (0: batch_edges). Turns
- * delta tracking on. Collective: every rank must call it. */
+ * delta tracking on. batch_edges == 0 creates a tree-combine-only group (no
+ * exchange buffers, tracking untouched: fold partials with gs_fold[_device], then
+ * gs_group_tree_combine). Collective: every rank must call it. */
 int gs_group_create(gs_group_t* g, gs_handle h, const void* id, int nranks, int rank, size_t batch_edges,
                     size_t first_cap);
 
@@ -52,6 +54,19 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
 /* Drain every rank's queued records (synchronous rounds) and synchronise; then all
  * replicas are identical. Collective. */
 int gs_group_finish(gs_group_t g);
+
+/* Log-depth tree combine of PER-RANK PARTIAL summaries: the reference's
+ * SummaryTreeReduce / ConnectedComponentsTree (SummaryTreeReduce.java:68-123:
+ * `enhance` keys partition pairs by f0/2 and reduces them level by level until the
+ * parallelism is <= 2, then the all-window reduce and Merger at parallelism 1).
+ * Here a binomial tree over the group's ranks: at level l, rank r with
+ * r mod 2^(l+1) == 2^l sends its summary -- (v, label, parity) arrays + verdict,
+ * ncclSend on the summary's stream -- to r - 2^l, which folds it
+ * (gs_combine_exported_device). After ceil(log2 n) levels rank 0 holds the
+ * combination of every rank's partial; senders keep theirs unchanged. Collective
+ * (every rank calls it), synchronous. Unlike gs_group_fold_device (replicas kept
+ * equal by delta exchange) this is the bulk path: O(V) per level. */
+int gs_group_tree_combine(gs_group_t g);
 
 /* Exchange statistics: exchanges run, records this rank has sent, the current
  * per-rank capacity of one exchange (synchronises the stream). */

@@ -99,6 +99,15 @@ int gs_set_pipelining(gs_handle h, int depth);
  * (BipartitenessCheck.java:128-130, Candidates.java:77-139); the verdict is the AND. */
 int gs_combine(gs_handle dst, gs_handle src);
 
+/* Receiving half of a combine from EXPORTED arrays (gs_export_labels_device of
+ * another summary, e.g. received from another rank): folds union(v[i], label[i])
+ * with required parity parity[i] (NULL for GS_KIND_CC) -- DisjointSet.merge
+ * (DisjointSet.java:127-131: union(k, parent(k)) for every entry) -- and ANDs the
+ * verdict with !failed (BipartitenessCheck.java:128-130 -> Candidates.java:79-81).
+ * DEVICE arrays on h's device; queued on h's stream. */
+int gs_combine_exported_device(gs_handle h, const int64_t* v, const int64_t* label, const uint8_t* parity, size_t n,
+                               int failed);
+
 /* Block until all work queued on the handle has finished. */
 int gs_sync(gs_handle h);
 

@@ -28,3 +28,57 @@ def test_group_single_rank_matches_oracle(gs, oracle_mod, monkeypatch, first_cap
         g.close()
     ov, olab = oracle_mod.cc_labels(src.cpu().numpy(), dst.cpu().numpy())
     assert np.array_equal(v, ov) and np.array_equal(lab, olab)
+
+
+@pytest.mark.parametrize("kind", ["cc", "signed"])
+def test_combine_exported_device_equals_combine(gs, oracle_mod, kind):
+    """gs_combine_exported_device (the receiving half of the tree combine) folds
+    another summary's exported arrays: same result as gs_combine."""
+    import torch
+    n = 1 << 15
+    if kind == "cc":
+        s, d = oracle_mod.rmat_edges(0x5EED0026, 12, 0, n, True)
+    else:
+        s, d = oracle_mod.bip_edges(0x5EED0B1B, 11, 0, n)
+    h = n // 2
+    with gs.Summary(kind, capacity_hint=64) as a, gs.Summary(kind, capacity_hint=64) as b, \
+            gs.Summary(kind, capacity_hint=64) as c:
+        a.fold(s[:h], d[:h])
+        b.fold(s[h:], d[h:])
+        c.fold(s[h:], d[h:])
+        m = a.num_vertices() + 1
+        v = torch.empty(m, dtype=torch.int64, device="cuda")
+        lab = torch.empty(m, dtype=torch.int64, device="cuda")
+        par = torch.empty(m, dtype=torch.uint8, device="cuda")
+        got = a.export_labels_device(v, lab, par)
+        b.combine_exported_device(v, lab, par, got, failed=not a.ok())
+        c.combine(a)
+        if kind == "cc":
+            ov, olab = oracle_mod.cc_labels(s, d)
+            for x in (b, c):
+                xv, xl = x.labels()
+                assert np.array_equal(xv, ov) and np.array_equal(xl, olab)
+        else:
+            t = oracle_mod.bip_truth(s, d)
+            for x in (b, c):
+                ok, comp, xv, sign = x.colouring()
+                assert ok == t[0] and ok
+                assert np.array_equal(comp, t[1]) and np.array_equal(xv, t[2]) and np.array_equal(sign, t[3])
+        b.combine_exported_device(v, lab, par, 0, failed=True)
+        assert kind == "cc" or not b.ok()
+
+
+def test_tree_only_group_single_rank(gs, oracle_mod):
+    """batch_edges 0: a tree-combine-only group (no exchange buffers, tracking off);
+    at one rank the tree is empty and the summary is unchanged."""
+    s, d = oracle_mod.rmat_edges(0x5EED0026, 12, 0, 1 << 14, True)
+    with gs.Summary("cc", capacity_hint=1 << 12) as x:
+        g = gs.Group(x, gs.group_unique_id(), 1, 0, 0)
+        x.fold(s, d)  # tracking is off: no delta capacity limit applies
+        g.tree_combine()
+        with pytest.raises(gs.GSError):
+            g.fold_device(None, None, 0)
+        v, lab = x.labels()
+        g.close()
+    ov, olab = oracle_mod.cc_labels(s, d)
+    assert np.array_equal(v, ov) and np.array_equal(lab, olab)
