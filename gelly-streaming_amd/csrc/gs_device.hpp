@@ -347,6 +347,63 @@ __device__ __forceinline__ void find_root(const Table& t, uint32_t x, uint32_t l
 #define GS_DBG(c) ((void)0)
 #endif
 
+// Wave-level combining of hooks that target the same root (the hub of a skewed
+// stream: while a giant component forms, most active edges of a wave are
+// (hub root H, smaller root lo_i) and every one of them would CAS H's link --
+// same-address atomics serialise at the memory side). For up to `rounds` groups of
+// active lanes sharing the larger-key root H, the lane with the smallest lo_m keeps
+// (H, lo_m) and every other lane rewrites its edge to (lo_i, lo_m) with parity
+// need_i ^ need_m -- the same partition (and colouring): H ~ lo_m and lo_i ~ lo_m
+// instead of H ~ lo_i, but CASes on lo_i's own link. Call in wave-uniform control
+// flow; `active` marks the lanes holding an edge.
+__device__ __forceinline__ int64_t wave_min_i64(int64_t x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int64_t y = __shfl_xor(x, o, 64);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+__device__ __forceinline__ void combine_hooks(bool active, uint32_t& a, int64_t& ka, uint32_t& b, int64_t& kb,
+                                              uint32_t& need, int rounds) {
+  const int lane = (int)(threadIdx.x & 63u);
+  const bool alo = ka < kb;
+  const uint32_t hi = alo ? b : a, lo = alo ? a : b;
+  const int64_t klo = alo ? ka : kb;
+  unsigned long long pending = __ballot(active);
+  for (int r = 0; r < rounds && __popcll(pending) >= 2; ++r) {
+    const int leader = __ffsll((long long)pending) - 1;
+    const uint32_t H = __shfl(hi, leader, 64);
+    const bool in = active && ((pending >> lane) & 1ull) && hi == H;
+    const unsigned long long grp = __ballot(in);
+    pending &= ~grp;
+    if (__popcll(grp) < 2) continue;
+    const int64_t m = wave_min_i64(in ? klo : INT64_MAX);
+    const int ml = __ffsll((long long)__ballot(in && klo == m)) - 1;
+    const uint32_t lo_m = __shfl(lo, ml, 64);
+    const uint32_t need_m = __shfl(need, ml, 64);
+    if (in && lane != ml) {
+      a = lo;
+      ka = klo;
+      b = lo_m;
+      kb = m;
+      need ^= need_m;
+    }
+  }
+}
+
+// Hook-loop finds with agent-scope (memory-side) link loads, or plain L2-cached
+// loads: a stale root only costs a failed CAS, which returns the live link.
+#ifndef GS_HOOK_FRESH
+#define GS_HOOK_FRESH 1
+#endif
+constexpr bool kHookFresh = GS_HOOK_FRESH != 0;
+#ifndef GS_HOOK_TTAS
+#define GS_HOOK_TTAS 1
+#endif
+constexpr bool kHookTTAS = GS_HOOK_TTAS != 0;
+
 template <bool SIGNED, bool TRACK>
 __device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, uint32_t a, uint32_t la, int64_t ka,
                                      uint32_t b, uint32_t lb, int64_t kb, uint32_t need) {
@@ -355,7 +412,7 @@ __device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, 
     GS_DBG(CTR_DBG_ITERS);
     GS_DIAG(1);
     uint32_t pa = 0, pb = 0;
-    find_root2<true>(t, a, la, ka, pa, b, lb, kb, pb);
+    find_root2<kHookFresh>(t, a, la, ka, pa, b, lb, kb, pb);
     la = a << 1;
     lb = b << 1;
     need ^= pa ^ pb;
@@ -368,7 +425,11 @@ __device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, 
     const uint32_t lo = a_lo ? a : b;
     const uint32_t expect = hi << 1;
     const uint32_t desired = (lo << 1) | (SIGNED ? (need & 1u) : 0u);
-    const uint32_t old = atomicCAS(&t.tab[hi].link, expect, desired);
+    // test-and-test-and-set: a root that a concurrent hook already moved (the hub
+    // root while a giant component forms) is seen by a cheap fresh load instead of
+    // a CAS that would queue behind every other CAS on that address
+    const uint32_t seen = kHookTTAS ? load_link_fresh(t.tab + hi) : expect;
+    const uint32_t old = seen == expect ? atomicCAS(&t.tab[hi].link, expect, desired) : seen;
     if (old == expect) {
       if (TRACK) {
         const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_DELTA + shard)], 1u);

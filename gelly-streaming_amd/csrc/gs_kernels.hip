@@ -102,6 +102,11 @@ struct FoldArgs {
   int inline_max;
 };
 
+#ifndef GS_COMBINE_ROUNDS
+#define GS_COMBINE_ROUNDS 2
+#endif
+constexpr int kCombineRounds = GS_COMBINE_ROUNDS;  // wave-level hook combining (combine_hooks)
+
 template <bool SIGNED, bool TRACK, int EPT, bool HOT>
 __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Lists L, FoldArgs a) {
   if (!HOT) t.hotcap = 0;  // compile-time: the plain path carries no hot-level code
@@ -218,6 +223,8 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Lists L, FoldArgs a) 
   for (int e = 0; e < EPT; ++e) {
     const unsigned long long m = __ballot(act[e]);
     const bool in_place = __popcll(m) <= (unsigned)a.inline_max;
+    if (in_place && kCombineRounds > 0 && __popcll(m) >= 2)  // wave-uniform
+      combine_hooks(act[e], ru[e], kru[e], rv[e], krv[e], need[e], kCombineRounds);
     if (!act[e]) continue;
     if (in_place) {
       hook<SIGNED, TRACK>(t, L, shard, ru[e], ru[e] << 1, kru[e], rv[e], rv[e] << 1, krv[e], need[e]);
