@@ -900,11 +900,12 @@ static int ensure_queue(gs_summary* h) {
 }
 
 // backlog q[qsel] + fresh delta -> send rows (first cap) and q[qsel ^ 1] (the rest)
-static int stage(gs_summary* h, int64_t* send, uint64_t cap) {
+static int stage(gs_summary* h, int64_t* send, uint64_t cap, int width = 3) {
   if (int rc = flush_hooks(h)) return rc;
   if (int rc = ensure_queue(h)) return rc;
   const int a = h->qsel, b = h->qsel ^ 1;
-  gs::launch_stage(h->table(), h->lists(), h->q[a], h->qn + a, h->q[b], h->qn + b, h->qcap, send, cap, h->stream);
+  gs::launch_stage(h->table(), h->lists(), h->q[a], h->qn + a, h->q[b], h->qn + b, h->qcap, send, cap, h->stream,
+                   nullptr, width);
   GS_HIP(hipGetLastError());
   h->qsel = b;
   h->delta_fill_ub = 0;
@@ -1176,6 +1177,7 @@ int rccl_fail(const char* what, int r) {
 constexpr int kNcclInt64 = 4;  // ncclInt64 (rccl.h)
 constexpr int kNcclUint8 = 1;  // ncclUint8 (rccl.h)
 constexpr uint64_t kHdrLag = 4;  // a retune reads the headers of the exchange kHdrLag batches back
+constexpr uint64_t kHdrSlots = 8;  // > kHdrLag: header copies of every retune period stay distinct
 
 }  // namespace
 
@@ -1183,41 +1185,82 @@ struct gs_group {
   gs_summary* h = nullptr;
   void* comm = nullptr;
   int nranks = 1, rank = 0;
+  int width = 3;  // int64 per exchange row: {a, b} for CC (16 B), {a, b, parity} for the signed kind
+  bool self_apply = false;  // test knob (GS_GROUP_SELF_APPLY=1): also fold this rank's own rows back
   uint64_t max_cap = 0, first_cap = 0, cap = 0, retune = 4;
-  int64_t* send = nullptr;  // [(max_cap + 1) * 3]
-  int64_t* recv = nullptr;  // [nranks * (max_cap + 1) * 3]
-  int64_t* hdr_host = nullptr;  // pinned [nranks * 3]
-  hipEvent_t hdr_ev = nullptr;
-  int64_t hdr_batch = -1;
+  // double-buffered exchange: exchange b stages into send[b % 2] and gathers into
+  // recv[b % 2] on the communication stream `xs` while the summary stream folds the
+  // next batch; its rows are folded during the next exchange (or finish)
+  int64_t* send[2] = {nullptr, nullptr};  // [(max_cap + 1) * 3]
+  int64_t* recv[2] = {nullptr, nullptr};  // [nranks * (max_cap + 1) * 3]
+  hipStream_t xs = nullptr;
+  hipEvent_t staged[2] = {nullptr, nullptr};    // on h->stream after the stage of an exchange
+  hipEvent_t gathered[2] = {nullptr, nullptr};  // on xs after its all-gather
+  // rank headers of kept exchanges, a ring of kHdrSlots: slot b % kHdrSlots holds
+  // the headers of exchange hdr_batch[slot] once hdr_ev[slot] has completed
+  int64_t* hdr_host = nullptr;  // pinned [kHdrSlots][nranks * 3]
+  hipEvent_t hdr_ev[kHdrSlots] = {};
+  int64_t hdr_batch[kHdrSlots] = {-1, -1, -1, -1, -1, -1, -1, -1};
   uint64_t b = 0;            // exchanges since create / finish
-  uint64_t last_rows = 0;
+  int pend = -1;             // buffer of the gathered-but-not-folded exchange, -1: none
+  uint64_t pend_rows = 0;
+  uint64_t last_rows = 0;    // rows per rank of the last exchange
+  int last_k = 0;            // its buffer
   uint64_t exchanges = 0;
 };
 
 namespace {
 
-// stage -> all-gather -> fold the other ranks' rows, all on the summary's stream
-int group_exchange(gs_group* g, uint64_t cap, bool keep_header) {
+// fold the other ranks' rows of a gathered exchange on the summary stream, behind
+// its all-gather (event), without host synchronisation
+int group_apply(gs_group* g, int k, uint64_t rows) {
+  gs_summary* h = g->h;
+  if (g->nranks == 1 && !g->self_apply) return GS_OK;
+  GS_HIP(hipStreamWaitEvent(h->stream, g->gathered[k], 0));
+  ExchangeLayout xl;
+  xl.rows = (uint32_t)rows;
+  xl.skip_rank = g->self_apply ? -1 : g->rank;
+  xl.base = g->recv[k];
+  const uint8_t* w = g->width == 3 ? reinterpret_cast<const uint8_t*>(g->recv[k] + 2) : nullptr;
+  return fold_device_impl(h, g->recv[k], g->recv[k] + 1, w, g->nranks * rows, g->width, 8 * g->width,
+                          /*track=*/false, true, xl);
+}
+
+// stage (summary stream) -> all-gather (communication stream) -> fold the PREVIOUS
+// exchange's rows (summary stream, overlapping this all-gather). apply_now also
+// folds this exchange's rows (finish).
+int group_exchange(gs_group* g, uint64_t cap, bool keep_header, bool apply_now) {
   gs_summary* h = g->h;
   const uint64_t rows = cap + 1;
-  if (int rc = stage(h, g->send, cap)) return rc;
-  const int r = g_rccl.allGather(g->send, g->recv, rows * 3, kNcclInt64, g->comm, h->stream);
+  const int k = (int)(g->b & 1u);
+  if (int rc = stage(h, g->send[k], cap, g->width)) return rc;
+  GS_HIP(hipEventRecord(g->staged[k], h->stream));
+  GS_HIP(hipStreamWaitEvent(g->xs, g->staged[k], 0));
+  const int r = g_rccl.allGather(g->send[k], g->recv[k], rows * g->width, kNcclInt64, g->comm, g->xs);
   if (r != 0) return rccl_fail("ncclAllGather", r);
   if (keep_header) {  // rank headers (row 0 of each rank's block) -> pinned host memory
-    GS_HIP(hipMemcpy2DAsync(g->hdr_host, 24, g->recv, rows * 24, 24, g->nranks, hipMemcpyDeviceToHost, h->stream));
-    GS_HIP(hipEventRecord(g->hdr_ev, h->stream));
-    g->hdr_batch = (int64_t)g->b;
+    const int slot = (int)(g->b % kHdrSlots);
+    GS_HIP(hipMemcpy2DAsync(g->hdr_host + (size_t)slot * g->nranks * 3, 24, g->recv[k], rows * 8 * g->width, 16,
+                            g->nranks, hipMemcpyDeviceToHost, g->xs));
+    GS_HIP(hipEventRecord(g->hdr_ev[slot], g->xs));
+    g->hdr_batch[slot] = (int64_t)g->b;
   }
-  if (g->nranks > 1) {
-    ExchangeLayout xl;
-    xl.rows = (uint32_t)rows;
-    xl.skip_rank = g->rank;
-    xl.base = g->recv;
-    if (int rc = fold_device_impl(h, g->recv, g->recv + 1, reinterpret_cast<const uint8_t*>(g->recv + 2),
-                                  g->nranks * rows, 3, 24, /*track=*/false, true, xl))
-      return rc;
+  GS_HIP(hipEventRecord(g->gathered[k], g->xs));
+  // Buffer reuse is ordered by construction: stage(b + 2) into send[k] follows, on
+  // the summary stream, the fold of exchange b (which waited for all-gather b), and
+  // all-gather(b + 2) into recv[k] waits for staged(b + 2), recorded after that fold.
+  if (g->pend >= 0) {
+    if (int rc = group_apply(g, g->pend, g->pend_rows)) return rc;
+    g->pend = -1;
+  }
+  if (apply_now) {
+    if (int rc = group_apply(g, k, rows)) return rc;
+  } else {
+    g->pend = k;
+    g->pend_rows = rows;
   }
   g->last_rows = rows;
+  g->last_k = k;
   g->b++;
   g->exchanges++;
   return GS_OK;
@@ -1249,19 +1292,29 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   g->h = h;
   g->nranks = nranks;
   g->rank = rank;
+  g->width = h->kind == GS_KIND_SIGNED ? 3 : 2;
   g->max_cap = std::min<uint64_t>(3ull * batch_edges, (uint64_t)gs::kShards * h->delta_shard_cap);
   g->first_cap = std::min<uint64_t>(first_cap ? first_cap : batch_edges, g->max_cap);
   g->cap = g->first_cap;
   if (const char* m = getenv("GS_GROUP_RETUNE")) g->retune = std::max(1, atoi(m));
+  if (const char* m = getenv("GS_GROUP_SELF_APPLY")) g->self_apply = atoi(m) != 0;
   auto bail = [&](int code) {
     gs_group_destroy(g);
     return code;
   };
   const size_t rows = g->max_cap + 1;
-  if (exchange && (hipMalloc(&g->send, rows * 24) != hipSuccess || hipMalloc(&g->recv, (size_t)nranks * rows * 24) != hipSuccess ||
-      hipHostMalloc(&g->hdr_host, (size_t)nranks * 24, hipHostMallocDefault) != hipSuccess ||
-      hipEventCreateWithFlags(&g->hdr_ev, hipEventDisableTiming) != hipSuccess))
-    return bail(fail(GS_ERR_HIP, "group buffer allocation failed"));
+  if (exchange) {
+    bool ok = hipHostMalloc(&g->hdr_host, (size_t)kHdrSlots * nranks * 24, hipHostMallocDefault) == hipSuccess &&
+              hipStreamCreateWithFlags(&g->xs, hipStreamNonBlocking) == hipSuccess;
+    for (int k = 0; k < (int)kHdrSlots && ok; ++k)
+      ok = hipEventCreateWithFlags(&g->hdr_ev[k], hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; k < 2 && ok; ++k)
+      ok = hipMalloc(&g->send[k], rows * 24) == hipSuccess &&
+           hipMalloc(&g->recv[k], (size_t)nranks * rows * 24) == hipSuccess &&
+           hipEventCreateWithFlags(&g->staged[k], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&g->gathered[k], hipEventDisableTiming) == hipSuccess;
+    if (!ok) return bail(fail(GS_ERR_HIP, "group buffer allocation failed"));
+  }
   Id128 uid;
   memcpy(uid.b, id, GS_GROUP_ID_BYTES);
   typedef int (*InitRank)(void**, int, Id128, int);
@@ -1275,40 +1328,49 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   if (!g) return fail(GS_ERR_INVALID, "null group");
   gs_summary* h = g->h;
   DeviceGuard dg(h->device);
-  if (!g->send) return fail(GS_ERR_INVALID, "tree-combine-only group (created with batch_edges 0)");
+  if (!g->send[0]) return fail(GS_ERR_INVALID, "tree-combine-only group (created with batch_edges 0)");
   if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
-  if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, /*track=*/true)) return rc;
   const uint64_t b = g->b;
-  const bool keep = (b + kHdrLag) % g->retune == 0;
-  if (int rc = group_exchange(g, g->cap, keep)) return rc;
-  // every `retune` exchanges all ranks re-derive the capacity from the same headers
-  if (b % g->retune == 0 && b >= kHdrLag && g->hdr_batch == (int64_t)(b - kHdrLag)) {
-    GS_HIP(hipEventSynchronize(g->hdr_ev));
+  // every `retune` exchanges all ranks re-derive the capacity from the same headers:
+  // those of exchange b - kHdrLag, read BEFORE this exchange may copy its own
+  const int lag_slot = (int)((b - kHdrLag) % kHdrSlots);
+  if (b % g->retune == 0 && b >= kHdrLag && g->hdr_batch[lag_slot] == (int64_t)(b - kHdrLag)) {
+    GS_HIP(hipEventSynchronize(g->hdr_ev[lag_slot]));
+    const int64_t* hh = g->hdr_host + (size_t)lag_slot * g->nranks * 3;
     int64_t queued = 0;
-    for (int r = 0; r < g->nranks; ++r) queued = std::max(queued, g->hdr_host[r * 3 + 1]);
+    for (int r = 0; r < g->nranks; ++r) queued = std::max(queued, hh[r * 3 + 1]);
     g->cap = std::min<uint64_t>(g->max_cap, std::max<uint64_t>(4096, (uint64_t)queued + (uint64_t)queued / 4 + 1024));
   }
-  return GS_OK;
+  if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, /*track=*/true)) return rc;
+  const bool keep = (b + kHdrLag) % g->retune == 0;
+  return group_exchange(g, g->cap, keep, /*apply_now=*/false);
 }
 
 int gs_group_finish(gs_group_t g) {
   if (!g) return fail(GS_ERR_INVALID, "null group");
   gs_summary* h = g->h;
   DeviceGuard dg(h->device);
+  if (g->pend >= 0) {
+    if (int rc = group_apply(g, g->pend, g->pend_rows)) return rc;
+    g->pend = -1;
+  }
   while (g->last_rows) {
     // headers of the last exchange -> remaining backlog on any rank (identical on every rank)
-    GS_HIP(hipMemcpy2DAsync(g->hdr_host, 24, g->recv, g->last_rows * 24, 24, g->nranks, hipMemcpyDeviceToHost,
-                            h->stream));
+    GS_HIP(hipStreamSynchronize(g->xs));
+    GS_HIP(hipMemcpy2DAsync(g->hdr_host, 24, g->recv[g->last_k], g->last_rows * 8 * g->width, 16, g->nranks,
+                            hipMemcpyDeviceToHost, h->stream));
     GS_HIP(hipStreamSynchronize(h->stream));
     int64_t remaining = 0;
     for (int r = 0; r < g->nranks; ++r) remaining = std::max(remaining, g->hdr_host[r * 3 + 1] - g->hdr_host[r * 3]);
     if (remaining <= 0) break;
-    if (int rc = group_exchange(g, std::min<uint64_t>((uint64_t)remaining, g->max_cap), false)) return rc;
+    if (int rc = group_exchange(g, std::min<uint64_t>((uint64_t)remaining, g->max_cap), false, /*apply_now=*/true))
+      return rc;
   }
   if (int rc = gs_sync(h)) return rc;
+  GS_HIP(hipStreamSynchronize(g->xs));
   g->b = 0;
   g->last_rows = 0;
-  g->hdr_batch = -1;
+  for (int k = 0; k < (int)kHdrSlots; ++k) g->hdr_batch[k] = -1;
   g->cap = g->first_cap;
   return GS_OK;
 }
@@ -1434,10 +1496,17 @@ int gs_group_destroy(gs_group_t g) {
   DeviceGuard dg(g->h->device);
   (void)hipStreamSynchronize(g->h->stream);
   if (g->comm && g_rccl.commDestroy) g_rccl.commDestroy(g->comm);
-  (void)hipFree(g->send);
-  (void)hipFree(g->recv);
+  if (g->xs) (void)hipStreamSynchronize(g->xs);
+  for (int k = 0; k < 2; ++k) {
+    (void)hipFree(g->send[k]);
+    (void)hipFree(g->recv[k]);
+    if (g->staged[k]) (void)hipEventDestroy(g->staged[k]);
+    if (g->gathered[k]) (void)hipEventDestroy(g->gathered[k]);
+  }
+  if (g->xs) (void)hipStreamDestroy(g->xs);
   if (g->hdr_host) (void)hipHostFree(g->hdr_host);
-  if (g->hdr_ev) (void)hipEventDestroy(g->hdr_ev);
+  for (int k = 0; k < (int)kHdrSlots; ++k)
+    if (g->hdr_ev[k]) (void)hipEventDestroy(g->hdr_ev[k]);
   delete g;
   return GS_OK;
 }

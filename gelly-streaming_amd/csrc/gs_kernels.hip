@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Lists L, FoldArgs a) 
     act[e] = false;
     if (valid[e] && a.rows) {  // exchange layout: per-rank header gives the live row count
       const uint32_t ig = a.base + i, r = ig / a.rows, j = ig - r * a.rows;
-      valid[e] = j >= 1 && (int)r != a.skip_rank && (int64_t)j <= a.hdr[(size_t)r * a.rows * 3];
+      valid[e] = j >= 1 && (int)r != a.skip_rank && (int64_t)j <= a.hdr[(size_t)r * a.rows * a.stride];
     }
     const uint32_t wi = (valid[e] && a.w) ? a.w[(size_t)i * a.w_stride] : 1u;
     if (wi & 0x80u) valid[e] = false;
@@ -322,15 +322,21 @@ __global__ __launch_bounds__(256) void k_export(Table t, int64_t* __restrict__ o
 // One exchange stage, one launch. Every delta record -- first the backlog q_in
 // (qn_in records left over from the previous stage), then the sharded delta list --
 // takes a position from one counter (block-aggregated): positions < cap go to send rows 1..cap,
-// the rest to the backlog q_out. The last block to finish writes the header row
-// {sent, queued, skip}, *qn_out, and resets the counters it consumed. The receiver
+// the rest to the backlog q_out. Send rows are `width` int64 wide ({a, b} or
+// {a, b, w}); the backlog is always {a, b, w}. The last block to finish writes the
+// header row {sent, queued[, skip]}, *qn_out, and resets the counters it consumed. The receiver
 // reads `sent` from the header, so unused send rows need no padding.
 // cap == 0 with send == nullptr: everything goes to q_out (gs_take_delta_records).
 __device__ __forceinline__ void stage_write(const Table& t, unsigned long long pos, int64_t a, int64_t b, int64_t w,
-                                            int64_t* send, uint64_t cap, int64_t* q_out, uint64_t qcap, bool plain) {
+                                            int64_t* send, uint64_t cap, int64_t* q_out, uint64_t qcap, bool plain,
+                                            int width) {
   int64_t* r;
-  if (pos < cap) {
-    r = send + (pos + (plain ? 0 : 1)) * 3;
+  if (pos < cap) {  // send rows are `width` int64 wide: {a, b} (CC) or {a, b, w}
+    r = send + (pos + (plain ? 0 : 1)) * width;
+    r[0] = a;
+    r[1] = b;
+    if (width == 3) r[2] = w;
+    return;
   } else if (plain) {
     return;  // take: records past cap are dropped (the caller sees the total count)
   } else if (pos - cap < qcap) {
@@ -351,7 +357,7 @@ __device__ __forceinline__ void stage_write(const Table& t, unsigned long long p
 __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* __restrict__ q_in,
                                                unsigned long long* qn_in, int64_t* __restrict__ q_out,
                                                unsigned long long* qn_out, uint64_t qcap, int64_t* __restrict__ send,
-                                               uint64_t cap, unsigned long long* count_out) {
+                                               uint64_t cap, unsigned long long* count_out, int width) {
   const bool plain = count_out != nullptr;  // take: rows from 0, no header, total -> *count_out
   __shared__ uint32_t cnt[kShards];
   __shared__ uint64_t off_sh, total_sh;
@@ -373,13 +379,13 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* 
   // backlog slice s
   const uint64_t per = (backlog + kShards - 1) / kShards;
   const uint64_t b0 = (uint64_t)s * per, b1 = min(backlog, b0 + per);
-  for (uint64_t i = b0 + threadIdx.x; i < b1; i += 256) stage_write(t, i, q_in[i * 3], q_in[i * 3 + 1], q_in[i * 3 + 2], send, cap, q_out, qcap, plain);
+  for (uint64_t i = b0 + threadIdx.x; i < b1; i += 256) stage_write(t, i, q_in[i * 3], q_in[i * 3 + 1], q_in[i * 3 + 2], send, cap, q_out, qcap, plain, width);
   // delta shard s
   const int64_t* in = L.drec + (size_t)s * L.delta_shard_cap * 3;
   const uint64_t off = off_sh;
   for (uint32_t j = threadIdx.x; j < cnt[s]; j += 256)
     stage_write(t, off + j, in[(size_t)j * 3], in[(size_t)j * 3 + 1], in[(size_t)j * 3 + 2], send, cap, q_out, qcap,
-                plain);
+                plain, width);
   if (s == 0 && threadIdx.x == 0 && plain) {
     *count_out = total;
     *qn_out = 0ull;
@@ -388,7 +394,7 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* 
     if (send) {
       send[0] = (int64_t)sent;
       send[1] = (int64_t)total;
-      send[2] = 0x80;
+      if (width == 3) send[2] = 0x80;
       atomicAdd((unsigned long long*)&t.ctr[ctr_index(CTR_SENT)], (unsigned long long)sent);
     }
     *qn_out = total - sent;
@@ -475,9 +481,9 @@ void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t*
 
 void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned long long* qn_in, int64_t* q_out,
                   unsigned long long* qn_out, uint64_t qcap, int64_t* send, uint64_t cap, hipStream_t st,
-                  unsigned long long* count_out) {
+                  unsigned long long* count_out, int width) {
   hipLaunchKernelGGL(k_stage, dim3(kShards), dim3(256), 0, st, t, L, q_in, qn_in, q_out, qn_out, qcap, send, cap,
-                     count_out);
+                     count_out, width);
 }
 
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st) {

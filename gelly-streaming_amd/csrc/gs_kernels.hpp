@@ -21,7 +21,7 @@ void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t*
                    hipStream_t st);
 void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned long long* qn_in, int64_t* q_out,
                   unsigned long long* qn_out, uint64_t qcap, int64_t* send, uint64_t cap, hipStream_t st,
-                  unsigned long long* count_out = nullptr);
+                  unsigned long long* count_out = nullptr, int width = 3);
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st);
 
 }  // namespace gs

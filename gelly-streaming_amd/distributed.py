@@ -29,6 +29,7 @@ import torch.distributed as dist
 
 SKIP = 0x80  # wire record w bit 7: padding / header row
 HDR_LAG = 4  # a retune reads the gathered headers of the exchange HDR_LAG batches back
+HDR_SLOTS = 8  # > HDR_LAG: header copies of successive retune periods never overwrite each other
 
 
 class DeltaExchangeFold:
@@ -54,13 +55,15 @@ class DeltaExchangeFold:
         rows = self.max_cap + 1
         self.send = [torch.empty((rows, 3), dtype=torch.int64, device=self.dev) for _ in range(2)]
         self.recv = [torch.empty((self.world * rows, 3), dtype=torch.int64, device=self.dev) for _ in range(2)]
-        self.hdr = torch.zeros((self.world, 3), dtype=torch.int64, pin_memory=self.cuda)
+        # ring of HDR_SLOTS header copies (slot b % HDR_SLOTS = exchange hdr_batch[slot])
+        self.hdr = torch.zeros((HDR_SLOTS, self.world, 3), dtype=torch.int64, pin_memory=self.cuda)
         if self.cuda:
             self.stream = torch.cuda.ExternalStream(summary.stream, device=self.dev)
             self.ev_staged = [torch.cuda.Event() for _ in range(2)]
             self.ev_done = [torch.cuda.Event() for _ in range(2)]
-            self.ev_hdr = torch.cuda.Event()
+            self.ev_hdr = [torch.cuda.Event() for _ in range(HDR_SLOTS)]
         self.rows_received = 0
+        self.cap_history = []  # cap of every exchange (diagnostics / tests)
         self._reset_state()
         self.s.set_delta_tracking(True)
 
@@ -70,9 +73,10 @@ class DeltaExchangeFold:
         asynchronously and apply the previous batch's remote rows."""
         b = self.b
         self.b += 1
+        self._retune(b)  # before this exchange's own header copy can replace the lagged one
         self.s.fold_device(src, dst, n=n)
         self._exchange(b, self.cap, apply_now=False)
-        self._after(b)
+        self.cap_history.append(self.cap)
 
     def finish(self):
         """Apply the last exchange and drain every rank's backlog; afterwards all
@@ -95,7 +99,7 @@ class DeltaExchangeFold:
         self.b = 0
         self.cap = self.first_cap
         self.pending = None
-        self.hdr_batch = -1
+        self.hdr_batch = [-1] * HDR_SLOTS
         self.last_rows = 0
 
     def _exchange(self, b, cap, apply_now):
@@ -112,9 +116,9 @@ class DeltaExchangeFold:
             self.ev_done[k].record(cur)
             done = self.ev_done[k]
             if (b + HDR_LAG) % self.retune == 0:  # headers for the retune HDR_LAG batches later
-                self.hdr.copy_(recv.view(self.world, rows, 3)[:, 0, :], non_blocking=True)
-                self.ev_hdr.record(cur)
-                self.hdr_batch = b
+                self.hdr[b % HDR_SLOTS].copy_(recv.view(self.world, rows, 3)[:, 0, :], non_blocking=True)
+                self.ev_hdr[b % HDR_SLOTS].record(cur)
+                self.hdr_batch[b % HDR_SLOTS] = b
         else:  # gloo: stage through host memory (CPU tests, several ranks on one GPU)
             self.s.sync()
             local = send.cpu()
@@ -122,8 +126,8 @@ class DeltaExchangeFold:
             dist.all_gather(parts, local, group=self.group)
             recv.copy_(torch.cat(parts))
             if (b + HDR_LAG) % self.retune == 0:
-                self.hdr.copy_(torch.stack([p[0] for p in parts]))
-                self.hdr_batch = b
+                self.hdr[b % HDR_SLOTS].copy_(torch.stack([p[0] for p in parts]))
+                self.hdr_batch[b % HDR_SLOTS] = b
             done = None
         item = (recv, done, rows)
         if apply_now:
@@ -133,12 +137,14 @@ class DeltaExchangeFold:
                 self._apply(*self.pending)
             self.pending = item
 
-    def _after(self, b):
+    def _retune(self, b):
         # every `retune` batches all ranks re-derive cap from the same gathered headers
-        if b % self.retune == 0 and b >= HDR_LAG and self.hdr_batch == b - HDR_LAG:
+        # (those of exchange b - HDR_LAG, copied when that exchange ran)
+        slot = (b - HDR_LAG) % HDR_SLOTS
+        if b % self.retune == 0 and b >= HDR_LAG and self.hdr_batch[slot] == b - HDR_LAG:
             if self.cuda:
-                self.ev_hdr.synchronize()
-            queued = int(self.hdr[:, 1].max())
+                self.ev_hdr[slot].synchronize()
+            queued = int(self.hdr[slot, :, 1].max())
             self.cap = int(min(self.max_cap, max(4096, queued + queued // 4 + 1024)))
 
     def _remaining_after_last(self):

@@ -101,7 +101,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, src, dst, batch, out):
+def _worker(rank, world, port, src, dst, batch, retune, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -111,7 +111,7 @@ def _worker(rank, world, port, src, dst, batch, out):
     from gelly_streaming_amd.distributed import DeltaExchangeFold
 
     rep = ModelReplica()
-    x = DeltaExchangeFold(rep, batch, torch.device("cpu"), first_cap=max(1, batch // 16), retune=4)
+    x = DeltaExchangeFold(rep, batch, torch.device("cpu"), first_cap=max(1, batch // 16), retune=retune)
     s = torch.from_numpy(src)
     d = torch.from_numpy(dst)
     g = batch * world
@@ -121,20 +121,23 @@ def _worker(rank, world, port, src, dst, batch, out):
         x.step(s[lo:], d[lo:], n)
     x.finish()
     v, lab = rep.labels()
-    out[rank] = (v.tolist(), lab.tolist(), x.rows_received)
+    out[rank] = (v.tolist(), lab.tolist(), x.rows_received, list(x.cap_history))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_delta_exchange_gloo(oracle_mod, world):
+@pytest.mark.parametrize("world,retune", [(2, 4), (3, 4), (2, 2), (3, 1)])
+def test_delta_exchange_gloo(oracle_mod, world, retune):
     src, dst = oracle_mod.rmat_edges(0x5EED0026, 12, 0, 1 << 13, True)
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), src, dst, 256, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), src, dst, 256, retune, out), nprocs=world, join=True)
     ov, olab = oracle_mod.cc_labels(src, dst)
     for r in range(world):
-        v, lab, exchanged = out[r]
+        v, lab, exchanged, caps = out[r]
         assert v == ov.tolist(), "rank %d vertex set" % r
         assert lab == olab.tolist(), "rank %d labels" % r
         assert exchanged > 0
+        # the capacity is re-derived from lagged headers (every 4 exchanges from the 4th)
+        assert caps[0] == 16 and caps[4] != 16, caps[:8]
+        assert caps == out[0][3], "ranks must agree on every exchange size"
