@@ -69,6 +69,26 @@ for k in fold:
 os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
 with open(os.path.join(root, "profiles", "%s_rocprof_summary.json" % tag), "w") as f:
     json.dump(out, f, indent=1)
+# per-launch HBM traffic of the plain CC fold, read by bench.py for roofline.traffic
+plain = "k_fold<false, false, 1, false>"
+r = out["kernels"].get(plain, {})
+if "derived" in r and r["derived"].get("read_requests"):
+    dv = r["derived"]
+    traffic = {
+        "round": tag, "workload": "rmat26-cc-stream", "batch": 1 << 20, "kernel": plain,
+        "avg_us_rocprof": r.get("avg_us"), "read_requests_per_launch": dv["read_requests"],
+        "bytes_per_read_request": 128, "write_bytes_per_launch": dv["write_bytes"],
+        "hbm_bytes_per_launch": dv["hbm_read_bytes"] + dv["write_bytes"],
+        "fetch_size_kib_raw": r["pmc_FETCH_SIZE"], "l2_hit_rate": dv["l2_hit_rate"],
+        "method": "separate rocprofv3 --pmc passes (tools/rocprof_round.sh, --pipeline 1) over one bench step; "
+                  "read bytes = TCC_EA0_RDREQ x 128 B: on gfx950 one L2->fabric read request moves 128 B both "
+                  "for 16-B/lane streaming (256 MiB = 2.10 M requests) and for random 16-B loads (same request "
+                  "ceiling), see profiles/r01_calib_random_pmc.json; FETCH_SIZE tallies 64 B per request "
+                  "(MI355X_MICROARCH.md HBM section: x2); writes = WRITE_SIZE (KiB)",
+        "source": "profiles/%s_rocprof_summary.json" % tag,
+    }
+    with open(os.path.join(root, "profiles", "pmc_fold_traffic.json"), "w") as f:
+        json.dump(traffic, f, indent=1)
 lines = ["# rocprofv3 summary %s" % tag, "", "| kernel | calls | avg us | total us | % | extra |", "|---|---|---|---|---|---|"]
 for k, r in sorted(out["kernels"].items(), key=lambda kv: -kv[1].get("total_us", 0)):
     extra = ", ".join("%s=%s" % (a[4:], b) for a, b in r.items() if a.startswith("pmc_"))
