@@ -63,6 +63,10 @@ class NativeExchange:
     def step(self, src, dst, n):
         self.g.fold_device(src, dst, n)
 
+    def run(self, src, dst, n, batch):
+        """every micro-batch of this rank's shard, looped natively"""
+        self.g.fold_batches(src, dst, n, batch)
+
     def finish(self):
         self.g.finish()
 
@@ -288,13 +292,16 @@ def main():
 
     def one_step():
         summ.reset()
-        for b in range(nbatch):
-            o = b * B
-            n = min(B, per - o)
-            if xch is None:
-                summ.fold_device(src[o:], dst[o:], n=n)
-            else:
-                xch.step(src[o:], dst[o:], n)
+        if isinstance(xch, NativeExchange):
+            xch.run(src, dst, per, B)
+        else:
+            for b in range(nbatch):
+                o = b * B
+                n = min(B, per - o)
+                if xch is None:
+                    summ.fold_device(src[o:], dst[o:], n=n)
+                else:
+                    xch.step(src[o:], dst[o:], n)
         if xch is not None:
             xch.finish()
         nlabels[0] = summ.export_labels_device(out_v, out_l)  # canonical label pass (syncs)

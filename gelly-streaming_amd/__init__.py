@@ -45,6 +45,7 @@ EXPORTED_SYMBOLS = (
     "gs_parse_edges_device", "gs_fold_text",
     "gs_group_unique_id", "gs_group_create", "gs_group_fold_device", "gs_group_finish", "gs_group_stats",
     "gs_group_destroy", "gs_group_tree_combine", "gs_combine_exported_device",
+    "gs_group_fold_batches_device",
 )
 
 
@@ -121,6 +122,7 @@ def lib():
     L.gs_group_stats.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_u64)]
     L.gs_group_destroy.argtypes = [_vp]
     L.gs_group_tree_combine.argtypes = [_vp]
+    L.gs_group_fold_batches_device.argtypes = [_vp, _vp, _vp, _sz, _sz]
     L.gs_combine_exported_device.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.c_int]
     _lib = L
     return L
@@ -361,6 +363,10 @@ class Group:
 
     def fold_device(self, src, dst, n):
         _check(lib().gs_group_fold_device(self._g, _ptr(src), _ptr(dst), int(n)))
+
+    def fold_batches(self, src, dst, n, batch):
+        """ceil(n / batch) micro-batches of fold_device, looped in native code."""
+        _check(lib().gs_group_fold_batches_device(self._g, _ptr(src), _ptr(dst), int(n), int(batch)))
 
     def finish(self):
         _check(lib().gs_group_finish(self._g))

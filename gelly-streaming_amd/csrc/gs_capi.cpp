@@ -1346,6 +1346,14 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   return group_exchange(g, g->cap, keep, /*apply_now=*/false);
 }
 
+int gs_group_fold_batches_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n, size_t batch) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  if (batch == 0) return fail(GS_ERR_INVALID, "batch is 0");
+  for (size_t off = 0; off < n; off += batch)
+    if (int rc = gs_group_fold_device(g, src + off, dst + off, std::min(batch, n - off))) return rc;
+  return GS_OK;
+}
+
 int gs_group_finish(gs_group_t g) {
   if (!g) return fail(GS_ERR_INVALID, "null group");
   gs_summary* h = g->h;

@@ -51,6 +51,11 @@ int gs_group_create(gs_group_t* g, gs_handle h, const void* id, int nranks, int 
  * including 0). */
 int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n);
 
+/* ceil(n / batch) consecutive gs_group_fold_device calls over src[0..n) in
+ * batch-edge micro-batches, looped natively (no per-batch host-language hop).
+ * Collective: every rank must issue the same number of micro-batches. */
+int gs_group_fold_batches_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n, size_t batch);
+
 /* Drain every rank's queued records (synchronous rounds) and synchronise; then all
  * replicas are identical. Collective. */
 int gs_group_finish(gs_group_t g);

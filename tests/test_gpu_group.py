@@ -36,6 +36,26 @@ def test_group_single_rank_matches_oracle(gs, oracle_mod, monkeypatch, first_cap
     assert np.array_equal(v, ov) and np.array_equal(lab, olab)
 
 
+def test_group_fold_batches_native_loop(gs, oracle_mod, monkeypatch):
+    """gs_group_fold_batches_device == the per-batch calls (ragged last batch)."""
+    import torch
+    monkeypatch.setenv("GS_GROUP_SELF_APPLY", "1")
+    n, B = (1 << 16) + 777, 1 << 12
+    src = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int64, device="cuda")
+    gs.gen_rmat(src, dst, 0, n, 14, 0x5EED0026, True)
+    torch.cuda.synchronize()
+    with gs.Summary("cc", capacity_hint=1 << 14) as s:
+        g = gs.Group(s, gs.group_unique_id(), 1, 0, B)
+        g.fold_batches(src, dst, n, B)
+        g.finish()
+        assert g.stats()["exchanges"] >= (n + B - 1) // B
+        v, lab = s.labels()
+        g.close()
+    ov, olab = oracle_mod.cc_labels(src.cpu().numpy(), dst.cpu().numpy())
+    assert np.array_equal(v, ov) and np.array_equal(lab, olab)
+
+
 @pytest.mark.parametrize("inject", [(), (1 << 15,)])
 def test_group_signed_rows_self_apply(gs, oracle_mod, monkeypatch, inject):
     """Signed summary in a group: 24-B rows {a, b, parity}; the rank folds its own
