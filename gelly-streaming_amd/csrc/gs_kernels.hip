@@ -94,7 +94,7 @@ struct FoldArgs {
   uint32_t w_stride;  // bytes between consecutive w entries
   uint32_t rows;      // > 0: exchange layout, `rows` records per rank, row 0 = header {sent, ...}
   int skip_rank;      // rank whose rows are skipped (the caller's own)
-  const int64_t* hdr; // exchange layout: start of the gathered buffer (rank r header at hdr[r * rows * 3])
+  const int64_t* hdr; // exchange layout: start of the gathered buffer (rank r header at hdr[r * rows * stride])
   uint32_t base;      // exchange layout: index of this launch's first record in the gathered buffer
   int cur;
   int drain;
@@ -249,23 +249,28 @@ __global__ __launch_bounds__(256) void k_hook(Table t, Lists L, int set) {
 }
 
 // Export (vertex, label, parity) of every occupied slot. Each thread owns 16 slots
-// of a 4096-slot tile (slot = tile + j*256 + tid: coalesced 16-B loads); the block
+// of a 16 x kExportBS-slot tile (slot = tile + j*kExportBS + tid: coalesced 16-B loads); the block
 // reserves its output range with ONE atomic per tile.
+#ifndef GS_EXPORT_BS
+#define GS_EXPORT_BS 256
+#endif
+constexpr uint32_t kExportBS = GS_EXPORT_BS;  // one output-reservation atomic per 16 x kExportBS slots
+
 template <bool SIGNED>
-__global__ __launch_bounds__(256) void k_export(Table t, int64_t* __restrict__ ov, int64_t* __restrict__ ol,
+__global__ __launch_bounds__(kExportBS) void k_export(Table t, int64_t* __restrict__ ov, int64_t* __restrict__ ol,
                                                 uint8_t* __restrict__ op, uint64_t cap_out) {
   constexpr int PER = 16;
-  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t wsum[kExportBS / 64];
   __shared__ uint32_t base_sh;
   const uint64_t nslots = (uint64_t)t.r0 + 2;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (uint64_t tile = (uint64_t)blockIdx.x * (256 * PER); tile < nslots; tile += (uint64_t)gridDim.x * (256 * PER)) {
+  for (uint64_t tile = (uint64_t)blockIdx.x * (kExportBS * PER); tile < nslots; tile += (uint64_t)gridDim.x * (kExportBS * PER)) {
     int64_t vk[PER], lk[PER];
     uint32_t pp[PER];
     uint32_t occ = 0, cnt = 0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const uint64_t s = tile + (uint64_t)j * 256 + threadIdx.x;
+      const uint64_t s = tile + (uint64_t)j * kExportBS + threadIdx.x;
       vk[j] = 0;
       lk[j] = 0;
       pp[j] = 0;
@@ -297,7 +302,7 @@ __global__ __launch_bounds__(256) void k_export(Table t, int64_t* __restrict__ o
     if (lane == 63) wsum[wid] = x;
     __syncthreads();
     uint32_t wbase = 0, total = 0;
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < (int)(kExportBS / 64); ++q) {
       if (q < wid) wbase += wsum[q];
       total += wsum[q];
     }
@@ -471,12 +476,14 @@ void launch_hook(bool sign, bool track, const Table& t, const Lists& L, int set,
 
 void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, hipStream_t st) {
   const uint64_t nslots = (uint64_t)t.r0 + 2;
-  const uint64_t tiles = (nslots + 4095) / 4096;
-  const unsigned g = (unsigned)(tiles < 4096 ? tiles : 4096);
+  const uint64_t tile = 16ull * kExportBS;
+  const uint64_t tiles = (nslots + tile - 1) / tile;
+  const uint64_t cap_blocks = 4096ull * 256 / kExportBS;
+  const unsigned g = (unsigned)(tiles < cap_blocks ? tiles : cap_blocks);
   if (sign)
-    hipLaunchKernelGGL((k_export<true>), dim3(g), dim3(256), 0, st, t, ov, ol, op, cap_out);
+    hipLaunchKernelGGL((k_export<true>), dim3(g), dim3(kExportBS), 0, st, t, ov, ol, op, cap_out);
   else
-    hipLaunchKernelGGL((k_export<false>), dim3(g), dim3(256), 0, st, t, ov, ol, op, cap_out);
+    hipLaunchKernelGGL((k_export<false>), dim3(g), dim3(kExportBS), 0, st, t, ov, ol, op, cap_out);
 }
 
 void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned long long* qn_in, int64_t* q_out,
