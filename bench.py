@@ -304,7 +304,10 @@ def main():
                     xch.step(src[o:], dst[o:], n)
         if xch is not None:
             xch.finish()
-        nlabels[0] = summ.export_labels_device(out_v, out_l)  # canonical label pass (syncs)
+        if world > 1:  # replicas are equal: each rank emits its 1/N slot range of the label pass
+            nlabels[0] = summ.export_labels_part_device(rank, world, out_v, out_l)
+        else:
+            nlabels[0] = summ.export_labels_device(out_v, out_l)  # canonical label pass (syncs)
 
     def barrier():
         summ.sync()
@@ -326,6 +329,11 @@ def main():
         elapsed = float(t.item())
     total_edges = E * args.steps
     value = total_edges / elapsed
+    labelled = nlabels[0]
+    if world > 1:  # vertices labelled by all ranks' slices (outside the timed region)
+        c = torch.tensor([labelled], dtype=torch.int64, device=dev)
+        dist.all_reduce(c)
+        labelled = int(c.item())
 
     # Roofline of the dominant kernel (k_fold): HIP events around every launch on
     # the summary's own stream, over one extra full step (same work as a timed step).
@@ -395,7 +403,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": "rmat%d-cc-stream" % args.scale, "scale": args.scale,
                        "edges": E, "micro_batch": B, "ids": "sparse 64-bit (scrambled)",
-                       "vertices_labelled": int(nlabels[0]),
+                       "vertices_labelled": int(labelled),
                        "parallelism": ("edge-shard x%d, per-batch delta all-gather (%s)" % (world, args.exchange_impl))
                        if xch is not None else "single GPU"},
             "roofline": roof,

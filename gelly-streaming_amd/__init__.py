@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
     "gs_parse_edges_device", "gs_fold_text",
     "gs_group_unique_id", "gs_group_create", "gs_group_fold_device", "gs_group_finish", "gs_group_stats",
     "gs_group_destroy", "gs_group_tree_combine", "gs_combine_exported_device",
-    "gs_group_fold_batches_device",
+    "gs_group_fold_batches_device", "gs_export_labels_part_device",
 )
 
 
@@ -123,6 +123,8 @@ def lib():
     L.gs_group_destroy.argtypes = [_vp]
     L.gs_group_tree_combine.argtypes = [_vp]
     L.gs_group_fold_batches_device.argtypes = [_vp, _vp, _vp, _sz, _sz]
+    L.gs_export_labels_part_device.argtypes = [_vp, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _sz,
+                                               ctypes.POINTER(_sz)]
     L.gs_combine_exported_device.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.c_int]
     _lib = L
     return L
@@ -225,6 +227,14 @@ class Summary:
         _check(lib().gs_export_labels(self._h, v.ctypes.data, lab.ctypes.data, n, ctypes.byref(got)))
         o = np.argsort(v[: got.value], kind="stable")
         return v[: got.value][o], lab[: got.value][o]
+
+    def export_labels_part_device(self, part, nparts, v, label, parity=None):
+        """Part `part` of `nparts` disjoint slot ranges of export_labels_device."""
+        got = _sz()
+        cap = v.numel() if hasattr(v, "numel") else len(v)
+        _check(lib().gs_export_labels_part_device(self._h, int(part), int(nparts), _ptr(v), _ptr(label),
+                                                  _ptr(parity), cap, ctypes.byref(got)))
+        return got.value
 
     def combine_exported_device(self, v, label, parity, n, failed=False):
         """Fold another summary's exported (v, label, parity) DEVICE arrays into this

@@ -296,13 +296,14 @@ int flush_hooks(gs_summary* h) {
 }
 
 // Export every (vertex, label, parity) into device arrays; returns count.
-int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n) {
+int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n, int part = 0,
+                       int nparts = 1) {
   if (int rc = join_lanes(h)) return rc;
   if (int rc = flush_hooks(h)) return rc;
   GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, h->stream));
   {
     Prof pr(h, KID_EXPORT);
-    gs::launch_export(h->kind == GS_KIND_SIGNED, h->table(), v, l, p, cap, h->stream);
+    gs::launch_export(h->kind == GS_KIND_SIGNED, h->table(), v, l, p, cap, h->stream, part, nparts);
   }
   GS_HIP(hipGetLastError());
   uint32_t cnt = 0;
@@ -670,6 +671,16 @@ int gs_export_labels_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* pa
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
   return export_device_impl(h, v, label, parity, cap, n);
+}
+
+int gs_export_labels_part_device(gs_handle h, int part, int nparts, int64_t* v, int64_t* label, uint8_t* parity,
+                                 size_t cap, size_t* n) {
+  if (int rc = check(h)) return rc;
+  if (!n) return fail(GS_ERR_INVALID, "n is null");
+  if (nparts < 1 || part < 0 || part >= nparts) return fail(GS_ERR_INVALID, "bad part");
+  DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
+  return export_device_impl(h, v, label, parity, cap, n, part, nparts);
 }
 
 static int export_host(gs_handle h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n) {

@@ -258,13 +258,15 @@ constexpr uint32_t kExportBS = GS_EXPORT_BS;  // one output-reservation atomic p
 
 template <bool SIGNED>
 __global__ __launch_bounds__(kExportBS) void k_export(Table t, int64_t* __restrict__ ov, int64_t* __restrict__ ol,
-                                                uint8_t* __restrict__ op, uint64_t cap_out) {
+                                                uint8_t* __restrict__ op, uint64_t cap_out, uint64_t s_begin,
+                                                uint64_t s_end) {
   constexpr int PER = 16;
   __shared__ uint32_t wsum[kExportBS / 64];
   __shared__ uint32_t base_sh;
-  const uint64_t nslots = (uint64_t)t.r0 + 2;
+  const uint64_t nslots = s_end;  // slots [s_begin, s_end) of [0, r0 + 2)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (uint64_t tile = (uint64_t)blockIdx.x * (kExportBS * PER); tile < nslots; tile += (uint64_t)gridDim.x * (kExportBS * PER)) {
+  for (uint64_t tile = s_begin + (uint64_t)blockIdx.x * (kExportBS * PER); tile < nslots;
+       tile += (uint64_t)gridDim.x * (kExportBS * PER)) {
     int64_t vk[PER], lk[PER];
     uint32_t pp[PER];
     uint32_t occ = 0, cnt = 0;
@@ -474,16 +476,19 @@ void launch_hook(bool sign, bool track, const Table& t, const Lists& L, int set,
   if (sign && track) hipLaunchKernelGGL((k_hook<true, true>), g, b, 0, st, t, L, set);
 }
 
-void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, hipStream_t st) {
-  const uint64_t nslots = (uint64_t)t.r0 + 2;
+void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, hipStream_t st,
+                   int part, int nparts) {
+  const uint64_t all = (uint64_t)t.r0 + 2;
+  const uint64_t s0 = all * (uint64_t)part / (uint64_t)nparts, s1 = all * (uint64_t)(part + 1) / (uint64_t)nparts;
+  const uint64_t nslots = s1 - s0;
   const uint64_t tile = 16ull * kExportBS;
   const uint64_t tiles = (nslots + tile - 1) / tile;
   const uint64_t cap_blocks = 4096ull * 256 / kExportBS;
   const unsigned g = (unsigned)(tiles < cap_blocks ? tiles : cap_blocks);
   if (sign)
-    hipLaunchKernelGGL((k_export<true>), dim3(g), dim3(kExportBS), 0, st, t, ov, ol, op, cap_out);
+    hipLaunchKernelGGL((k_export<true>), dim3(g), dim3(kExportBS), 0, st, t, ov, ol, op, cap_out, s0, s1);
   else
-    hipLaunchKernelGGL((k_export<false>), dim3(g), dim3(kExportBS), 0, st, t, ov, ol, op, cap_out);
+    hipLaunchKernelGGL((k_export<false>), dim3(g), dim3(kExportBS), 0, st, t, ov, ol, op, cap_out, s0, s1);
 }
 
 void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned long long* qn_in, int64_t* q_out,

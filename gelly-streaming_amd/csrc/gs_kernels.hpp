@@ -18,7 +18,7 @@ void launch_fold(bool sign, bool track, int ept, const Table& t, const Lists& L,
                  uint32_t base, hipStream_t st);
 void launch_hook(bool sign, bool track, const Table& t, const Lists& L, int set, int blocks, hipStream_t st);
 void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out,
-                   hipStream_t st);
+                   hipStream_t st, int part = 0, int nparts = 1);
 void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned long long* qn_in, int64_t* q_out,
                   unsigned long long* qn_out, uint64_t qcap, int64_t* send, uint64_t cap, hipStream_t st,
                   unsigned long long* count_out = nullptr, int width = 3);

@@ -129,6 +129,15 @@ int gs_export_labels(gs_handle h, int64_t* v, int64_t* label, size_t cap, size_t
  * may be NULL) receives parity(v) xor parity(label) for GS_KIND_SIGNED. */
 int gs_export_labels_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* parity, size_t cap, size_t* n);
 
+/* Part `part` of `nparts` of the same export: the vertices whose dense id (table
+ * slot) lies in the part-th of nparts equal slot ranges. The parts are disjoint and
+ * together are exactly gs_export_labels_device. Replicas kept equal by a group
+ * (gs_group.h) emit the final label pass partitioned: rank r exports part r, like
+ * a Flink sink at parallelism p consuming a keyed stream. DEVICE arrays; *n on the
+ * host (synchronises). */
+int gs_export_labels_part_device(gs_handle h, int part, int nparts, int64_t* v, int64_t* label, uint8_t* parity,
+                                 size_t cap, size_t* n);
+
 /* Bipartiteness verdict so far (Candidates.getSuccess, :44-46): 1 = bipartite. */
 int gs_bip_status(gs_handle h, int* ok);
 

@@ -215,6 +215,33 @@ def test_pipelined_signed_folds(gs, oracle_mod):
         assert all(np.array_equal(x, y) for x, y in zip(ca[1:], cb[1:]))
 
 
+@pytest.mark.parametrize("kind,nparts", [("cc", 1), ("cc", 3), ("cc", 8), ("signed", 5)])
+def test_export_parts_partition_the_label_pass(gs, oracle_mod, kind, nparts):
+    """gs_export_labels_part_device: the parts are disjoint and together equal the
+    whole export (incl. the reserved INT64_MIN / INT64_MIN + 1 slots at the end)."""
+    import torch
+    if kind == "cc":
+        s, d = oracle_mod.rmat_edges(0x5EED0026, 13, 0, 1 << 16, True)
+        s = np.concatenate([s, np.array([np.iinfo(np.int64).min, 7], np.int64)])
+        d = np.concatenate([d, np.array([np.iinfo(np.int64).min + 1, np.iinfo(np.int64).min], np.int64)])
+    else:
+        s, d = oracle_mod.bip_edges(0x5EED0B1B, 11, 0, 1 << 15)
+    with gs.Summary(kind, capacity_hint=1 << 14) as x:
+        x.fold(s, d)
+        n = x.num_vertices()
+        v = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        lab = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        par = torch.empty(n + 1, dtype=torch.uint8, device="cuda")
+        got = x.export_labels_device(v, lab, par)
+        whole = sorted(zip(v[:got].tolist(), lab[:got].tolist(), par[:got].tolist()))
+        parts = []
+        for p in range(nparts):
+            k = x.export_labels_part_device(p, nparts, v, lab, par)
+            parts += list(zip(v[:k].tolist(), lab[:k].tolist(), par[:k].tolist()))
+        assert len(parts) == got == n
+        assert sorted(parts) == whole
+
+
 # ------------------------------------------------------------- combine / serialize / delta
 def test_combine_equals_whole(gs, oracle_mod):
     s, d = oracle_mod.rmat_edges(3, 14, 0, 1 << 16, True)
