@@ -118,6 +118,12 @@ struct gs_summary {
   hipEvent_t main_ev = nullptr;
   int lane_next = 0;
   bool lanes_dirty = false;
+  // side stream (a multi-GPU group's apply stream): folds of remote rows run there,
+  // overlapping this rank's own folds; every reader joins it (join_lanes), the
+  // handle's own folds do not (union commutes)
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev = nullptr;
+  bool side_dirty = false;
   // profiling
   bool profiling = false;
   struct Pending {
@@ -211,13 +217,28 @@ void drain_profile(gs_summary* h) {
 }
 
 // Order the handle's stream behind every fold still running on a lane.
-int join_lanes(gs_summary* h) {
+int join_pipe_lanes(gs_summary* h) {
   if (!h->lanes_dirty) return GS_OK;
   for (int i = 0; i < h->pipe_depth; ++i) {
     GS_HIP(hipEventRecord(h->lane_ev[i], h->lane[i]));
     GS_HIP(hipStreamWaitEvent(h->stream, h->lane_ev[i], 0));
   }
   h->lanes_dirty = false;
+  return GS_OK;
+}
+
+// can folds be launched on the side stream (plain fused folds, no profiling)
+bool side_ok(const gs_summary* h) {
+  return h->side && h->mode == gs_summary::FUSED && h->hotcap == 0 && !h->profiling;
+}
+
+int join_lanes(gs_summary* h) {
+  if (int rc = join_pipe_lanes(h)) return rc;
+  if (h->side_dirty) {
+    GS_HIP(hipEventRecord(h->side_ev, h->side));
+    GS_HIP(hipStreamWaitEvent(h->stream, h->side_ev, 0));
+    h->side_dirty = false;
+  }
   return GS_OK;
 }
 
@@ -277,6 +298,7 @@ struct ExchangeLayout {
   uint32_t rows = 0;  // > 0: gathered exchange buffer, rows per rank
   int skip_rank = -1;
   const int64_t* base = nullptr;
+  bool on_side = false;  // launch on h->side (a group's apply stream) instead of h->stream
 };
 int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
                      size_t stride, size_t w_stride, bool track, bool check_cap = true,
@@ -380,8 +402,10 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
   // commutative, so the forest after both is the same; readers join the lanes.
   const bool pipe = allow_pipe && h->pipe_depth > 1 && h->mode == gs_summary::FUSED && !track && xl.rows == 0 &&
                     h->hotcap == 0 && !h->profiling;
+  // remote rows of a group exchange: on the side stream, overlapping own folds
+  const bool side = xl.on_side && side_ok(h) && !track;
   if (!pipe) {
-    if (int rc = join_lanes(h)) return rc;
+    if (int rc = join_pipe_lanes(h)) return rc;  // the side stream is NOT joined: union commutes
   }
   const bool sign = h->kind == GS_KIND_SIGNED;
   for (size_t off = 0; off < n; off += kMaxChunk) {
@@ -404,7 +428,8 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       h->nv_pending = false;
       if (nv >= h->hot_target) h->hot_open = false;
     }
-    hipStream_t st = h->stream;
+    hipStream_t st = side ? h->side : h->stream;
+    if (side) h->side_dirty = true;
     if (pipe) {  // the lane waits for the caller's work on the handle stream, not for the other lane
       GS_HIP(hipEventRecord(h->main_ev, h->stream));
       st = h->lane[h->lane_next];
@@ -1207,6 +1232,10 @@ struct gs_group {
   hipStream_t xs = nullptr;
   hipEvent_t staged[2] = {nullptr, nullptr};    // on h->stream after the stage of an exchange
   hipEvent_t gathered[2] = {nullptr, nullptr};  // on xs after its all-gather
+  hipEvent_t applied[2] = {nullptr, nullptr};   // after the fold of its rows (side or summary stream)
+  bool used[2] = {false, false};                // buffer k holds an exchange (events valid)
+  hipStream_t as = nullptr;                     // apply stream (installed as the summary's side stream)
+  hipEvent_t as_ev = nullptr;
   // rank headers of kept exchanges, a ring of kHdrSlots: slot b % kHdrSlots holds
   // the headers of exchange hdr_batch[slot] once hdr_ev[slot] has completed
   int64_t* hdr_host = nullptr;  // pinned [kHdrSlots][nranks * 3]
@@ -1224,17 +1253,26 @@ namespace {
 
 // fold the other ranks' rows of a gathered exchange on the summary stream, behind
 // its all-gather (event), without host synchronisation
+// On the summary's side stream (the group's apply stream) when possible, so this
+// rank's next own fold does not wait for the remote rows (union commutes).
 int group_apply(gs_group* g, int k, uint64_t rows) {
   gs_summary* h = g->h;
-  if (g->nranks == 1 && !g->self_apply) return GS_OK;
-  GS_HIP(hipStreamWaitEvent(h->stream, g->gathered[k], 0));
-  ExchangeLayout xl;
-  xl.rows = (uint32_t)rows;
-  xl.skip_rank = g->self_apply ? -1 : g->rank;
-  xl.base = g->recv[k];
-  const uint8_t* w = g->width == 3 ? reinterpret_cast<const uint8_t*>(g->recv[k] + 2) : nullptr;
-  return fold_device_impl(h, g->recv[k], g->recv[k] + 1, w, g->nranks * rows, g->width, 8 * g->width,
-                          /*track=*/false, true, xl);
+  const bool use_side = side_ok(h);
+  hipStream_t s = use_side ? h->side : h->stream;
+  if (g->nranks > 1 || g->self_apply) {
+    GS_HIP(hipStreamWaitEvent(s, g->gathered[k], 0));
+    ExchangeLayout xl;
+    xl.rows = (uint32_t)rows;
+    xl.skip_rank = g->self_apply ? -1 : g->rank;
+    xl.base = g->recv[k];
+    xl.on_side = use_side;
+    const uint8_t* w = g->width == 3 ? reinterpret_cast<const uint8_t*>(g->recv[k] + 2) : nullptr;
+    if (int rc = fold_device_impl(h, g->recv[k], g->recv[k] + 1, w, g->nranks * rows, g->width, 8 * g->width,
+                                  /*track=*/false, true, xl))
+      return rc;
+  }
+  GS_HIP(hipEventRecord(g->applied[k], s));
+  return GS_OK;
 }
 
 // stage (summary stream) -> all-gather (communication stream) -> fold the PREVIOUS
@@ -1244,6 +1282,14 @@ int group_exchange(gs_group* g, uint64_t cap, bool keep_header, bool apply_now) 
   gs_summary* h = g->h;
   const uint64_t rows = cap + 1;
   const int k = (int)(g->b & 1u);
+  if (g->used[k]) {
+    // buffer k last served exchange b - 2: its all-gather must have read send[k]
+    // before this stage rewrites it, and its rows must have been folded before this
+    // all-gather rewrites recv[k] (both long done in steady state)
+    GS_HIP(hipStreamWaitEvent(h->stream, g->gathered[k], 0));
+    GS_HIP(hipStreamWaitEvent(g->xs, g->applied[k], 0));
+  }
+  g->used[k] = true;
   if (int rc = stage(h, g->send[k], cap, g->width)) return rc;
   GS_HIP(hipEventRecord(g->staged[k], h->stream));
   GS_HIP(hipStreamWaitEvent(g->xs, g->staged[k], 0));
@@ -1257,9 +1303,6 @@ int group_exchange(gs_group* g, uint64_t cap, bool keep_header, bool apply_now) 
     g->hdr_batch[slot] = (int64_t)g->b;
   }
   GS_HIP(hipEventRecord(g->gathered[k], g->xs));
-  // Buffer reuse is ordered by construction: stage(b + 2) into send[k] follows, on
-  // the summary stream, the fold of exchange b (which waited for all-gather b), and
-  // all-gather(b + 2) into recv[k] waits for staged(b + 2), recorded after that fold.
   if (g->pend >= 0) {
     if (int rc = group_apply(g, g->pend, g->pend_rows)) return rc;
     g->pend = -1;
@@ -1323,8 +1366,21 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
       ok = hipMalloc(&g->send[k], rows * 24) == hipSuccess &&
            hipMalloc(&g->recv[k], (size_t)nranks * rows * 24) == hipSuccess &&
            hipEventCreateWithFlags(&g->staged[k], hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&g->gathered[k], hipEventDisableTiming) == hipSuccess;
+           hipEventCreateWithFlags(&g->gathered[k], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&g->applied[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) return bail(fail(GS_ERR_HIP, "group buffer allocation failed"));
+    // GS_GROUP_SIDE=0: fold remote rows on the summary stream (no overlap)
+    const char* sv = getenv("GS_GROUP_SIDE");
+    if (!(sv && atoi(sv) == 0)) {
+      if (h->side) return bail(fail(GS_ERR_INVALID, "the summary already belongs to an exchange group"));
+      if (hipStreamCreateWithFlags(&g->as, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&g->as_ev, hipEventDisableTiming) != hipSuccess)
+        return bail(fail(GS_ERR_HIP, "group stream creation failed"));
+      if (int rc = join_lanes(h)) return bail(rc);
+      h->side = g->as;
+      h->side_ev = g->as_ev;
+      h->side_dirty = false;
+    }
   }
   Id128 uid;
   memcpy(uid.b, id, GS_GROUP_ID_BYTES);
@@ -1388,6 +1444,7 @@ int gs_group_finish(gs_group_t g) {
   if (int rc = gs_sync(h)) return rc;
   GS_HIP(hipStreamSynchronize(g->xs));
   g->b = 0;
+  g->used[0] = g->used[1] = false;
   g->last_rows = 0;
   for (int k = 0; k < (int)kHdrSlots; ++k) g->hdr_batch[k] = -1;
   g->cap = g->first_cap;
@@ -1516,7 +1573,18 @@ int gs_group_destroy(gs_group_t g) {
   (void)hipStreamSynchronize(g->h->stream);
   if (g->comm && g_rccl.commDestroy) g_rccl.commDestroy(g->comm);
   if (g->xs) (void)hipStreamSynchronize(g->xs);
+  if (g->as) {
+    (void)hipStreamSynchronize(g->as);
+    if (g->h->side == g->as) {
+      g->h->side = nullptr;
+      g->h->side_ev = nullptr;
+      g->h->side_dirty = false;
+    }
+    (void)hipStreamDestroy(g->as);
+  }
+  if (g->as_ev) (void)hipEventDestroy(g->as_ev);
   for (int k = 0; k < 2; ++k) {
+    if (g->applied[k]) (void)hipEventDestroy(g->applied[k]);
     (void)hipFree(g->send[k]);
     (void)hipFree(g->recv[k]);
     if (g->staged[k]) (void)hipEventDestroy(g->staged[k]);
