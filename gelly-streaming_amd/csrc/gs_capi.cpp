@@ -70,6 +70,14 @@ struct gs_summary {
   bool nv_pending = false;
   uint32_t* ctr = nullptr;
   uint64_t nv_ub = 0;  // host upper bound of the vertex count
+  // capacity reports (k_report after every capacity-checked fold): a ring of packed
+  // words in host-coherent memory, read without any HIP call
+  static constexpr int kRepRing = 16;
+  unsigned long long* rep = nullptr;      // host pointer
+  unsigned long long* rep_dev = nullptr;  // its device mapping
+  uint64_t rep_seq = 0;
+  uint64_t e_launched = 0;  // edges of capacity-checked folds since reset / rebuild
+  uint64_t nv_exact = 0, e_exact = 0;  // an exact count and the edges complete when it was read
   // lists
   uint2* act = nullptr;
   uint32_t act_shard_cap = 0;
@@ -265,6 +273,21 @@ int read_nv(gs_summary* h, uint64_t* nv) {
   return GS_OK;
 }
 
+// After a reset or rebuild: `nv` vertices exactly, no fold in flight (the caller
+// joined every stream), the device's completed-edges counter zeroed with the rest.
+int reset_capacity_tracking(gs_summary* h, uint64_t nv) {
+  if (h->rep) {
+    // reports of earlier folds may still be landing: wait for them, then clear
+    if (h->stream) GS_HIP(hipStreamSynchronize(h->stream));
+    memset(h->rep, 0, gs_summary::kRepRing * 8);
+  }
+  h->nv_ub = nv;
+  h->nv_exact = nv;
+  h->e_exact = 0;
+  h->e_launched = 0;
+  return GS_OK;
+}
+
 // keep_delta: a rebuild (grow) keeps the pending delta counters.
 int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
   h->cap = cap;
@@ -288,7 +311,7 @@ int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
     gs::launch_init(h->tab, h->hotcap + cap + 2, h->stream);
   }
   GS_HIP(hipGetLastError());
-  h->nv_ub = 0;
+  reset_capacity_tracking(h, 0);
   h->epoch = 0;
   h->pending = -1;
   return GS_OK;
@@ -361,7 +384,7 @@ int grow(gs_summary* h, uint64_t new_cap) {
   rc = alloc_table(h, new_cap, /*keep_delta=*/true);
   if (rc) return rc;
   if (fail_flag) GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, h->stream));
-  h->nv_ub = got;
+  reset_capacity_tracking(h, got);
   rc = fold_device_impl(h, v, l, p, got, 1, 1, /*track=*/false, /*check_cap=*/false);
   h->track = track;
   if (rc) return rc;
@@ -372,20 +395,60 @@ int grow(gs_summary* h, uint64_t new_cap) {
   return GS_OK;
 }
 
+// Upper bound of the vertex count once `e_launched` edges have been folded: the
+// last exact count, or any capacity report, plus 2 new vertices per edge not yet
+// covered. Also returns whether every launched fold has reported.
+uint64_t capacity_bound(gs_summary* h, bool* all_reported) {
+  uint64_t best = h->nv_exact + 2 * (h->e_launched - h->e_exact);
+  uint64_t max_done = h->e_exact;
+  for (int i = 0; i < gs_summary::kRepRing; ++i) {
+    const unsigned long long w = __atomic_load_n(&h->rep[i], __ATOMIC_ACQUIRE);
+    if (!w) continue;
+    const uint64_t low = w & ((1ull << 33) - 1), c = w >> 33;
+    const uint64_t behind = (h->e_launched - low) & ((1ull << 33) - 1);  // edges launched after that report
+    if (behind > h->e_launched) continue;  // not from this epoch
+    best = std::min<uint64_t>(best, c + 2 * behind);
+    max_done = std::max<uint64_t>(max_done, h->e_launched - behind);
+  }
+  if (all_reported) *all_reported = max_done >= h->e_launched;
+  return best;
+}
+
 int ensure_capacity(gs_summary* h, size_t n) {
   const double limit = kMaxLoad * (double)h->cap;
-  h->nv_ub += 2 * (uint64_t)n;
-  if ((double)h->nv_ub <= limit) return GS_OK;
+  bool all = false;
+  // (the ring holds reports of capacity-checked folds only; e_launched counts them)
+  if ((double)(capacity_bound(h, nullptr) + 2 * (uint64_t)n) <= limit) {
+    h->nv_ub = capacity_bound(h, nullptr) + 2 * (uint64_t)n;
+    h->e_launched += n;
+    return GS_OK;
+  }
+  // wait for reports of the folds in flight (the GPU keeps working: no drain)
+  const auto t0 = std::chrono::steady_clock::now();
+  while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200)) {
+    const uint64_t b = capacity_bound(h, &all);
+    if ((double)(b + 2 * (uint64_t)n) <= limit) {
+      h->nv_ub = b + 2 * (uint64_t)n;
+      h->e_launched += n;
+      return GS_OK;
+    }
+    if (all) break;
+    std::this_thread::yield();
+  }
   uint64_t nv = 0;
-  int rc = read_nv(h, &nv);
+  int rc = read_nv(h, &nv);  // exact (joins every stream)
   if (rc) return rc;
+  h->nv_exact = nv;
+  h->e_exact = h->e_launched;
   h->nv_ub = nv + 2 * (uint64_t)n;
-  if ((double)h->nv_ub <= limit) return GS_OK;
-  uint64_t nc = h->cap;
-  while (kMaxLoad * (double)nc < (double)h->nv_ub) nc <<= 1;
-  rc = grow(h, nc);
-  if (rc) return rc;
-  h->nv_ub += 2 * (uint64_t)n;
+  if ((double)h->nv_ub > limit) {
+    uint64_t nc = h->cap;
+    while (kMaxLoad * (double)nc < (double)h->nv_ub) nc <<= 1;
+    rc = grow(h, nc);  // resets the tracking to the rebuilt table's exact count
+    if (rc) return rc;
+    h->nv_ub = h->nv_exact + 2 * (uint64_t)n;
+  }
+  h->e_launched += n;
   return GS_OK;
 }
 
@@ -444,6 +507,10 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
                       inline_max, xl.rows, xl.skip_rank, xl.base, (uint32_t)off, st);
     }
     GS_HIP(hipGetLastError());
+    if (check_cap) {
+      gs::launch_report(h->ctr, c, h->rep_dev + (h->rep_seq++ % gs_summary::kRepRing), st);
+      GS_HIP(hipGetLastError());
+    }
     if (h->hot_open && !h->nv_pending) {  // vertex count for the next hot-level decision
       GS_HIP(hipMemcpyAsync(h->h_nv, h->ctr + gs::ctr_index(gs::CTR_NV), gs::kShards * gs::kCtrStride * 4,
                             hipMemcpyDeviceToHost, h->stream));
@@ -533,6 +600,10 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
       return bail(fail(GS_ERR_HIP, "lane stream creation failed"));
   if (hipEventCreateWithFlags(&h->main_ev, hipEventDisableTiming) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
+  if (hipHostMalloc(&h->rep, gs_summary::kRepRing * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&h->rep_dev), h->rep, 0) != hipSuccess)
+    return bail(fail(GS_ERR_HIP, "capacity report buffer allocation failed"));
+  memset(h->rep, 0, gs_summary::kRepRing * 8);
   if (hipEventCreateWithFlags(&h->nv_ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(&h->h_nv, gs::kShards * gs::kCtrStride * 4, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&h->h_flags, 16, hipHostMallocDefault) != hipSuccess)
@@ -560,6 +631,7 @@ int gs_destroy(gs_handle h) {
     if (h->stage_ev[i]) (void)hipEventDestroy(h->stage_ev[i]);
   if (h->nv_ev) (void)hipEventDestroy(h->nv_ev);
   if (h->h_nv) (void)hipHostFree(h->h_nv);
+  if (h->rep) (void)hipHostFree(h->rep);
   if (h->h_flags) (void)hipHostFree(h->h_flags);
   if (h->h_text) (void)hipHostFree(h->h_text);
   if (h->h_tres) (void)hipHostFree(h->h_tres);
@@ -599,7 +671,7 @@ int gs_reset(gs_handle h) {
   h->nv_pending = false;
   GS_HIP(hipGetLastError());
   if (h->qn) GS_HIP(hipMemsetAsync(h->qn, 0, 16, h->stream));
-  h->nv_ub = 0;
+  if (int rc = reset_capacity_tracking(h, 0)) return rc;
   h->epoch = 0;
   h->pending = -1;
   h->delta_fill_ub = 0;

@@ -39,6 +39,10 @@ constexpr uint32_t kHotBucket = GS_HOT_BUCKET;  // hot-level bucket: slots loade
 #define GS_FOLD_BS 256
 #endif
 constexpr uint32_t kFoldBS = GS_FOLD_BS;  // k_fold threads per block
+#ifndef GS_INSERT_TTAS
+#define GS_INSERT_TTAS 1
+#endif
+constexpr bool kInsertTTAS = GS_INSERT_TTAS != 0;  // fresh key load before an insert CAS (lookup_resolve)
 constexpr int kShards = 64;      // sharded append counters (one 128-B line each)
 constexpr int kCtrStride = 32;   // u32 per counter line
 constexpr int kActSets = 3;     // active-edge lists: appended at epoch e, drained at e+1, zeroed at e+2
@@ -54,6 +58,7 @@ enum CounterBlock : int {
   CTR_STAGE_N_HI,
   CTR_STAGE_DONE,                // k_stage block ticket
   CTR_SENT,                      // records sent by all stages since reset (u64)
+  CTR_EDONE,                     // edges of completed folds since reset (u64, k_report)
   CTR_DBG_HOOKS,                 // debug build (-DGS_DEBUG_COUNTERS): hook calls,
   CTR_DBG_ITERS,                 //   hook-loop iterations,
   CTR_DBG_CASFAIL,               //   failed hook CASes
@@ -215,6 +220,17 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
     if (k == key) {
       link = l;
       return h;
+    }
+    if (k == kEmpty && kInsertTTAS) {
+      // test-and-test-and-set: an EMPTY read may be a stale line of a hub's slot that
+      // another XCD has filled; a fresh load settles it without queueing a CAS on
+      // that address (all of a hub's occurrences in a batch would otherwise CAS it)
+      k = (int64_t)__hip_atomic_load((unsigned long long*)&t.tab[h].key, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+      if (k == key) {
+        link = load_link_fresh(t.tab + h);
+        return h;
+      }
     }
     if (k == kEmpty) {
       const unsigned long long old =

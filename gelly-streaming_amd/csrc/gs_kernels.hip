@@ -419,6 +419,32 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* 
   }
 }
 
+// Capacity report, queued behind a fold on its stream: adds the fold's edge count
+// to the completed-edges counter, then reads the new-vertex count and writes both,
+// packed into one 64-bit word (count << 33 | edges mod 2^33), to host-coherent
+// memory. Every fold whose report preceded this one (by the atomic order of the
+// adds) had completed before this read, so count + 2 x (edges launched - edges
+// done) bounds the vertex count without a host synchronisation.
+__global__ __launch_bounds__(64) void k_report(uint32_t* ctr, unsigned long long n, unsigned long long* out) {
+  __shared__ unsigned long long done_sh;
+  if (threadIdx.x == 0)
+    done_sh = atomicAdd(reinterpret_cast<unsigned long long*>(ctr + ctr_index(CTR_EDONE)), n) + n;
+  __syncthreads();
+  uint32_t c = threadIdx.x < (uint32_t)kShards
+                   ? __hip_atomic_load(ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : 0u;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (threadIdx.x == 0) {
+    const unsigned long long w = ((unsigned long long)c << 33) | (done_sh & ((1ull << 33) - 1));
+    __hip_atomic_store(out, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+void launch_report(uint32_t* ctr, uint64_t n, unsigned long long* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_report, dim3(1), dim3(64), 0, st, ctr, (unsigned long long)n, out);
+}
+
 // Single-vertex lookup (gs_find): label and presence.
 __global__ void k_find_one(Table t, int64_t key, int64_t* out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
