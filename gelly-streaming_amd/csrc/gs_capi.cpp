@@ -76,6 +76,9 @@ struct gs_summary {
   unsigned long long* rep = nullptr;      // host pointer
   unsigned long long* rep_dev = nullptr;  // its device mapping
   uint64_t rep_seq = 0;
+  static constexpr int kRepEvery = 4;  // unpipelined folds report every 4th launch (one stream: a report is a gap)
+  int rep_skip = 0;
+  uint64_t rep_pending_edges = 0;      // edges of capacity-checked chunks not yet reported
   uint64_t e_launched = 0;  // edges of capacity-checked folds since reset / rebuild
   uint64_t nv_exact = 0, e_exact = 0;  // an exact count and the edges complete when it was read
   // lists
@@ -285,6 +288,8 @@ int reset_capacity_tracking(gs_summary* h, uint64_t nv) {
   h->nv_exact = nv;
   h->e_exact = 0;
   h->e_launched = 0;
+  h->rep_skip = 0;
+  h->rep_pending_edges = 0;
   return GS_OK;
 }
 
@@ -410,7 +415,9 @@ uint64_t capacity_bound(gs_summary* h, bool* all_reported) {
     best = std::min<uint64_t>(best, c + 2 * behind);
     max_done = std::max<uint64_t>(max_done, h->e_launched - behind);
   }
-  if (all_reported) *all_reported = max_done >= h->e_launched;
+  // edges waiting on the handle stream for its next report will not be claimed by
+  // waiting: count them as reported for the decision to stop waiting
+  if (all_reported) *all_reported = max_done + h->rep_pending_edges >= h->e_launched;
   return best;
 }
 
@@ -440,6 +447,8 @@ int ensure_capacity(gs_summary* h, size_t n) {
   if (rc) return rc;
   h->nv_exact = nv;
   h->e_exact = h->e_launched;
+  h->rep_pending_edges = 0;  // covered by e_exact (never claimed by a report: ring bounds stay conservative)
+  h->rep_skip = 0;
   h->nv_ub = nv + 2 * (uint64_t)n;
   if ((double)h->nv_ub > limit) {
     uint64_t nc = h->cap;
@@ -508,8 +517,26 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     }
     GS_HIP(hipGetLastError());
     if (check_cap) {
-      gs::launch_report(h->ctr, c, h->rep_dev + (h->rep_seq++ % gs_summary::kRepRing), st);
-      GS_HIP(hipGetLastError());
+      // A report may only claim chunks queued before it on ITS stream. Lanes and the
+      // side stream report every chunk (off the critical path); on the handle's own
+      // stream a report is a gap between folds, so it reports every kRepEvery-th
+      // chunk, claiming the chunks since its previous report. Unclaimed edges stay
+      // "in flight" in the bound, which is therefore always valid.
+      uint64_t claim = c;
+      bool report = true;
+      if (st == h->stream) {
+        h->rep_pending_edges += c;
+        claim = h->rep_pending_edges;
+        report = ++h->rep_skip >= gs_summary::kRepEvery;
+      }
+      if (report) {
+        gs::launch_report(h->ctr, claim, h->rep_dev + (h->rep_seq++ % gs_summary::kRepRing), st);
+        GS_HIP(hipGetLastError());
+        if (st == h->stream) {
+          h->rep_pending_edges = 0;
+          h->rep_skip = 0;
+        }
+      }
     }
     if (h->hot_open && !h->nv_pending) {  // vertex count for the next hot-level decision
       GS_HIP(hipMemcpyAsync(h->h_nv, h->ctr + gs::ctr_index(gs::CTR_NV), gs::kShards * gs::kCtrStride * 4,
