@@ -252,15 +252,19 @@ __global__ __launch_bounds__(256) void k_hook(Table t, Lists L, int set) {
 // of a 16 x kExportBS-slot tile (slot = tile + j*kExportBS + tid: coalesced 16-B loads); the block
 // reserves its output range with ONE atomic per tile.
 #ifndef GS_EXPORT_BS
-#define GS_EXPORT_BS 256
+#define GS_EXPORT_BS 1024
 #endif
-constexpr uint32_t kExportBS = GS_EXPORT_BS;  // one output-reservation atomic per 16 x kExportBS slots
+constexpr uint32_t kExportBS = GS_EXPORT_BS;  // one output-reservation atomic per kExportPer x kExportBS slots
+#ifndef GS_EXPORT_PER
+#define GS_EXPORT_PER 16
+#endif
+constexpr int kExportPer = GS_EXPORT_PER;  // slots per thread per tile
 
 template <bool SIGNED>
 __global__ __launch_bounds__(kExportBS) void k_export(Table t, int64_t* __restrict__ ov, int64_t* __restrict__ ol,
                                                 uint8_t* __restrict__ op, uint64_t cap_out, uint64_t s_begin,
                                                 uint64_t s_end) {
-  constexpr int PER = 16;
+  constexpr int PER = kExportPer;
   __shared__ uint32_t wsum[kExportBS / 64];
   __shared__ uint32_t base_sh;
   const uint64_t nslots = s_end;  // slots [s_begin, s_end) of [0, r0 + 2)
@@ -270,29 +274,36 @@ __global__ __launch_bounds__(kExportBS) void k_export(Table t, int64_t* __restri
     int64_t vk[PER], lk[PER];
     uint32_t pp[PER];
     uint32_t occ = 0, cnt = 0;
+    // 1) all of the thread's slots in flight together (coalesced 16-B loads)
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const uint64_t s = tile + (uint64_t)j * kExportBS + threadIdx.x;
       vk[j] = 0;
-      lk[j] = 0;
       pp[j] = 0;
       if (s < nslots) {
-        int64_t k;
-        uint32_t l;
-        load_slot(t.tab + s, k, l);
+        load_slot(t.tab + s, vk[j], pp[j]);
         const bool present = (s >= t.r0) ? ((t.tab[s].aux & 1u) != 0)
-                                         : (k != kEmpty && !(s < t.hotcap && k == kSealed));
+                                         : (vk[j] != kEmpty && !(s < t.hotcap && vk[j] == kSealed));
         if (present) {
-          uint32_t r, p;
-          int64_t rk;
-          find_root<false>(t, (uint32_t)s, l, k, r, p, rk);
-          vk[j] = k;
-          lk[j] = rk;
-          pp[j] = p;
           occ |= 1u << j;
           ++cnt;
         }
       }
+    }
+    // 2) read-only finds (the label pass does not compress: no stores between loads)
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      lk[j] = vk[j];
+      if (!((occ >> j) & 1u)) continue;
+      uint32_t x = (uint32_t)(tile + (uint64_t)j * kExportBS + threadIdx.x), lx = pp[j], acc = 0;
+      int64_t kx = vk[j];
+      while ((lx >> 1) != x) {
+        acc ^= lx & 1u;
+        x = lx >> 1;
+        load_slot(t.tab + x, kx, lx);
+      }
+      lk[j] = kx;
+      pp[j] = acc;
     }
     // block exclusive scan of cnt: wave inclusive scan + 4 wave totals in LDS
     uint32_t x = cnt;
@@ -507,7 +518,7 @@ void launch_export(bool sign, const Table& t, int64_t* ov, int64_t* ol, uint8_t*
   const uint64_t all = (uint64_t)t.r0 + 2;
   const uint64_t s0 = all * (uint64_t)part / (uint64_t)nparts, s1 = all * (uint64_t)(part + 1) / (uint64_t)nparts;
   const uint64_t nslots = s1 - s0;
-  const uint64_t tile = 16ull * kExportBS;
+  const uint64_t tile = (uint64_t)kExportPer * kExportBS;
   const uint64_t tiles = (nslots + tile - 1) / tile;
   const uint64_t cap_blocks = 4096ull * 256 / kExportBS;
   const unsigned g = (unsigned)(tiles < cap_blocks ? tiles : cap_blocks);
