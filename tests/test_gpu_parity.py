@@ -158,6 +158,25 @@ def test_table_growth_from_tiny_hint(gs, oracle_mod):
         _assert_cc_equal(ds, oracle_mod, s, d)
 
 
+@pytest.mark.parametrize("depth", [1, 3])
+def test_growth_under_pipelined_device_folds(gs, oracle_mod, depth):
+    """Capacity tracking from the k_report words (no host sync per fold): device
+    folds on 3 lanes from a tiny hint must grow the table in time (a missed bound
+    would overflow it: CTR_ERR -> GSError) and stay bit-exact."""
+    import torch
+    n, B = 1 << 18, 1 << 12
+    s = torch.empty(n, dtype=torch.int64, device="cuda")
+    d = torch.empty(n, dtype=torch.int64, device="cuda")
+    gs.gen_er(s, d, 0, n, 17, 0x5EED00E5, True)  # ER: nearly every endpoint is new early on
+    torch.cuda.synchronize()
+    with gs.Summary("cc", capacity_hint=16) as ds:
+        ds.set_pipelining(depth)
+        for i in range(0, n, B):
+            ds.fold_device(s[i:], d[i:], n=B)
+        assert ds.table_capacity() >= 1 << 17
+        _assert_cc_equal(ds, oracle_mod, s.cpu().numpy(), d.cpu().numpy())
+
+
 def test_rmat20_config2_full(gs, oracle_mod):
     # BASELINE config 2: RMAT-20, 16M edges, sparse ids, 1M-edge micro-batches.
     import torch
