@@ -1,3 +1,9 @@
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <unistd.h>
 // gs_capi.cpp -- implementation of the C ABI in include/gs_summary.h.
 //
 // One handle = one GPU-resident summary: the slot table (relabel + forest), the
@@ -1311,6 +1317,186 @@ int rccl_fail(const char* what, int r) {
 
 constexpr int kNcclInt64 = 4;  // ncclInt64 (rccl.h)
 constexpr int kNcclUint8 = 1;  // ncclUint8 (rccl.h)
+
+// ---------------------------------------------------------------------------
+// In-process emulation of the four RCCL calls the group uses, selected with
+// GS_GROUP_FAKE_COMM=1: N threads of ONE process, each driving one rank's summary
+// on the same GPU, meet at host barriers; the data moves with device copies
+// ordered by events. Test infrastructure only (RCCL refuses two ranks on one GPU,
+// and the GPU box has one): it runs the group's N-rank code paths -- exchange
+// layout with real remote rows, per-rank headers, retune, backlog drain, side-stream
+// apply, the binomial tree -- exactly as with RCCL.
+struct FakeShared {
+  int n = 0, refs = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  std::vector<const void*> src;
+  std::vector<hipEvent_t> ev;
+  struct Msg {
+    const void* buf;
+    size_t bytes;
+    hipEvent_t ready, copied;
+    bool done = false;
+  };
+  std::map<std::pair<int, int>, std::deque<Msg*>> box;  // (from, to) -> messages
+};
+struct FakeComm {
+  FakeShared* s;
+  int rank;
+  hipEvent_t ready = nullptr, done = nullptr;
+  std::vector<hipEvent_t> spare;  // message events, destroyed with the comm
+};
+std::mutex g_fake_mu;
+std::map<std::string, FakeShared*> g_fake_reg;
+
+void fake_barrier(FakeShared* s) {
+  std::unique_lock<std::mutex> lk(s->m);
+  const uint64_t g0 = s->gen;
+  if (++s->arrived == s->n) {
+    s->arrived = 0;
+    s->gen++;
+    s->cv.notify_all();
+  } else {
+    s->cv.wait(lk, [&] { return s->gen != g0; });
+  }
+}
+size_t fake_elem(int dtype) { return dtype == kNcclUint8 ? 1 : 8; }
+int fake_unique_id(void* id) {
+  static std::atomic<uint64_t> ctr{1};
+  memset(id, 0, GS_GROUP_ID_BYTES);
+  const uint64_t v[2] = {(uint64_t)getpid(), ctr++};
+  memcpy(id, v, sizeof v);
+  return 0;
+}
+int fake_init(void** comm, int n, Id128 id, int rank) {
+  std::lock_guard<std::mutex> lk(g_fake_mu);
+  FakeShared*& s = g_fake_reg[std::string(id.b, GS_GROUP_ID_BYTES)];
+  if (!s) {
+    s = new FakeShared();
+    s->n = n;
+    s->src.resize(n);
+    s->ev.resize(n);
+  }
+  s->refs++;
+  FakeComm* c = new FakeComm{s, rank};
+  if (hipEventCreateWithFlags(&c->ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess)
+    return 1;
+  *comm = c;
+  return 0;
+}
+int fake_destroy(void* comm) {
+  FakeComm* c = (FakeComm*)comm;
+  (void)hipEventDestroy(c->ready);
+  (void)hipEventDestroy(c->done);
+  for (hipEvent_t e : c->spare) (void)hipEventDestroy(e);
+  std::lock_guard<std::mutex> lk(g_fake_mu);
+  if (--c->s->refs == 0) {
+    for (auto it = g_fake_reg.begin(); it != g_fake_reg.end(); ++it)
+      if (it->second == c->s) {
+        g_fake_reg.erase(it);
+        break;
+      }
+    delete c->s;
+  }
+  delete c;
+  return 0;
+}
+int fake_all_gather(const void* send, void* recv, size_t count, int dtype, void* comm, hipStream_t st) {
+  FakeComm* c = (FakeComm*)comm;
+  FakeShared* s = c->s;
+  const size_t bytes = count * fake_elem(dtype);
+  if (hipEventRecord(c->ready, st) != hipSuccess) return 1;
+  {
+    std::lock_guard<std::mutex> lk(s->m);
+    s->src[c->rank] = send;
+    s->ev[c->rank] = c->ready;
+  }
+  fake_barrier(s);  // every rank's send buffer is staged (in its stream order)
+  for (int q = 0; q < s->n; ++q) {
+    if (hipStreamWaitEvent(st, s->ev[q], 0) != hipSuccess) return 1;
+    if (hipMemcpyAsync((char*)recv + (size_t)q * bytes, s->src[q], bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+      return 1;
+  }
+  if (hipEventRecord(c->done, st) != hipSuccess) return 1;
+  fake_barrier(s);  // (the ready events were captured by every stream's wait)
+  {
+    std::lock_guard<std::mutex> lk(s->m);
+    s->ev[c->rank] = c->done;
+  }
+  fake_barrier(s);
+  // the collective completes on this rank once every rank has read its send buffer
+  for (int q = 0; q < s->n; ++q)
+    if (q != c->rank && hipStreamWaitEvent(st, s->ev[q], 0) != hipSuccess) return 1;
+  fake_barrier(s);  // slots and events may be reused after this
+  return 0;
+}
+int fake_send(const void* buf, size_t count, int dtype, int peer, void* comm, hipStream_t st) {
+  FakeComm* c = (FakeComm*)comm;
+  FakeShared* s = c->s;
+  FakeShared::Msg msg{buf, count * fake_elem(dtype), nullptr, nullptr};
+  if (hipEventCreateWithFlags(&msg.ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&msg.copied, hipEventDisableTiming) != hipSuccess || hipEventRecord(msg.ready, st))
+    return 1;
+  c->spare.push_back(msg.ready);
+  c->spare.push_back(msg.copied);
+  std::unique_lock<std::mutex> lk(s->m);
+  s->box[{c->rank, peer}].push_back(&msg);
+  s->cv.notify_all();
+  s->cv.wait(lk, [&] { return msg.done; });  // the receiver has queued its copy
+  return hipStreamWaitEvent(st, msg.copied, 0) == hipSuccess ? 0 : 1;
+}
+int fake_recv(void* buf, size_t count, int dtype, int peer, void* comm, hipStream_t st) {
+  FakeComm* c = (FakeComm*)comm;
+  FakeShared* s = c->s;
+  std::unique_lock<std::mutex> lk(s->m);
+  auto& q = s->box[{peer, c->rank}];
+  s->cv.wait(lk, [&] { return !q.empty(); });
+  FakeShared::Msg* msg = q.front();
+  q.pop_front();
+  int r = 0;
+  if (msg->bytes != count * fake_elem(dtype)) r = 1;
+  if (!r && (hipStreamWaitEvent(st, msg->ready, 0) != hipSuccess ||
+             hipMemcpyAsync(buf, msg->buf, msg->bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+             hipEventRecord(msg->copied, st) != hipSuccess))
+    r = 1;
+  msg->done = true;
+  s->cv.notify_all();
+  return r;
+}
+int fake_noop() { return 0; }
+const char* fake_error(int) { return "in-process comm emulation error"; }
+
+RcclApi make_fake_api() {
+  RcclApi a;
+  a.lib = (void*)&g_fake_reg;
+  a.getUniqueId = fake_unique_id;
+  a.allGather = fake_all_gather;
+  a.commDestroy = fake_destroy;
+  a.send = fake_send;
+  a.recv = fake_recv;
+  a.groupStart = fake_noop;
+  a.groupEnd = fake_noop;
+  a.getErrorString = fake_error;
+  a.initRankSym = (void*)&fake_init;
+  return a;
+}
+const RcclApi g_fake = make_fake_api();
+
+// the communication API a new group (or id) uses
+int comm_api(const RcclApi** api) {
+  const char* f = getenv("GS_GROUP_FAKE_COMM");
+  if (f && atoi(f) != 0) {
+    *api = &g_fake;
+    return GS_OK;
+  }
+  if (int rc = rccl_load()) return rc;
+  *api = &g_rccl;
+  return GS_OK;
+}
+
 constexpr uint64_t kHdrLag = 4;  // a retune reads the headers of the exchange kHdrLag batches back
 constexpr uint64_t kHdrSlots = 8;  // > kHdrLag: header copies of every retune period stay distinct
 
@@ -1318,6 +1504,7 @@ constexpr uint64_t kHdrSlots = 8;  // > kHdrLag: header copies of every retune p
 
 struct gs_group {
   gs_summary* h = nullptr;
+  const RcclApi* api = nullptr;  // RCCL, or the in-process emulation (GS_GROUP_FAKE_COMM=1, tests)
   void* comm = nullptr;
   int nranks = 1, rank = 0;
   int width = 3;  // int64 per exchange row: {a, b} for CC (16 B), {a, b, parity} for the signed kind
@@ -1350,10 +1537,10 @@ struct gs_group {
 
 namespace {
 
-// fold the other ranks' rows of a gathered exchange on the summary stream, behind
-// its all-gather (event), without host synchronisation
-// On the summary's side stream (the group's apply stream) when possible, so this
-// rank's next own fold does not wait for the remote rows (union commutes).
+// Fold the other ranks' rows of a gathered exchange behind its all-gather (event),
+// without host synchronisation, on the summary's side stream (the group's apply
+// stream) when possible, so this rank's next own fold does not wait for the remote
+// rows (union commutes).
 int group_apply(gs_group* g, int k, uint64_t rows) {
   gs_summary* h = g->h;
   const bool use_side = side_ok(h);
@@ -1392,7 +1579,7 @@ int group_exchange(gs_group* g, uint64_t cap, bool keep_header, bool apply_now) 
   if (int rc = stage(h, g->send[k], cap, g->width)) return rc;
   GS_HIP(hipEventRecord(g->staged[k], h->stream));
   GS_HIP(hipStreamWaitEvent(g->xs, g->staged[k], 0));
-  const int r = g_rccl.allGather(g->send[k], g->recv[k], rows * g->width, kNcclInt64, g->comm, g->xs);
+  const int r = g->api->allGather(g->send[k], g->recv[k], rows * g->width, kNcclInt64, g->comm, g->xs);
   if (r != 0) return rccl_fail("ncclAllGather", r);
   if (keep_header) {  // rank headers (row 0 of each rank's block) -> pinned host memory
     const int slot = (int)(g->b % kHdrSlots);
@@ -1425,8 +1612,9 @@ extern "C" {
 
 int gs_group_unique_id(void* id) {
   if (!id) return fail(GS_ERR_INVALID, "id is null");
-  if (int rc = rccl_load()) return rc;
-  const int r = g_rccl.getUniqueId(id);
+  const RcclApi* api = nullptr;
+  if (int rc = comm_api(&api)) return rc;
+  const int r = api->getUniqueId(id);
   return r ? rccl_fail("ncclGetUniqueId", r) : GS_OK;
 }
 
@@ -1436,13 +1624,15 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   *out = nullptr;
   if (int rc = check(h)) return rc;
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(GS_ERR_INVALID, "bad group shape");
-  if (int rc = rccl_load()) return rc;
+  const RcclApi* api = nullptr;
+  if (int rc = comm_api(&api)) return rc;
   DeviceGuard dg(h->device);
   const bool exchange = batch_edges != 0;  // 0: tree-combine-only group
   if (exchange)
     if (int rc = gs_set_delta_tracking(h, 1)) return rc;
   gs_group* g = new gs_group();
   g->h = h;
+  g->api = api;
   g->nranks = nranks;
   g->rank = rank;
   g->width = h->kind == GS_KIND_SIGNED ? 3 : 2;
@@ -1484,7 +1674,7 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   Id128 uid;
   memcpy(uid.b, id, GS_GROUP_ID_BYTES);
   typedef int (*InitRank)(void**, int, Id128, int);
-  const int r = ((InitRank)g_rccl.initRankSym)(&g->comm, nranks, uid, rank);
+  const int r = ((InitRank)api->initRankSym)(&g->comm, nranks, uid, rank);
   if (r != 0) return bail(rccl_fail("ncclCommInitRank", r));
   *out = g;
   return GS_OK;
@@ -1585,14 +1775,14 @@ int tree_send(gs_group* g, int peer, int64_t* hdr) {
   GS_HIP(hipStreamSynchronize(h->stream));
   const int64_t hv[2] = {(int64_t)got, (int64_t)((failed & 0xff) != 0)};
   GS_HIP(hipMemcpyAsync(hdr, hv, 16, hipMemcpyHostToDevice, h->stream));
-  int r = g_rccl.send(hdr, 2, kNcclInt64, peer, g->comm, h->stream);
+  int r = g->api->send(hdr, 2, kNcclInt64, peer, g->comm, h->stream);
   if (r) return rccl_fail("ncclSend", r);
   if (got) {
-    g_rccl.groupStart();
-    r = g_rccl.send(a.v, got, kNcclInt64, peer, g->comm, h->stream);
-    if (!r) r = g_rccl.send(a.l, got, kNcclInt64, peer, g->comm, h->stream);
-    if (!r) r = g_rccl.send(a.p, got, kNcclUint8, peer, g->comm, h->stream);
-    const int e = g_rccl.groupEnd();
+    g->api->groupStart();
+    r = g->api->send(a.v, got, kNcclInt64, peer, g->comm, h->stream);
+    if (!r) r = g->api->send(a.l, got, kNcclInt64, peer, g->comm, h->stream);
+    if (!r) r = g->api->send(a.p, got, kNcclUint8, peer, g->comm, h->stream);
+    const int e = g->api->groupEnd();
     if (r || e) return rccl_fail("ncclSend", r ? r : e);
   }
   GS_HIP(hipStreamSynchronize(h->stream));  // the arrays are freed on return
@@ -1602,7 +1792,7 @@ int tree_send(gs_group* g, int peer, int64_t* hdr) {
 // one tree edge, receiving side: fold the peer's exported summary into this one
 int tree_recv(gs_group* g, int peer, int64_t* hdr) {
   gs_summary* h = g->h;
-  int r = g_rccl.recv(hdr, 2, kNcclInt64, peer, g->comm, h->stream);
+  int r = g->api->recv(hdr, 2, kNcclInt64, peer, g->comm, h->stream);
   if (r) return rccl_fail("ncclRecv", r);
   int64_t hv[2] = {0, 0};
   GS_HIP(hipMemcpyAsync(hv, hdr, 16, hipMemcpyDeviceToHost, h->stream));
@@ -1611,11 +1801,11 @@ int tree_recv(gs_group* g, int peer, int64_t* hdr) {
   ExportedArrays a;
   if (int rc = a.alloc(got)) return rc;
   if (got) {
-    g_rccl.groupStart();
-    r = g_rccl.recv(a.v, got, kNcclInt64, peer, g->comm, h->stream);
-    if (!r) r = g_rccl.recv(a.l, got, kNcclInt64, peer, g->comm, h->stream);
-    if (!r) r = g_rccl.recv(a.p, got, kNcclUint8, peer, g->comm, h->stream);
-    const int e = g_rccl.groupEnd();
+    g->api->groupStart();
+    r = g->api->recv(a.v, got, kNcclInt64, peer, g->comm, h->stream);
+    if (!r) r = g->api->recv(a.l, got, kNcclInt64, peer, g->comm, h->stream);
+    if (!r) r = g->api->recv(a.p, got, kNcclUint8, peer, g->comm, h->stream);
+    const int e = g->api->groupEnd();
     if (r || e) return rccl_fail("ncclRecv", r ? r : e);
   }
   const bool track = h->track;
@@ -1631,7 +1821,7 @@ int tree_recv(gs_group* g, int peer, int64_t* hdr) {
 
 int gs_group_tree_combine(gs_group_t g) {
   if (!g) return fail(GS_ERR_INVALID, "null group");
-  if (!g_rccl.send || !g_rccl.recv || !g_rccl.groupStart || !g_rccl.groupEnd)
+  if (!g->api || !g->api->send || !g->api->recv || !g->api->groupStart || !g->api->groupEnd)
     return fail(GS_ERR_HIP, "RCCL is missing ncclSend/ncclRecv/ncclGroupStart/ncclGroupEnd");
   gs_summary* h = g->h;
   DeviceGuard dg(h->device);
@@ -1670,7 +1860,7 @@ int gs_group_destroy(gs_group_t g) {
   if (!g) return GS_OK;
   DeviceGuard dg(g->h->device);
   (void)hipStreamSynchronize(g->h->stream);
-  if (g->comm && g_rccl.commDestroy) g_rccl.commDestroy(g->comm);
+  if (g->comm && g->api && g->api->commDestroy) g->api->commDestroy(g->comm);
   if (g->xs) (void)hipStreamSynchronize(g->xs);
   if (g->as) {
     (void)hipStreamSynchronize(g->as);
