@@ -1,4 +1,5 @@
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <map>
@@ -82,23 +83,29 @@ struct gs_summary {
   unsigned long long* rep = nullptr;      // host pointer
   unsigned long long* rep_dev = nullptr;  // its device mapping
   uint64_t rep_seq = 0;
-  static constexpr int kRepEvery = 4;  // unpipelined folds report every 4th launch (one stream: a report is a gap)
-  int rep_skip = 0;
-  uint64_t rep_pending_edges = 0;      // edges of capacity-checked chunks not yet reported
+  static constexpr int kRepEvery = 4;  // each stream reports every 4th capacity-checked chunk (a report costs a launch)
+  static constexpr int kRepStreams = 6;  // handle stream, 4 lanes, side stream
+  int rep_skip[kRepStreams] = {};
+  uint64_t rep_pending[kRepStreams] = {};  // per stream: edges of chunks queued since its last report
+  uint64_t rep_pending_edges = 0;      // sum of rep_pending: edges of capacity-checked chunks not yet reported
   uint64_t e_launched = 0;  // edges of capacity-checked folds since reset / rebuild
   uint64_t nv_exact = 0, e_exact = 0;  // an exact count and the edges complete when it was read
   // lists
   uint2* act = nullptr;
   uint32_t act_shard_cap = 0;
   bool track = false;
-  int64_t* drec = nullptr;  // [kShards][delta_shard_cap][3]
+  // two delta sets, so that a fold can record into one while the previous fold's
+  // set is staged (a group's pipelined exchange); everything else uses set 0
+  int64_t* drec = nullptr;  // [2][kShards][delta_shard_cap][3]
   uint32_t delta_shard_cap = 0;
+  int dset = 0;             // the set folds record into
+  int force_lane = -1;      // >= 0: the next fold goes to this lane (a group's pipelined own fold)
   // exchange record queue (ping-pong): packed records not yet sent
   int64_t* q[2] = {nullptr, nullptr};
   unsigned long long* qn = nullptr;  // [2] device counts
   uint64_t qcap = 0;
   int qsel = 0;
-  uint64_t delta_fill_ub = 0;  // worst-case per-shard fill since the last take
+  uint64_t delta_fill_ub[2] = {0, 0};  // worst-case per-shard fill of each set since its last stage
   // hook policy (DESIGN.md "Kernels"): FUSED hooks in k_fold; DEFER hooks waves
   // with <= inline_max active edges in place and hands the rest to the next
   // k_fold launch (triple-buffered active sets); COMPACT runs k_hook per chunk.
@@ -166,12 +173,14 @@ struct gs_summary {
     t.r0 = (uint32_t)(hotcap + cap);
     return t;
   }
-  gs::Lists lists() const {
+  gs::Lists lists(int set = -1) const {
+    if (set < 0) set = dset;
     gs::Lists L;
     L.act = act;
     L.act_shard_cap = act_shard_cap;
-    L.drec = drec;
+    L.drec = drec ? drec + (size_t)set * gs::kShards * delta_shard_cap * 3 : nullptr;
     L.delta_shard_cap = delta_shard_cap;
+    L.dctr = (uint32_t)(gs::CTR_DELTA + set * gs::kShards);
     return L;
   }
 };
@@ -249,6 +258,11 @@ bool side_ok(const gs_summary* h) {
   return h->side && h->mode == gs_summary::FUSED && h->hotcap == 0 && !h->profiling;
 }
 
+// can a (tracked) fold run on a lane stream of its own (plain fused folds, no profiling)
+bool lane_fold_ok(const gs_summary* h) {
+  return h->pipe_depth >= 2 && h->mode == gs_summary::FUSED && h->hotcap == 0 && !h->profiling;
+}
+
 int join_lanes(gs_summary* h) {
   if (int rc = join_pipe_lanes(h)) return rc;
   if (h->side_dirty) {
@@ -294,7 +308,7 @@ int reset_capacity_tracking(gs_summary* h, uint64_t nv) {
   h->nv_exact = nv;
   h->e_exact = 0;
   h->e_launched = 0;
-  h->rep_skip = 0;
+  for (int i = 0; i < gs_summary::kRepStreams; ++i) h->rep_skip[i] = 0, h->rep_pending[i] = 0;
   h->rep_pending_edges = 0;
   return GS_OK;
 }
@@ -454,7 +468,7 @@ int ensure_capacity(gs_summary* h, size_t n) {
   h->nv_exact = nv;
   h->e_exact = h->e_launched;
   h->rep_pending_edges = 0;  // covered by e_exact (never claimed by a report: ring bounds stay conservative)
-  h->rep_skip = 0;
+  for (int i = 0; i < gs_summary::kRepStreams; ++i) h->rep_skip[i] = 0, h->rep_pending[i] = 0;
   h->nv_ub = nv + 2 * (uint64_t)n;
   if ((double)h->nv_ub > limit) {
     uint64_t nc = h->cap;
@@ -478,11 +492,14 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
   // Pipelined: plain fused folds (no delta tracking, no exchange layout, no hot
   // level, not profiling) may overlap the previous fold. Union is associative and
   // commutative, so the forest after both is the same; readers join the lanes.
-  const bool pipe = allow_pipe && h->pipe_depth > 1 && h->mode == gs_summary::FUSED && !track && xl.rows == 0 &&
-                    h->hotcap == 0 && !h->profiling;
+  // A group's own tracked fold may be forced onto a lane (h->force_lane): it records
+  // into its own delta set, staged on the same lane, so the next fold overlaps it.
+  const bool forced = h->force_lane >= 0 && xl.rows == 0 && lane_fold_ok(h);
+  const bool pipe = forced || (allow_pipe && h->pipe_depth > 1 && h->mode == gs_summary::FUSED && !track &&
+                               xl.rows == 0 && h->hotcap == 0 && !h->profiling);
   // remote rows of a group exchange: on the side stream, overlapping own folds
   const bool side = xl.on_side && side_ok(h) && !track;
-  if (!pipe) {
+  if (!pipe && !side) {
     if (int rc = join_pipe_lanes(h)) return rc;  // the side stream is NOT joined: union commutes
   }
   const bool sign = h->kind == GS_KIND_SIGNED;
@@ -492,8 +509,8 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     const uint32_t blocks = (c + per_block - 1) / per_block;
     const uint32_t per_shard_edges = ((blocks + gs::kShards - 1) / gs::kShards) * per_block;
     if (track) {
-      h->delta_fill_ub += (uint64_t)per_shard_edges * 3;
-      if (h->delta_fill_ub > h->delta_shard_cap)
+      h->delta_fill_ub[h->dset] += (uint64_t)per_shard_edges * 3;
+      if (h->delta_fill_ub[h->dset] > h->delta_shard_cap)
         return fail(GS_ERR_CAPACITY, "delta list full: call gs_take_delta_records after each fold of <= 2^22 edges");
     }
     const int cur = (int)(h->epoch % gs::kActSets);
@@ -510,8 +527,12 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     if (side) h->side_dirty = true;
     if (pipe) {  // the lane waits for the caller's work on the handle stream, not for the other lane
       GS_HIP(hipEventRecord(h->main_ev, h->stream));
-      st = h->lane[h->lane_next];
-      h->lane_next = (h->lane_next + 1) % h->pipe_depth;
+      if (forced) {
+        st = h->lane[h->force_lane];
+      } else {
+        st = h->lane[h->lane_next];
+        h->lane_next = (h->lane_next + 1) % h->pipe_depth;
+      }
       GS_HIP(hipStreamWaitEvent(st, h->main_ev, 0));
       h->lanes_dirty = true;
     }
@@ -523,25 +544,27 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     }
     GS_HIP(hipGetLastError());
     if (check_cap) {
-      // A report may only claim chunks queued before it on ITS stream. Lanes and the
-      // side stream report every chunk (off the critical path); on the handle's own
-      // stream a report is a gap between folds, so it reports every kRepEvery-th
-      // chunk, claiming the chunks since its previous report. Unclaimed edges stay
+      // A report may only claim chunks queued before it on ITS stream. Every stream
+      // (handle, lanes, side) reports every kRepEvery-th chunk queued on it, claiming
+      // that stream's chunks since its previous report: a report is a launch, and
+      // host launch cost bounds the multi-GPU exchange loop. Unclaimed edges stay
       // "in flight" in the bound, which is therefore always valid.
-      uint64_t claim = c;
-      bool report = true;
-      if (st == h->stream) {
-        h->rep_pending_edges += c;
-        claim = h->rep_pending_edges;
-        report = ++h->rep_skip >= gs_summary::kRepEvery;
-      }
-      if (report) {
+      int rs = 0;
+      if (st == h->side) rs = gs_summary::kRepStreams - 1;
+      for (int i = 0; i < gs_summary::kLanes; ++i)
+        if (st == h->lane[i]) rs = 1 + i;
+      h->rep_pending[rs] += c;
+      h->rep_pending_edges += c;
+      // off the handle stream a report is not a gap between folds: report every chunk
+      // while the bound is near the load limit (small tables), so no fold has to wait
+      const bool tight = rs != 0 && (double)(h->nv_ub + 4ull * gs_summary::kRepEvery * c) > kMaxLoad * (double)h->cap;
+      if (++h->rep_skip[rs] >= gs_summary::kRepEvery || tight) {
+        const uint64_t claim = h->rep_pending[rs];
         gs::launch_report(h->ctr, claim, h->rep_dev + (h->rep_seq++ % gs_summary::kRepRing), st);
         GS_HIP(hipGetLastError());
-        if (st == h->stream) {
-          h->rep_pending_edges = 0;
-          h->rep_skip = 0;
-        }
+        h->rep_pending_edges -= claim;
+        h->rep_pending[rs] = 0;
+        h->rep_skip[rs] = 0;
       }
     }
     if (h->hot_open && !h->nv_pending) {  // vertex count for the next hot-level decision
@@ -707,7 +730,7 @@ int gs_reset(gs_handle h) {
   if (int rc = reset_capacity_tracking(h, 0)) return rc;
   h->epoch = 0;
   h->pending = -1;
-  h->delta_fill_ub = 0;
+  h->delta_fill_ub[0] = h->delta_fill_ub[1] = 0;
   return GS_OK;
 }
 
@@ -1020,11 +1043,12 @@ int gs_set_delta_tracking(gs_handle h, int on) {
     // worst case between two takes: one fold chunk of kMaxChunk edges
     h->delta_shard_cap = ((kMaxChunk / 256 + gs::kShards - 1) / gs::kShards) * 256 * 3;
     const size_t m = (size_t)gs::kShards * h->delta_shard_cap;
-    GS_HIP(hipMalloc(&h->drec, m * 24));
+    GS_HIP(hipMalloc(&h->drec, 2 * m * 24));
   }
-  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, gs::kShards * gs::kCtrStride * 4, h->stream));
+  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, 2 * gs::kShards * gs::kCtrStride * 4, h->stream));
   if (h->qn) GS_HIP(hipMemsetAsync(h->qn, 0, 16, h->stream));
-  h->delta_fill_ub = 0;
+  h->delta_fill_ub[0] = h->delta_fill_ub[1] = 0;
+  h->dset = 0;
   h->track = on != 0;
   return GS_OK;
 }
@@ -1040,16 +1064,17 @@ static int ensure_queue(gs_summary* h) {
   return GS_OK;
 }
 
-// backlog q[qsel] + fresh delta -> send rows (first cap) and q[qsel ^ 1] (the rest)
-static int stage(gs_summary* h, int64_t* send, uint64_t cap, int width = 3) {
+// backlog q[qsel] + delta set `set` -> send rows (first cap) and q[qsel ^ 1] (the
+// rest), on stream st (default: the handle's stream). Stages must run in queue order.
+static int stage(gs_summary* h, int64_t* send, uint64_t cap, int width = 3, hipStream_t st = nullptr, int set = 0) {
   if (int rc = flush_hooks(h)) return rc;
   if (int rc = ensure_queue(h)) return rc;
   const int a = h->qsel, b = h->qsel ^ 1;
-  gs::launch_stage(h->table(), h->lists(), h->q[a], h->qn + a, h->q[b], h->qn + b, h->qcap, send, cap, h->stream,
-                   nullptr, width);
+  gs::launch_stage(h->table(), h->lists(set), h->q[a], h->qn + a, h->q[b], h->qn + b, h->qcap, send, cap,
+                   st ? st : h->stream, nullptr, width);
   GS_HIP(hipGetLastError());
   h->qsel = b;
-  h->delta_fill_ub = 0;
+  h->delta_fill_ub[set] = 0;
   return GS_OK;
 }
 
@@ -1063,11 +1088,11 @@ int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count
   if (int rc = flush_hooks(h)) return rc;
   if (int rc = ensure_queue(h)) return rc;
   const int a = h->qsel, b = h->qsel ^ 1;
-  gs::launch_stage(h->table(), h->lists(), h->q[a], h->qn + a, h->q[b], h->qn + b, h->qcap, rec, cap, h->stream,
+  gs::launch_stage(h->table(), h->lists(0), h->q[a], h->qn + a, h->q[b], h->qn + b, h->qcap, rec, cap, h->stream,
                    reinterpret_cast<unsigned long long*>(count));
   GS_HIP(hipGetLastError());
   h->qsel = b;
-  h->delta_fill_ub = 0;
+  h->delta_fill_ub[0] = 0;
   return GS_OK;
 }
 
@@ -1524,7 +1549,8 @@ struct gs_group {
   hipEvent_t as_ev = nullptr;
   // rank headers of kept exchanges, a ring of kHdrSlots: slot b % kHdrSlots holds
   // the headers of exchange hdr_batch[slot] once hdr_ev[slot] has completed
-  int64_t* hdr_host = nullptr;  // pinned [kHdrSlots][nranks * 3]
+  int64_t* hdr_host = nullptr;  // pinned, host-mapped [kHdrSlots][nranks * 3]
+  long long* hdr_dev = nullptr;  // its device mapping (k_headers writes it)
   hipEvent_t hdr_ev[kHdrSlots] = {};
   int64_t hdr_batch[kHdrSlots] = {-1, -1, -1, -1, -1, -1, -1, -1};
   uint64_t b = 0;            // exchanges since create / finish
@@ -1533,7 +1559,35 @@ struct gs_group {
   uint64_t last_rows = 0;    // rows per rank of the last exchange
   int last_k = 0;            // its buffer
   uint64_t exchanges = 0;
+  // pipelined own folds: exchange b's fold AND stage run on lane b % 2 of the summary,
+  // recording into delta set b % 2, so fold b + 1 (other lane, other set) overlaps
+  // fold b and stage b; stages stay in order through the staged[] events
+  bool lanes = false;        // decided per exchange (lane_fold_ok)
+  // GS_GROUP_LANES=1 enables the lane pipeline. Off by default: measured slower at one
+  // rank
+  bool no_lanes = true;
+  // GS_GROUP_HOSTPROF=1: host seconds per phase of the exchange loop, printed at destroy
+  bool hostprof = false;
+  double hp[6] = {};  // retune, own fold, stage+events, collective, headers, remote fold
+  uint64_t hp_calls = 0;
+  double cap_sum = 0;
 };
+
+namespace {
+struct HostTimer {
+  double* acc;
+  std::chrono::steady_clock::time_point t0;
+  explicit HostTimer(double* a) : acc(a), t0(a ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point()) {}
+  void lap(double* next) {  // charge the time so far to acc, continue on next
+    if (!acc) return;
+    const auto t = std::chrono::steady_clock::now();
+    *acc += std::chrono::duration<double>(t - t0).count();
+    t0 = t;
+    acc = next;
+  }
+  ~HostTimer() { lap(nullptr); }
+};
+}  // namespace
 
 namespace {
 
@@ -1568,27 +1622,37 @@ int group_exchange(gs_group* g, uint64_t cap, bool keep_header, bool apply_now) 
   gs_summary* h = g->h;
   const uint64_t rows = cap + 1;
   const int k = (int)(g->b & 1u);
+  HostTimer ht(g->hostprof ? &g->hp[2] : nullptr);
+  // the stage runs where this exchange's own fold ran (lane k, delta set k), or on
+  // the handle's stream (set 0) when folds cannot run on lanes
+  hipStream_t ss = g->lanes ? h->lane[k] : h->stream;
   if (g->used[k]) {
     // buffer k last served exchange b - 2: its all-gather must have read send[k]
     // before this stage rewrites it, and its rows must have been folded before this
     // all-gather rewrites recv[k] (both long done in steady state)
-    GS_HIP(hipStreamWaitEvent(h->stream, g->gathered[k], 0));
+    GS_HIP(hipStreamWaitEvent(ss, g->gathered[k], 0));
     GS_HIP(hipStreamWaitEvent(g->xs, g->applied[k], 0));
   }
+  // stages consume the backlog queue in order: behind the previous exchange's stage
+  if (g->used[k ^ 1]) GS_HIP(hipStreamWaitEvent(ss, g->staged[k ^ 1], 0));
   g->used[k] = true;
-  if (int rc = stage(h, g->send[k], cap, g->width)) return rc;
-  GS_HIP(hipEventRecord(g->staged[k], h->stream));
+  if (int rc = stage(h, g->send[k], cap, g->width, ss, g->lanes ? k : 0)) return rc;
+  GS_HIP(hipEventRecord(g->staged[k], ss));
+  if (g->lanes) h->lanes_dirty = true;
   GS_HIP(hipStreamWaitEvent(g->xs, g->staged[k], 0));
+  ht.lap(g->hostprof ? &g->hp[3] : nullptr);
   const int r = g->api->allGather(g->send[k], g->recv[k], rows * g->width, kNcclInt64, g->comm, g->xs);
   if (r != 0) return rccl_fail("ncclAllGather", r);
+  ht.lap(g->hostprof ? &g->hp[4] : nullptr);
   if (keep_header) {  // rank headers (row 0 of each rank's block) -> pinned host memory
     const int slot = (int)(g->b % kHdrSlots);
-    GS_HIP(hipMemcpy2DAsync(g->hdr_host + (size_t)slot * g->nranks * 3, 24, g->recv[k], rows * 8 * g->width, 16,
-                            g->nranks, hipMemcpyDeviceToHost, g->xs));
+    gs::launch_headers(g->recv[k], rows * g->width, g->nranks, g->hdr_dev + (size_t)slot * g->nranks * 3, g->xs);
+    GS_HIP(hipGetLastError());
     GS_HIP(hipEventRecord(g->hdr_ev[slot], g->xs));
     g->hdr_batch[slot] = (int64_t)g->b;
   }
   GS_HIP(hipEventRecord(g->gathered[k], g->xs));
+  ht.lap(g->hostprof ? &g->hp[5] : nullptr);
   if (g->pend >= 0) {
     if (int rc = group_apply(g, g->pend, g->pend_rows)) return rc;
     g->pend = -1;
@@ -1641,13 +1705,17 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   g->cap = g->first_cap;
   if (const char* m = getenv("GS_GROUP_RETUNE")) g->retune = std::max(1, atoi(m));
   if (const char* m = getenv("GS_GROUP_SELF_APPLY")) g->self_apply = atoi(m) != 0;
+  if (const char* m = getenv("GS_GROUP_LANES")) g->no_lanes = atoi(m) == 0;  // default: off
+  if (const char* m = getenv("GS_GROUP_HOSTPROF")) g->hostprof = atoi(m) != 0;
   auto bail = [&](int code) {
     gs_group_destroy(g);
     return code;
   };
   const size_t rows = g->max_cap + 1;
   if (exchange) {
-    bool ok = hipHostMalloc(&g->hdr_host, (size_t)kHdrSlots * nranks * 24, hipHostMallocDefault) == hipSuccess &&
+    bool ok = hipHostMalloc(&g->hdr_host, (size_t)kHdrSlots * nranks * 24, hipHostMallocMapped | hipHostMallocCoherent) ==
+                  hipSuccess &&
+              hipHostGetDevicePointer(reinterpret_cast<void**>(&g->hdr_dev), g->hdr_host, 0) == hipSuccess &&
               hipStreamCreateWithFlags(&g->xs, hipStreamNonBlocking) == hipSuccess;
     for (int k = 0; k < (int)kHdrSlots && ok; ++k)
       ok = hipEventCreateWithFlags(&g->hdr_ev[k], hipEventDisableTiming) == hipSuccess;
@@ -1658,6 +1726,8 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
            hipEventCreateWithFlags(&g->gathered[k], hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&g->applied[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) return bail(fail(GS_ERR_HIP, "group buffer allocation failed"));
+    if (int rc = join_lanes(h)) return bail(rc);
+    if (h->pipe_depth < 2) h->pipe_depth = 2;  // own folds alternate over lanes 0 and 1
     // GS_GROUP_SIDE=0: fold remote rows on the summary stream (no overlap)
     const char* sv = getenv("GS_GROUP_SIDE");
     if (!(sv && atoi(sv) == 0)) {
@@ -1687,6 +1757,8 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   if (!g->send[0]) return fail(GS_ERR_INVALID, "tree-combine-only group (created with batch_edges 0)");
   if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
   const uint64_t b = g->b;
+  g->hp_calls++;
+  HostTimer ht(g->hostprof ? &g->hp[0] : nullptr);
   // every `retune` exchanges all ranks re-derive the capacity from the same headers:
   // those of exchange b - kHdrLag, read BEFORE this exchange may copy its own
   const int lag_slot = (int)((b - kHdrLag) % kHdrSlots);
@@ -1697,7 +1769,20 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
     for (int r = 0; r < g->nranks; ++r) queued = std::max(queued, hh[r * 3 + 1]);
     g->cap = std::min<uint64_t>(g->max_cap, std::max<uint64_t>(4096, (uint64_t)queued + (uint64_t)queued / 4 + 1024));
   }
-  if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, /*track=*/true)) return rc;
+  // own fold: with GS_GROUP_LANES=1, on lane b % 2 into delta set b % 2 when possible
+  // (overlaps the previous exchange's fold and stage); default: the handle's stream
+  ht.lap(g->hostprof ? &g->hp[1] : nullptr);
+  g->lanes = lane_fold_ok(h) && !g->no_lanes;
+  if (g->lanes) {
+    h->force_lane = (int)(b & 1u);
+    h->dset = (int)(b & 1u);
+  }
+  const int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, /*track=*/true);
+  h->force_lane = -1;
+  h->dset = 0;
+  if (rc) return rc;
+  ht.lap(nullptr);
+  g->cap_sum += (double)g->cap;
   const bool keep = (b + kHdrLag) % g->retune == 0;
   return group_exchange(g, g->cap, keep, /*apply_now=*/false);
 }
@@ -1727,6 +1812,7 @@ int gs_group_finish(gs_group_t g) {
     int64_t remaining = 0;
     for (int r = 0; r < g->nranks; ++r) remaining = std::max(remaining, g->hdr_host[r * 3 + 1] - g->hdr_host[r * 3]);
     if (remaining <= 0) break;
+    g->lanes = lane_fold_ok(h) && !g->no_lanes;
     if (int rc = group_exchange(g, std::min<uint64_t>((uint64_t)remaining, g->max_cap), false, /*apply_now=*/true))
       return rc;
   }
@@ -1858,6 +1944,12 @@ int gs_group_stats(gs_group_t g, uint64_t* exchanges, uint64_t* records_sent, ui
 
 int gs_group_destroy(gs_group_t g) {
   if (!g) return GS_OK;
+  if (g->hostprof && g->hp_calls) {
+    const char* nm[6] = {"retune", "own fold", "stage+events", "collective", "headers", "remote fold"};
+    fprintf(stderr, "[gs_group rank %d] host us per batch over %llu batches:", g->rank, (unsigned long long)g->hp_calls);
+    for (int i = 0; i < 6; ++i) fprintf(stderr, " %s %.1f", nm[i], g->hp[i] * 1e6 / (double)g->hp_calls);
+    fprintf(stderr, "; mean cap %.0f rows\n", g->cap_sum / (double)g->hp_calls);
+  }
   DeviceGuard dg(g->h->device);
   (void)hipStreamSynchronize(g->h->stream);
   if (g->comm && g->api && g->api->commDestroy) g->api->commDestroy(g->comm);

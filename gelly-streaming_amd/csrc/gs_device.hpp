@@ -49,8 +49,8 @@ constexpr int kActSets = 3;     // active-edge lists: appended at epoch e, drain
 enum CounterBlock : int {
   CTR_NV = 0,                    // [kShards] new-vertex counts
   CTR_ACT = kShards,             // [kActSets][kShards] active-edge counts
-  CTR_DELTA = (1 + kActSets) * kShards,  // [kShards] delta counts
-  CTR_FAIL = (2 + kActSets) * kShards,   // sticky bipartiteness failure
+  CTR_DELTA = (1 + kActSets) * kShards,  // [2][kShards] delta counts (two delta sets)
+  CTR_FAIL = (3 + kActSets) * kShards,   // sticky bipartiteness failure
   CTR_ERR,                       // device-side error (table overflow)
   CTR_EXPORT,                    // export append counter
   CTR_OVF,                       // delta / active list overflow
@@ -106,8 +106,9 @@ struct Table {
 struct Lists {
   uint2* act;            // active (root<<1|parity, root) entries, [kActSets][kShards][act_shard_cap]
   uint32_t act_shard_cap;
-  int64_t* drec;         // delta records {a, b, parity}, [kShards][delta_shard_cap][3]
+  int64_t* drec;         // delta records {a, b, parity} of this set, [kShards][delta_shard_cap][3]
   uint32_t delta_shard_cap;
+  uint32_t dctr;         // counter index of this set's shard 0 (CTR_DELTA + set * kShards)
 };
 
 __device__ __forceinline__ uint32_t hash_slot(int64_t key, int shift) {
@@ -448,7 +449,7 @@ __device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, 
     const uint32_t old = seen == expect ? atomicCAS(&t.tab[hi].link, expect, desired) : seen;
     if (old == expect) {
       if (TRACK) {
-        const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_DELTA + shard)], 1u);
+        const uint32_t pos = atomicAdd(&t.ctr[ctr_index(L.dctr + shard)], 1u);
         if (pos < L.delta_shard_cap) {
           int64_t* r = L.drec + ((size_t)shard * L.delta_shard_cap + pos) * 3;
           r[0] = a_lo ? kb : ka;

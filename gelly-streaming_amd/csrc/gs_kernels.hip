@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Lists L, FoldArgs a) 
     // change through a CAS on it or onto it), so only a new vertex seen through a
     // self-loop needs a record of its own.
     if (TRACK && nu && su == sv) {
-      const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_DELTA + shard)], 1u);
+      const uint32_t pos = atomicAdd(&t.ctr[ctr_index(L.dctr + shard)], 1u);
       if (pos < L.delta_shard_cap) {
         int64_t* r = L.drec + ((size_t)shard * L.delta_shard_cap + pos) * 3;
         r[0] = ks[e];
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* 
   __shared__ uint64_t off_sh, total_sh;
   const uint32_t s = blockIdx.x;
   const uint64_t backlog = min((unsigned long long)*qn_in, (unsigned long long)qcap);
-  if (threadIdx.x < kShards) cnt[threadIdx.x] = min(t.ctr[ctr_index(CTR_DELTA + threadIdx.x)], L.delta_shard_cap);
+  if (threadIdx.x < kShards) cnt[threadIdx.x] = min(t.ctr[ctr_index(L.dctr + threadIdx.x)], L.delta_shard_cap);
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t off = backlog, tot = backlog;
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Lists L, const int64_t* 
   if (threadIdx.x == 0) last = atomicAdd(&t.ctr[ctr_index(CTR_STAGE_DONE)], 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  if (threadIdx.x < kShards) t.ctr[ctr_index(CTR_DELTA + threadIdx.x)] = 0u;
+  if (threadIdx.x < kShards) t.ctr[ctr_index(L.dctr + threadIdx.x)] = 0u;
   if (threadIdx.x == 0) {
     *qn_in = 0ull;
     atomicExch(&t.ctr[ctr_index(CTR_STAGE_DONE)], 0u);
@@ -542,6 +542,23 @@ void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned 
                   unsigned long long* count_out, int width) {
   hipLaunchKernelGGL(k_stage, dim3(kShards), dim3(256), 0, st, t, L, q_in, qn_in, q_out, qn_out, qcap, send, cap,
                      count_out, width);
+}
+
+// Exchange headers -> host-mapped memory: row 0 ({sent, queued}) of every rank's block
+// of a gathered exchange buffer, one thread per rank, system-scope stores. Replaces a
+// 2-D device-to-host copy whose host-side cost (~110 us per call) bounded the
+// exchange loop.
+__global__ __launch_bounds__(64) void k_headers(const int64_t* __restrict__ recv, uint64_t rank_stride, int nranks,
+                                                long long* out) {
+  for (int r = threadIdx.x; r < nranks; r += 64) {
+    const int64_t* hd = recv + (size_t)r * rank_stride;
+    __hip_atomic_store(out + r * 3, (long long)hd[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(out + r * 3 + 1, (long long)hd[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+void launch_headers(const int64_t* recv, uint64_t rank_stride, int nranks, long long* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_headers, dim3(1), dim3(64), 0, st, recv, (unsigned long long)rank_stride, nranks, out);
 }
 
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st) {

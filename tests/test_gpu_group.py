@@ -8,14 +8,16 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("first_cap,self_apply", [(0, 0), (64, 0), (64, 1)])
-def test_group_single_rank_matches_oracle(gs, oracle_mod, monkeypatch, first_cap, self_apply):
+@pytest.mark.parametrize("first_cap,self_apply,lanes", [(0, 0, "0"), (64, 0, "0"), (64, 1, "0"), (0, 0, "1"),
+                                                        (64, 1, "1")])
+def test_group_single_rank_matches_oracle(gs, oracle_mod, monkeypatch, first_cap, self_apply, lanes):
     """self_apply: the rank also folds its own gathered rows (16-B CC rows, exchange
     layout, lagged apply) -- the remote-fold path, exercised at one rank; folding a
     delta twice is idempotent, so any mis-parsed row would show in the labels."""
     import torch
     monkeypatch.setenv("GS_GROUP_RETUNE", "2")
     monkeypatch.setenv("GS_GROUP_SELF_APPLY", str(self_apply))
+    monkeypatch.setenv("GS_GROUP_LANES", lanes)
     n, B = 1 << 17, 1 << 13
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")

@@ -33,10 +33,14 @@ def _run_ranks(world, body):
     return out
 
 
+@pytest.mark.parametrize("lanes", ["0", "1"])
 @pytest.mark.parametrize("world,first_cap,retune", [(2, 0, "4"), (3, 256, "2"), (4, 64, "1")])
-def test_delta_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, world, first_cap, retune):
+def test_delta_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, world, first_cap, retune, lanes):
+    """lanes=1: each rank's own tracked folds alternate over two lane streams and two
+    delta sets (GS_GROUP_LANES), the stage of exchange b on fold b's lane."""
     import torch
     monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
+    monkeypatch.setenv("GS_GROUP_LANES", lanes)
     monkeypatch.setenv("GS_GROUP_RETUNE", retune)
     scale, n, B = 14, 1 << 18, 1 << 12
     src = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -71,10 +75,12 @@ def test_delta_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, world, first
     assert parts == sorted(zip(ov.tolist(), olab.tolist()))
 
 
+@pytest.mark.parametrize("lanes", ["0", "1"])
 @pytest.mark.parametrize("inject", [(), (1 << 15,)])
-def test_signed_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, inject):
+def test_signed_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, inject, lanes):
     import torch
     monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
+    monkeypatch.setenv("GS_GROUP_LANES", lanes)
     monkeypatch.setenv("GS_GROUP_RETUNE", "2")
     world, n, B = 3, 3 << 15, 1 << 12
     src = torch.empty(n, dtype=torch.int64, device="cuda")

@@ -59,6 +59,7 @@ int main(int argc, char** argv) {
   gs::Lists L{};
   L.act = act;
   L.act_shard_cap = act_cap;
+  L.dctr = gs::CTR_DELTA;
   const uint32_t nw = B / 64;
   std::vector<uint64_t> w(2 * nw);
   std::vector<uint32_t> m(nw);
