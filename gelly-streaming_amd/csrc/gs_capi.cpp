@@ -1646,7 +1646,8 @@ int group_exchange(gs_group* g, uint64_t cap, bool keep_header, bool apply_now) 
   ht.lap(g->hostprof ? &g->hp[4] : nullptr);
   if (keep_header) {  // rank headers (row 0 of each rank's block) -> pinned host memory
     const int slot = (int)(g->b % kHdrSlots);
-    gs::launch_headers(g->recv[k], rows * g->width, g->nranks, g->hdr_dev + (size_t)slot * g->nranks * 3, g->xs);
+    gs::launch_headers(g->recv[k], rows * g->width, g->nranks, g->hdr_dev + (size_t)slot * g->nranks * 3,
+                       (long long)g->b, g->xs);
     GS_HIP(hipGetLastError());
     GS_HIP(hipEventRecord(g->hdr_ev[slot], g->xs));
     g->hdr_batch[slot] = (int64_t)g->b;
@@ -1726,6 +1727,7 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
            hipEventCreateWithFlags(&g->gathered[k], hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&g->applied[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) return bail(fail(GS_ERR_HIP, "group buffer allocation failed"));
+    for (int k = 0; k < (int)kHdrSlots; ++k) g->hdr_host[(size_t)k * nranks * 3 + 2] = -1;  // no exchange yet
     if (int rc = join_lanes(h)) return bail(rc);
     if (h->pipe_depth < 2) h->pipe_depth = 2;  // own folds alternate over lanes 0 and 1
     // GS_GROUP_SIDE=0: fold remote rows on the summary stream (no overlap)
@@ -1763,8 +1765,18 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   // those of exchange b - kHdrLag, read BEFORE this exchange may copy its own
   const int lag_slot = (int)((b - kHdrLag) % kHdrSlots);
   if (b % g->retune == 0 && b >= kHdrLag && g->hdr_batch[lag_slot] == (int64_t)(b - kHdrLag)) {
-    GS_HIP(hipEventSynchronize(g->hdr_ev[lag_slot]));
+    // k_headers writes the exchange number into word 2 of the slot after the headers:
+    // poll it (an event synchronisation costs ~40 us of host time even when complete)
     const int64_t* hh = g->hdr_host + (size_t)lag_slot * g->nranks * 3;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(&hh[2], __ATOMIC_ACQUIRE) != (int64_t)(b - kHdrLag)) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+        GS_HIP(hipEventSynchronize(g->hdr_ev[lag_slot]));  // long wait: block instead of spinning
+        if (__atomic_load_n(&hh[2], __ATOMIC_ACQUIRE) != (int64_t)(b - kHdrLag))
+          return fail(GS_ERR_HIP, "exchange header sequence mismatch");
+        break;
+      }
+    }
     int64_t queued = 0;
     for (int r = 0; r < g->nranks; ++r) queued = std::max(queued, hh[r * 3 + 1]);
     g->cap = std::min<uint64_t>(g->max_cap, std::max<uint64_t>(4096, (uint64_t)queued + (uint64_t)queued / 4 + 1024));
@@ -1821,7 +1833,10 @@ int gs_group_finish(gs_group_t g) {
   g->b = 0;
   g->used[0] = g->used[1] = false;
   g->last_rows = 0;
-  for (int k = 0; k < (int)kHdrSlots; ++k) g->hdr_batch[k] = -1;
+  for (int k = 0; k < (int)kHdrSlots; ++k) {
+    g->hdr_batch[k] = -1;
+    __atomic_store_n(&g->hdr_host[(size_t)k * g->nranks * 3 + 2], (int64_t)-1, __ATOMIC_RELEASE);
+  }
   g->cap = g->first_cap;
   return GS_OK;
 }

@@ -547,18 +547,25 @@ void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned 
 // Exchange headers -> host-mapped memory: row 0 ({sent, queued}) of every rank's block
 // of a gathered exchange buffer, one thread per rank, system-scope stores. Replaces a
 // 2-D device-to-host copy whose host-side cost (~110 us per call) bounded the
-// exchange loop.
+// exchange loop. Then out[2] = seq (release): the host polls that word instead of
+// synchronising on an event.
 __global__ __launch_bounds__(64) void k_headers(const int64_t* __restrict__ recv, uint64_t rank_stride, int nranks,
-                                                long long* out) {
+                                                long long* out, long long seq) {
   for (int r = threadIdx.x; r < nranks; r += 64) {
     const int64_t* hd = recv + (size_t)r * rank_stride;
     __hip_atomic_store(out + r * 3, (long long)hd[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(out + r * 3 + 1, (long long)hd[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(out + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
-void launch_headers(const int64_t* recv, uint64_t rank_stride, int nranks, long long* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_headers, dim3(1), dim3(64), 0, st, recv, (unsigned long long)rank_stride, nranks, out);
+void launch_headers(const int64_t* recv, uint64_t rank_stride, int nranks, long long* out, long long seq,
+                    hipStream_t st) {
+  hipLaunchKernelGGL(k_headers, dim3(1), dim3(64), 0, st, recv, (unsigned long long)rank_stride, nranks, out, seq);
 }
 
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st) {

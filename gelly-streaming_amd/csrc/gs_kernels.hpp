@@ -23,7 +23,8 @@ void launch_stage(const Table& t, const Lists& L, const int64_t* q_in, unsigned 
                   unsigned long long* qn_out, uint64_t qcap, int64_t* send, uint64_t cap, hipStream_t st,
                   unsigned long long* count_out = nullptr, int width = 3);
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st);
-void launch_headers(const int64_t* recv, uint64_t rank_stride, int nranks, long long* out, hipStream_t st);
+void launch_headers(const int64_t* recv, uint64_t rank_stride, int nranks, long long* out, long long seq,
+                    hipStream_t st);
 void launch_report(uint32_t* ctr, uint64_t n, unsigned long long* out, hipStream_t st);
 
 }  // namespace gs
