@@ -1675,6 +1675,17 @@ int group_exchange(gs_group* g, uint64_t cap, bool keep_header, bool apply_now) 
 
 extern "C" {
 
+// The communication stream gets the device's highest priority (GS_GROUP_XS_PRIO=0:
+// normal): the collective's kernel (or copy) would otherwise wait for back-to-back
+// fold launches to release CUs, and every later stage waits on it.
+static hipError_t create_comm_stream(hipStream_t* st) {
+  const char* e = getenv("GS_GROUP_XS_PRIO");
+  int least = 0, greatest = 0;
+  if ((e && atoi(e) == 0) || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+    return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+  return hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest);
+}
+
 int gs_group_unique_id(void* id) {
   if (!id) return fail(GS_ERR_INVALID, "id is null");
   const RcclApi* api = nullptr;
@@ -1717,7 +1728,7 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
     bool ok = hipHostMalloc(&g->hdr_host, (size_t)kHdrSlots * nranks * 24, hipHostMallocMapped | hipHostMallocCoherent) ==
                   hipSuccess &&
               hipHostGetDevicePointer(reinterpret_cast<void**>(&g->hdr_dev), g->hdr_host, 0) == hipSuccess &&
-              hipStreamCreateWithFlags(&g->xs, hipStreamNonBlocking) == hipSuccess;
+              create_comm_stream(&g->xs) == hipSuccess;
     for (int k = 0; k < (int)kHdrSlots && ok; ++k)
       ok = hipEventCreateWithFlags(&g->hdr_ev[k], hipEventDisableTiming) == hipSuccess;
     for (int k = 0; k < 2 && ok; ++k)
