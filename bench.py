@@ -75,55 +75,125 @@ def bench_bip(args):
     """BASELINE config 4: random bipartite stream, sides of 2^19 vertices, E = 2^24, 2^20-edge
     windows, signed (parity) union-find. Throughput on the clean stream (nothing skipped: a failed
     verdict would short-circuit the fold); verdict check on the odd-cycle variant (edges injected at
-    E/8, E/4, E/2, 3E/4): the verdict must flip in the window of the first conflicting edge."""
+    E/8, E/4, E/2, 3E/4): at one GPU the verdict must flip in the window of the first conflicting
+    edge; at N GPUs (config 4 at G = 8: one process per GPU, each rank its contiguous 1/N shard,
+    signed 24-B delta rows exchanged per global micro-batch through the native group) every
+    replica's final verdict must equal the truth (the remote half of a window lands one exchange
+    late, so a per-window flip is only defined at one GPU)."""
     import gsamd as gs
-    dev = torch.device("cuda", 0)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    grouped = world > 1 or args.exchange
+    if grouped:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29534")
+            dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     logside, E, B, seed = 19, 1 << 24, 1 << 20, 0x5EED0B1B
-    summ = gs.Summary("signed", device=0, capacity_hint=1 << 20)
-    src = torch.empty(E, dtype=torch.int64, device=dev)
-    dst = torch.empty(E, dtype=torch.int64, device=dev)
-    gs.gen_bip(src, dst, 0, E, logside, seed, [], stream=summ.stream)
+    per = E // world
+    start = rank * per
+    summ = gs.Summary("signed", device=local, capacity_hint=1 << 20)
+    src = torch.empty(per, dtype=torch.int64, device=dev)
+    dst = torch.empty(per, dtype=torch.int64, device=dev)
+    gs.gen_bip(src, dst, start, per, logside, seed, [], stream=summ.stream)
     summ.sync()
-    if args.pipeline > 1:
+    group = None
+    if grouped:
+        uid = [gs.group_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        group = gs.Group(summ, uid[0], world, rank, B)
+    elif args.pipeline > 1:
         summ.set_pipelining(args.pipeline)
     ok = [True]
 
     def one_step():
         summ.reset()
-        for o in range(0, E, B):
-            summ.fold_device(src[o:], dst[o:], n=min(B, E - o))
+        if group is not None:
+            group.fold_batches(src, dst, per, B)
+            group.finish()
+        else:
+            for o in range(0, per, B):
+                summ.fold_device(src[o:], dst[o:], n=min(B, per - o))
         ok[0] = summ.ok()  # the verdict read joins every pending fold
+
+    def barrier():
+        summ.sync()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
 
     for _ in range(args.warmup):
         one_step()
-    summ.sync()
+    barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
-    summ.sync()
+    barrier()
     el = time.perf_counter() - t0
-    # odd-cycle variant: verdict per window against the parity union-find truth
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    # odd-cycle variant (outside the timed region)
     inject = [E // 8, E // 4, E // 2, 3 * E // 4]
-    gs.gen_bip(src, dst, 0, E, logside, seed, inject, stream=summ.stream)
+    gs.gen_bip(src, dst, start, per, logside, seed, [i for i in inject if start <= i < start + per],
+               stream=summ.stream)
     summ.reset()
     flip = None
-    for o in range(0, E, B):
-        summ.fold_device(src[o:], dst[o:], n=B)
-        if flip is None and not summ.ok():
-            flip = o // B
-    import oracle  # checker only
-    first = oracle.bip_first_failure(src.cpu().numpy(), dst.cpu().numpy())
-    expect = None if first < 0 else first // B
-    line = {"metric": "edges/sec for streaming bipartiteness (config 4)", "value": round(E * args.steps / el, 1),
-            "unit": "edges/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(el * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "int64", "data": "synthetic",
-            "config": {"workload": "bip-config4", "side_vertices": 1 << logside, "edges": E, "micro_batch": B,
-                       "clean_stream_bipartite": bool(ok[0]), "odd_cycle_flip_window": flip,
-                       "odd_cycle_flip_window_truth": expect, "verdict_parity": flip == expect}}
-    print(json.dumps(line), flush=True)
+    if group is not None:
+        group.fold_batches(src, dst, per, B)
+        group.finish()
+        final_ok = summ.ok()
+    else:
+        for o in range(0, per, B):
+            summ.fold_device(src[o:], dst[o:], n=B)
+            if flip is None and not summ.ok():
+                flip = o // B
+        final_ok = summ.ok()
+    oks = [bool(ok[0]), bool(final_ok)]
+    if world > 1:
+        v = torch.tensor(oks, dtype=torch.int32, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MIN)  # every replica must agree below
+        v2 = torch.tensor(oks, dtype=torch.int32, device=dev)
+        dist.all_reduce(v2, op=dist.ReduceOp.MAX)
+        agree = bool((v == v2).all().item())
+        oks = [bool(x) for x in v.tolist()]
+    else:
+        agree = True
+    line = None
+    if rank == 0:
+        import oracle  # checker only
+        fs = torch.empty(E, dtype=torch.int64, device=dev)
+        fd = torch.empty(E, dtype=torch.int64, device=dev)
+        gs.gen_bip(fs, fd, 0, E, logside, seed, inject, stream=summ.stream)
+        summ.sync()
+        first = oracle.bip_first_failure(fs.cpu().numpy(), fd.cpu().numpy())
+        del fs, fd
+        expect = None if first < 0 else first // B
+        cfg = {"workload": "bip-config4", "side_vertices": 1 << logside, "edges": E, "micro_batch": B,
+               "clean_stream_bipartite": oks[0], "odd_cycle_final_verdict": oks[1],
+               "odd_cycle_final_verdict_truth": first < 0, "replicas_agree": agree}
+        if group is None:
+            cfg.update({"odd_cycle_flip_window": flip, "odd_cycle_flip_window_truth": expect,
+                        "verdict_parity": flip == expect and oks[1] == (first < 0)})
+        else:
+            cfg.update({"verdict_parity": agree and oks[0] and oks[1] == (first < 0),
+                        "parallelism": "edge-shard x%d, per-batch signed delta all-gather (native group)" % world})
+        line = {"metric": "edges/sec for streaming bipartiteness (config 4)", "value": round(E * args.steps / el, 1),
+                "unit": "edges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(el * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "strong",
+                "vs_baseline": None, "dtype": "int64", "data": "synthetic", "config": cfg}
+        print(json.dumps(line), flush=True)
+    if group is not None:
+        group.close()
     summ.close()
+    if world > 1 or args.exchange:
+        dist.destroy_process_group()
 
 
 def bench_er_latency(args):
