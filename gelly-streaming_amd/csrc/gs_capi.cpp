@@ -1522,8 +1522,8 @@ int comm_api(const RcclApi** api) {
   return GS_OK;
 }
 
-constexpr uint64_t kHdrLag = 4;  // a retune reads the headers of the exchange kHdrLag batches back
-constexpr uint64_t kHdrSlots = 8;  // > kHdrLag: header copies of every retune period stay distinct
+constexpr uint64_t kHdrLag = 4;  // default lag: a retune reads the headers of the exchange `lag` batches back
+constexpr uint64_t kHdrSlots = 8;  // > lag: header copies of every retune period stay distinct
 
 }  // namespace
 
@@ -1535,6 +1535,7 @@ struct gs_group {
   int width = 3;  // int64 per exchange row: {a, b} for CC (16 B), {a, b, parity} for the signed kind
   bool self_apply = false;  // test knob (GS_GROUP_SELF_APPLY=1): also fold this rank's own rows back
   uint64_t max_cap = 0, first_cap = 0, cap = 0, retune = 4;
+  uint64_t lag = kHdrLag;  // GS_GROUP_LAG (1..7)
   // double-buffered exchange: exchange b stages into send[b % 2] and gathers into
   // recv[b % 2] on the communication stream `xs` while the summary stream folds the
   // next batch; its rows are folded during the next exchange (or finish)
@@ -1675,13 +1676,15 @@ int group_exchange(gs_group* g, uint64_t cap, bool keep_header, bool apply_now) 
 
 extern "C" {
 
-// The communication stream gets the device's highest priority (GS_GROUP_XS_PRIO=0:
-// normal): the collective's kernel (or copy) would otherwise wait for back-to-back
-// fold launches to release CUs, and every later stage waits on it.
+// GS_GROUP_XS_PRIO=1 gives the communication stream the device's highest priority,
+// so the collective's kernel (or copy) need not wait for back-to-back fold launches
+// to release CUs. Off by default: it only helps the lane pipeline at one rank, and
+// the multi-rank emulation (all ranks in one process) ran 2-3x slower with it
+// (DESIGN.md section 5).
 static hipError_t create_comm_stream(hipStream_t* st) {
   const char* e = getenv("GS_GROUP_XS_PRIO");
   int least = 0, greatest = 0;
-  if ((e && atoi(e) == 0) || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+  if (!(e && atoi(e) != 0) || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
     return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
   return hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest);
 }
@@ -1716,6 +1719,7 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   g->first_cap = std::min<uint64_t>(first_cap ? first_cap : batch_edges, g->max_cap);
   g->cap = g->first_cap;
   if (const char* m = getenv("GS_GROUP_RETUNE")) g->retune = std::max(1, atoi(m));
+  if (const char* m = getenv("GS_GROUP_LAG")) g->lag = (uint64_t)std::max(1, std::min((int)kHdrSlots - 1, atoi(m)));
   if (const char* m = getenv("GS_GROUP_SELF_APPLY")) g->self_apply = atoi(m) != 0;
   if (const char* m = getenv("GS_GROUP_LANES")) g->no_lanes = atoi(m) == 0;  // default: off
   if (const char* m = getenv("GS_GROUP_HOSTPROF")) g->hostprof = atoi(m) != 0;
@@ -1773,17 +1777,18 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   g->hp_calls++;
   HostTimer ht(g->hostprof ? &g->hp[0] : nullptr);
   // every `retune` exchanges all ranks re-derive the capacity from the same headers:
-  // those of exchange b - kHdrLag, read BEFORE this exchange may copy its own
-  const int lag_slot = (int)((b - kHdrLag) % kHdrSlots);
-  if (b % g->retune == 0 && b >= kHdrLag && g->hdr_batch[lag_slot] == (int64_t)(b - kHdrLag)) {
+  // those of exchange b - lag, read BEFORE this exchange may copy its own
+  const uint64_t lag = g->lag;
+  const int lag_slot = (int)((b - lag) % kHdrSlots);
+  if (b % g->retune == 0 && b >= lag && g->hdr_batch[lag_slot] == (int64_t)(b - lag)) {
     // k_headers writes the exchange number into word 2 of the slot after the headers:
     // poll it (an event synchronisation costs ~40 us of host time even when complete)
     const int64_t* hh = g->hdr_host + (size_t)lag_slot * g->nranks * 3;
     const auto t0 = std::chrono::steady_clock::now();
-    while (__atomic_load_n(&hh[2], __ATOMIC_ACQUIRE) != (int64_t)(b - kHdrLag)) {
+    while (__atomic_load_n(&hh[2], __ATOMIC_ACQUIRE) != (int64_t)(b - lag)) {
       if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
         GS_HIP(hipEventSynchronize(g->hdr_ev[lag_slot]));  // long wait: block instead of spinning
-        if (__atomic_load_n(&hh[2], __ATOMIC_ACQUIRE) != (int64_t)(b - kHdrLag))
+        if (__atomic_load_n(&hh[2], __ATOMIC_ACQUIRE) != (int64_t)(b - lag))
           return fail(GS_ERR_HIP, "exchange header sequence mismatch");
         break;
       }
@@ -1806,7 +1811,7 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   if (rc) return rc;
   ht.lap(nullptr);
   g->cap_sum += (double)g->cap;
-  const bool keep = (b + kHdrLag) % g->retune == 0;
+  const bool keep = (b + lag) % g->retune == 0;
   return group_exchange(g, g->cap, keep, /*apply_now=*/false);
 }
 
