@@ -8,9 +8,11 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("first_cap,self_apply,lanes", [(0, 0, "0"), (64, 0, "0"), (64, 1, "0"), (0, 0, "1"),
-                                                        (64, 1, "1")])
-def test_group_single_rank_matches_oracle(gs, oracle_mod, monkeypatch, first_cap, self_apply, lanes):
+@pytest.mark.parametrize("first_cap,self_apply,lanes,knobs", [
+    (0, 0, "0", {}), (64, 0, "0", {}), (64, 1, "0", {}), (0, 0, "1", {}), (64, 1, "1", {}),
+    (64, 1, "1", {"GS_GROUP_XS_PRIO": "1"}), (64, 1, "0", {"GS_GROUP_LAG": "1"}),
+    (64, 0, "1", {"GS_GROUP_LAG": "7"})])
+def test_group_single_rank_matches_oracle(gs, oracle_mod, monkeypatch, first_cap, self_apply, lanes, knobs):
     """self_apply: the rank also folds its own gathered rows (16-B CC rows, exchange
     layout, lagged apply) -- the remote-fold path, exercised at one rank; folding a
     delta twice is idempotent, so any mis-parsed row would show in the labels."""
@@ -18,6 +20,8 @@ def test_group_single_rank_matches_oracle(gs, oracle_mod, monkeypatch, first_cap
     monkeypatch.setenv("GS_GROUP_RETUNE", "2")
     monkeypatch.setenv("GS_GROUP_SELF_APPLY", str(self_apply))
     monkeypatch.setenv("GS_GROUP_LANES", lanes)
+    for k, v in knobs.items():  # opt-in knobs: stream priority, retune header lag
+        monkeypatch.setenv(k, v)
     n, B = 1 << 17, 1 << 13
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")
