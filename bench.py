@@ -49,6 +49,10 @@ def parse():
                    help="pipelined windows at N=1 (gs_set_pipelining depth; 1 = strictly in order)")
     p.add_argument("--exchange", action="store_true",
                    help="run the multi-GPU delta-exchange path even at one rank (overhead measurement)")
+    p.add_argument("--exchange-log-batch", type=int, default=21,
+                   help="per-rank micro-batch (log2 edges) between delta exchanges at N > 1 (or --exchange): "
+                        "each exchange has a fixed cost (stage, collective, header), so the multi-GPU path "
+                        "exchanges every 2^21 edges per rank (DESIGN.md section 5)")
     p.add_argument("--exchange-impl", choices=["native", "torch"], default="native",
                    help="native: RCCL inside libgs_summary (gs_group_*); torch: torch.distributed all-gather")
     return p.parse_args()
@@ -332,7 +336,7 @@ def main():
     from gelly_streaming_amd.distributed import DeltaExchangeFold
 
     E = (1 << args.scale) * args.edge_factor
-    B = 1 << args.log_batch
+    B = 1 << (args.exchange_log_batch if (world > 1 or args.exchange) else args.log_batch)
     per = E // world
     start = rank * per
     nbatch = (per + B - 1) // B

@@ -485,8 +485,19 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
                      size_t stride, size_t w_stride, bool track, bool check_cap, const ExchangeLayout& xl,
                      bool allow_pipe) {
   if (n == 0) return GS_OK;
-  if (check_cap) {
-    int rc = ensure_capacity(h, n);
+  // Capacity units (each may add 2 vertices): one per edge, or for a gathered exchange
+  // buffer one per record row of the ranks actually folded -- the header rows, the
+  // skipped (own) block and the padding past each header's count add no vertex. The
+  // valid rows may sit in any chunk, so an exchange fold claims all its units with
+  // its last chunk's report.
+  uint64_t units = n;
+  if (xl.rows) {
+    const uint64_t blocks = n / xl.rows;
+    const uint64_t folded = blocks - (xl.skip_rank >= 0 && (uint64_t)xl.skip_rank < blocks ? 1 : 0);
+    units = folded * (xl.rows - 1);
+  }
+  if (check_cap && units) {
+    int rc = ensure_capacity(h, units);
     if (rc) return rc;
   }
   // Pipelined: plain fused folds (no delta tracking, no exchange layout, no hot
@@ -543,7 +554,7 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
                       inline_max, xl.rows, xl.skip_rank, xl.base, (uint32_t)off, st);
     }
     GS_HIP(hipGetLastError());
-    if (check_cap) {
+    if (check_cap && units) {
       // A report may only claim chunks queued before it on ITS stream. Every stream
       // (handle, lanes, side) reports every kRepEvery-th chunk queued on it, claiming
       // that stream's chunks since its previous report: a report is a launch, and
@@ -553,8 +564,9 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       if (st == h->side) rs = gs_summary::kRepStreams - 1;
       for (int i = 0; i < gs_summary::kLanes; ++i)
         if (st == h->lane[i]) rs = 1 + i;
-      h->rep_pending[rs] += c;
-      h->rep_pending_edges += c;
+      const uint64_t cu = xl.rows ? (off + c >= n ? units : 0) : c;
+      h->rep_pending[rs] += cu;
+      h->rep_pending_edges += cu;
       // off the handle stream a report is not a gap between folds: report every chunk
       // while the bound is near the load limit (small tables), so no fold has to wait
       const bool tight = rs != 0 && (double)(h->nv_ub + 4ull * gs_summary::kRepEvery * c) > kMaxLoad * (double)h->cap;
