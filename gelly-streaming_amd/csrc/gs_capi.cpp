@@ -77,6 +77,7 @@ struct gs_summary {
   bool nv_pending = false;
   uint32_t* ctr = nullptr;
   uint64_t nv_ub = 0;  // host upper bound of the vertex count
+  uint64_t cap_waits = 0, cap_syncs = 0;  // capacity checks that waited for reports / joined every stream
   // capacity reports (k_report after every capacity-checked fold): a ring of packed
   // words in host-coherent memory, read without any HIP call
   static constexpr int kRepRing = 16;
@@ -451,6 +452,7 @@ int ensure_capacity(gs_summary* h, size_t n) {
     return GS_OK;
   }
   // wait for reports of the folds in flight (the GPU keeps working: no drain)
+  h->cap_waits++;
   const auto t0 = std::chrono::steady_clock::now();
   while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200)) {
     const uint64_t b = capacity_bound(h, &all);
@@ -463,6 +465,7 @@ int ensure_capacity(gs_summary* h, size_t n) {
     std::this_thread::yield();
   }
   uint64_t nv = 0;
+  h->cap_syncs++;
   int rc = read_nv(h, &nv);  // exact (joins every stream)
   if (rc) return rc;
   h->nv_exact = nv;
@@ -1991,7 +1994,8 @@ int gs_group_destroy(gs_group_t g) {
     const char* nm[6] = {"retune", "own fold", "stage+events", "collective", "headers", "remote fold"};
     fprintf(stderr, "[gs_group rank %d] host us per batch over %llu batches:", g->rank, (unsigned long long)g->hp_calls);
     for (int i = 0; i < 6; ++i) fprintf(stderr, " %s %.1f", nm[i], g->hp[i] * 1e6 / (double)g->hp_calls);
-    fprintf(stderr, "; mean cap %.0f rows\n", g->cap_sum / (double)g->hp_calls);
+    fprintf(stderr, "; mean cap %.0f rows; capacity waits %llu, syncs %llu\n", g->cap_sum / (double)g->hp_calls,
+            (unsigned long long)g->h->cap_waits, (unsigned long long)g->h->cap_syncs);
   }
   DeviceGuard dg(g->h->device);
   (void)hipStreamSynchronize(g->h->stream);

@@ -350,6 +350,36 @@ def test_delta_stage_backlog_and_exchange_fold(gs, oracle_mod):
         r.close()
 
 
+@pytest.mark.parametrize("skip", [-1, 7])
+def test_exchange_fold_grows_table_from_remote_rows(gs, oracle_mod, skip):
+    # A replica that folds nothing itself receives every vertex through exchange
+    # folds (padded 3-rank buffers, cap far above the live rows). The capacity bound
+    # charges only the folded ranks' record rows (gs_capi.cpp fold_device_impl), so
+    # the tiny table must still grow in time: labels equal the oracle's.
+    # skip = -1 folds every block; skip = 7 (no such rank) must not drop a block.
+    import torch
+    s, d = oracle_mod.rmat_edges(6, 12, 0, 1 << 14, True)
+    world, B, cap = 3, 1 << 10, 4000
+    senders = [gs.Summary("cc", capacity_hint=1 << 13) for _ in range(world)]
+    sink = gs.Summary("cc", capacity_hint=64)
+    for r in senders:
+        r.set_delta_tracking(True)
+    sends = [torch.empty((cap + 1, 3), dtype=torch.int64, device="cuda") for _ in range(world)]
+    for i in range(0, len(s), world * B):
+        for r in range(world):
+            lo = i + r * B
+            senders[r].fold(s[lo:lo + B], d[lo:lo + B])
+            senders[r].delta_stage(sends[r], cap)
+            senders[r].sync()
+        recv = torch.cat(sends)
+        hdr = recv.view(world, cap + 1, 3)[:, 0, :].cpu()
+        assert int((hdr[:, 1] - hdr[:, 0]).max()) == 0  # cap covers every batch: no backlog
+        sink.fold_exchange(recv, world, cap + 1, skip)
+    _assert_cc_equal(sink, oracle_mod, s, d)
+    for r in senders + [sink]:
+        r.close()
+
+
 def test_delta_records_skip_padding(gs, oracle_mod):
     import torch
     rec = torch.tensor([[1, 2, 0], [3, 4, 0x80], [5, 6, 0], [7, 7, 0x80]], dtype=torch.int64, device="cuda")
