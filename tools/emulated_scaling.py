@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--log-batch", type=int, default=20)
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--first-cap", type=int, default=0, help="rows of the first exchanges (0: the batch)")
     a = ap.parse_args()
     E, B = 16 << a.scale, 1 << a.log_batch
     src = torch.empty(E, dtype=torch.int64, device="cuda")
@@ -67,7 +68,7 @@ def main():
 
         def rank(r):
             try:
-                g = gs.Group(summ[r], uid, n, r, B)
+                g = gs.Group(summ[r], uid, n, r, B, a.first_cap)
                 for _ in range(a.reps + 1):
                     summ[r].reset()
                     summ[r].sync()
