@@ -49,10 +49,14 @@ def parse():
                    help="pipelined windows at N=1 (gs_set_pipelining depth; 1 = strictly in order)")
     p.add_argument("--exchange", action="store_true",
                    help="run the multi-GPU delta-exchange path even at one rank (overhead measurement)")
-    p.add_argument("--exchange-log-batch", type=int, default=21,
+    p.add_argument("--exchange-log-batch", type=int, default=22,
                    help="per-rank micro-batch (log2 edges) between delta exchanges at N > 1 (or --exchange): "
                         "each exchange has a fixed cost (stage, collective, header), so the multi-GPU path "
-                        "exchanges every 2^21 edges per rank (DESIGN.md section 5)")
+                        "exchanges every 2^22 edges per rank (DESIGN.md section 5)")
+    p.add_argument("--capacity-log2", type=int, default=0,
+                   help="relabel-table capacity hint of the CC summary (log2 vertices; 0: 2^scale, or "
+                        "2^(scale+1) on the exchange path: headroom for the host capacity bound while "
+                        "gathered rows are in flight, DESIGN.md section 5)")
     p.add_argument("--exchange-impl", choices=["native", "torch"], default="native",
                    help="native: RCCL inside libgs_summary (gs_group_*); torch: torch.distributed all-gather")
     return p.parse_args()
@@ -341,7 +345,8 @@ def main():
     start = rank * per
     nbatch = (per + B - 1) // B
 
-    summ = gs.Summary("cc", device=local, capacity_hint=1 << args.scale)
+    xlog = args.scale + 1 if (world > 1 or args.exchange) else args.scale
+    summ = gs.Summary("cc", device=local, capacity_hint=1 << (args.capacity_log2 or xlog))
     st = summ.stream
     src = torch.empty(per, dtype=torch.int64, device=dev)
     dst = torch.empty(per, dtype=torch.int64, device=dev)
@@ -477,6 +482,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": "rmat%d-cc-stream" % args.scale, "scale": args.scale,
                        "edges": E, "micro_batch": B, "ids": "sparse 64-bit (scrambled)",
+                       "capacity_hint": 1 << (args.capacity_log2 or xlog),
                        "vertices_labelled": int(labelled),
                        "parallelism": ("edge-shard x%d, per-batch delta all-gather (%s)" % (world, args.exchange_impl))
                        if xch is not None else "single GPU"},

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--log-batch", type=int, default=20)
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--hint-log2", type=int, default=0, help="capacity hint of the rank replicas (0: 2^scale)")
     ap.add_argument("--first-cap", type=int, default=0, help="rows of the first exchanges (0: the batch)")
     a = ap.parse_args()
     E, B = 16 << a.scale, 1 << a.log_batch
@@ -60,7 +61,7 @@ def main():
     for n in [int(x) for x in a.ranks.split(",")]:
         per = E // n
         uid = gs.group_unique_id()
-        summ = [gs.Summary("cc", capacity_hint=1 << a.scale) for _ in range(n)]
+        summ = [gs.Summary("cc", capacity_hint=1 << (a.hint_log2 or a.scale)) for _ in range(n)]
         bar = threading.Barrier(n)
         times = [[] for _ in range(n)]
         recs = [None] * n
