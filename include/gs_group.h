@@ -41,7 +41,11 @@ int gs_group_unique_id(void* id);
  * `first_cap` = records per rank in the first exchanges (0: batch_edges). Turns
  * delta tracking on. batch_edges == 0 creates a tree-combine-only group (no
  * exchange buffers, tracking untouched: fold partials with gs_fold[_device], then
- * gs_group_tree_combine). Collective: every rank must call it. */
+ * gs_group_tree_combine). Collective: every rank must call it.
+ * Sizing: the summary's host-side capacity bound charges 2 vertices per record row
+ * of every gathered exchange still in flight ((nranks - 1) x cap rows each), so give
+ * the summary headroom above the final vertex count (bench.py: 2x the vertex hint at
+ * 2^22-edge batches, 8 ranks), or a fold waits for the GPU to drain. */
 int gs_group_create(gs_group_t* g, gs_handle h, const void* id, int nranks, int rank, size_t batch_edges,
                     size_t first_cap);
 
