@@ -75,6 +75,42 @@ def test_delta_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, world, first
     assert parts == sorted(zip(ov.tolist(), olab.tolist()))
 
 
+_BENCH_SHAPE = {}
+
+
+@pytest.mark.parametrize("world,log_batch", [(2, 22), (4, 21)])
+def test_bench_exchange_shape_emulated_ranks(gs, oracle_mod, monkeypatch, world, log_batch):
+    """bench.py's N-GPU defaults at reduced scale: RMAT-20 (2^24 edges), 2^21-2^22-edge
+    exchanges per rank, a capacity hint of twice the vertex scale, the default first
+    capacity and knobs. Every replica equals the oracle."""
+    import torch
+    monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
+    scale, n, B = 20, 1 << 24, 1 << log_batch
+    src = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int64, device="cuda")
+    gs.gen_rmat(src, dst, 0, n, scale, 0x5EED0026, True)
+    torch.cuda.synchronize()
+    if "oracle" not in _BENCH_SHAPE:
+        _BENCH_SHAPE["oracle"] = oracle_mod.cc_labels(src.cpu().numpy(), dst.cpu().numpy())
+    ov, olab = _BENCH_SHAPE["oracle"]
+    uid = gs.group_unique_id()
+    per = n // world
+
+    def rank(r):
+        with gs.Summary("cc", capacity_hint=1 << (scale + 1)) as s:
+            g = gs.Group(s, uid, world, r, B)
+            g.fold_batches(src[r * per:], dst[r * per:], per, B)
+            g.finish()
+            st = g.stats()
+            v, lab = s.labels()
+            g.close()
+        return v, lab, st
+
+    for r, (v, lab, st) in enumerate(_run_ranks(world, rank)):
+        assert np.array_equal(v, ov) and np.array_equal(lab, olab), "rank %d replica" % r
+        assert st["exchanges"] >= per // B
+
+
 @pytest.mark.parametrize("lanes", ["0", "1"])
 @pytest.mark.parametrize("inject", [(), (1 << 15,)])
 def test_signed_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, inject, lanes):
