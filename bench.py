@@ -53,6 +53,9 @@ def parse():
                    help="per-rank micro-batch (log2 edges) between delta exchanges at N > 1 (or --exchange): "
                         "each exchange has a fixed cost (stage, collective, header), so the multi-GPU path "
                         "exchanges every 2^22 edges per rank (DESIGN.md section 5)")
+    p.add_argument("--exchange-first-cap", type=int, default=1 << 20,
+                   help="records per rank in the first exchanges, before the header-driven retune "
+                        "(0: the exchange batch); every padded row crosses xGMI to N - 1 ranks")
     p.add_argument("--capacity-log2", type=int, default=0,
                    help="relabel-table capacity hint of the CC summary (log2 vertices; 0: 2^scale, or "
                         "2^(scale+1) on the exchange path: headroom for the host capacity bound while "
@@ -361,7 +364,7 @@ def main():
         if args.exchange_impl == "native":
             uid = [gs.group_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
-            xch = NativeExchange(gs.Group(summ, uid[0], world, rank, B))
+            xch = NativeExchange(gs.Group(summ, uid[0], world, rank, B, args.exchange_first_cap))
         else:
             xch = DeltaExchangeFold(summ, B, dev)
 
