@@ -1552,6 +1552,7 @@ struct gs_group {
   int width = 3;  // int64 per exchange row: {a, b} for CC (16 B), {a, b, parity} for the signed kind
   bool self_apply = false;  // test knob (GS_GROUP_SELF_APPLY=1): also fold this rank's own rows back
   uint64_t max_cap = 0, first_cap = 0, cap = 0, retune = 1;
+  int margin = 3;  // GS_GROUP_MARGIN: a retuned cap is queued + queued >> margin + 1024 (>= 64: no margin)
   uint64_t lag = kHdrLag;  // GS_GROUP_LAG (1..7)
   // double-buffered exchange: exchange b stages into send[b % 2] and gathers into
   // recv[b % 2] on the communication stream `xs` while the summary stream folds the
@@ -1737,6 +1738,7 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   g->cap = g->first_cap;
   if (const char* m = getenv("GS_GROUP_RETUNE")) g->retune = std::max(1, atoi(m));
   if (const char* m = getenv("GS_GROUP_LAG")) g->lag = (uint64_t)std::max(1, std::min((int)kHdrSlots - 1, atoi(m)));
+  if (const char* m = getenv("GS_GROUP_MARGIN")) g->margin = std::max(0, atoi(m));
   if (const char* m = getenv("GS_GROUP_SELF_APPLY")) g->self_apply = atoi(m) != 0;
   if (const char* m = getenv("GS_GROUP_LANES")) g->no_lanes = atoi(m) == 0;  // default: off
   if (const char* m = getenv("GS_GROUP_HOSTPROF")) g->hostprof = atoi(m) != 0;
@@ -1812,7 +1814,8 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
     }
     int64_t queued = 0;
     for (int r = 0; r < g->nranks; ++r) queued = std::max(queued, hh[r * 3 + 1]);
-    g->cap = std::min<uint64_t>(g->max_cap, std::max<uint64_t>(4096, (uint64_t)queued + (uint64_t)queued / 4 + 1024));
+    const uint64_t q = (uint64_t)queued;
+    g->cap = std::min<uint64_t>(g->max_cap, std::max<uint64_t>(4096, q + (g->margin < 64 ? q >> g->margin : 0) + 1024));
   }
   // own fold: with GS_GROUP_LANES=1, on lane b % 2 into delta set b % 2 when possible
   // (overlaps the previous exchange's fold and stage); default: the handle's stream
