@@ -449,6 +449,9 @@ def main():
                 "fold_avg_us": round(fold_avg_ms * 1e3, 2), "fold_launches": int(nf),
                 "hook_avg_us": round(hook_ms * 1e3 / max(nh, 1), 2), "hook_launches": int(nh),
                 "export_ms": round(exp_ms, 3)}
+        if xch is not None:
+            roof["note"] = ("exchange path: fold launches include the other ranks' gathered rows (side stream); "
+                            "achieved assumes %d own edges per launch" % int(edges_per_launch))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
