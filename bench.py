@@ -49,13 +49,9 @@ def parse():
                    help="pipelined windows at N=1 (gs_set_pipelining depth; 1 = strictly in order)")
     p.add_argument("--exchange", action="store_true",
                    help="run the multi-GPU delta-exchange path even at one rank (overhead measurement)")
-    p.add_argument("--exchange-log-batch", type=int, default=22,
+    p.add_argument("--exchange-log-batch", type=int, default=20,
                    help="per-rank micro-batch (log2 edges) between delta exchanges at N > 1 (or --exchange): "
-                        "each exchange has a fixed cost (stage, collective, header), so the multi-GPU path "
-                        "exchanges every 2^22 edges per rank (DESIGN.md section 5)")
-    p.add_argument("--exchange-first-cap", type=int, default=1 << 20,
-                   help="records per rank in the first exchanges, before the header-driven retune "
-                        "(0: the exchange batch); every padded row crosses xGMI to N - 1 ranks")
+                        "SURVEY.md 8(d) config 3 = 2^20 per GPU, combine every global batch")
     p.add_argument("--capacity-log2", type=int, default=0,
                    help="relabel-table capacity hint of the CC summary (log2 vertices; 0: 2^scale, or "
                         "2^(scale+1) on the exchange path: headroom for the host capacity bound while "
@@ -364,7 +360,7 @@ def main():
         if args.exchange_impl == "native":
             uid = [gs.group_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
-            xch = NativeExchange(gs.Group(summ, uid[0], world, rank, B, args.exchange_first_cap))
+            xch = NativeExchange(gs.Group(summ, uid[0], world, rank, B))
         else:
             xch = DeltaExchangeFold(summ, B, dev)
 
@@ -426,7 +422,7 @@ def main():
         one_step()
         summ.sync()
         nf, fold_ms = summ.kernel_stats("fold")
-        nh, hook_ms = summ.kernel_stats("hook")
+        nh, hook_ms = summ.kernel_stats("stage")
         ne, exp_ms = summ.kernel_stats("export")
         summ.set_profiling(False)
         fold_avg_ms = fold_ms / max(nf, 1)
@@ -447,7 +443,7 @@ def main():
                 "traffic_frac": round(traffic_gbs / HBM_PEAK_GBS, 4) if traffic_gbs else None,
                 "bytes_per_edge": BYTES_PER_EDGE_SPARSE, "edges_per_launch": int(edges_per_launch),
                 "fold_avg_us": round(fold_avg_ms * 1e3, 2), "fold_launches": int(nf),
-                "hook_avg_us": round(hook_ms * 1e3 / max(nh, 1), 2), "hook_launches": int(nh),
+                "stage_avg_us": round(hook_ms * 1e3 / max(nh, 1), 2), "stage_launches": int(nh),
                 "export_ms": round(exp_ms, 3)}
         if xch is not None:
             roof["note"] = ("exchange path: fold launches include the other ranks' gathered rows (side stream); "

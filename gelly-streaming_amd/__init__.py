@@ -16,7 +16,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libgs_summary.so")
-if os.environ.get("GS_LIB_VARIANT"):  # experiment builds (Makefile target `variant`)
+if os.environ.get("GS_LIB_VARIANT"):  # debug-counter build (Makefile target `debug`: GS_LIB_VARIANT=debug)
     LIB_PATH = os.path.join(_HERE, "lib_" + os.environ["GS_LIB_VARIANT"], "libgs_summary.so")
 
 KIND_CC = 0
@@ -32,7 +32,7 @@ GS_ERR_PARSE = -5
 SEP_WHITESPACE = 0  # split("\\s") (ConnectedComponentsExample.java:113)
 SEP_TAB = 1         # split("\\t") (BipartitenessCheckExample.java:101)
 
-KERNEL_IDS = {"fold": 0, "hook": 1, "export": 2, "init": 3}
+KERNEL_IDS = {"fold": 0, "stage": 1, "export": 2, "init": 3}
 
 # Every symbol include/gs_summary.h and include/gs_gen.h declare.
 EXPORTED_SYMBOLS = (
@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "gs_group_unique_id", "gs_group_create", "gs_group_fold_device", "gs_group_finish", "gs_group_stats",
     "gs_group_destroy", "gs_group_tree_combine", "gs_combine_exported_device",
     "gs_group_fold_batches_device", "gs_export_labels_part_device",
+    "gs_delta_capacity", "gs_find_labels_device", "gs_capacity_stats",
 )
 
 
@@ -101,8 +102,11 @@ def lib():
     L.gs_set_delta_tracking.argtypes = [_vp, ctypes.c_int]
     L.gs_take_delta_records.argtypes = [_vp, _vp, _sz, _vp]
     L.gs_fold_records_device.argtypes = [_vp, _vp, _sz, ctypes.c_int]
-    L.gs_delta_stage.argtypes = [_vp, _vp, _sz]
-    L.gs_fold_exchange_device.argtypes = [_vp, _vp, _sz, _sz, ctypes.c_int]
+    L.gs_delta_stage.argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
+    L.gs_fold_exchange_device.argtypes = [_vp, _vp, _vp, _sz, _sz, ctypes.c_int, ctypes.c_int]
+    L.gs_delta_capacity.argtypes = [_vp, ctypes.POINTER(_u64)]
+    L.gs_find_labels_device.argtypes = [_vp, _vp, _sz, _vp, _vp]
+    L.gs_capacity_stats.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double)]
     L.gs_get_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
     L.gs_set_profiling.argtypes = [_vp, ctypes.c_int]
     L.gs_set_pipelining.argtypes = [_vp, ctypes.c_int]
@@ -116,7 +120,7 @@ def lib():
                                         ctypes.POINTER(_i64)]
     L.gs_fold_text.argtypes = [_vp, ctypes.c_char_p, _sz, ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(_i64)]
     L.gs_group_unique_id.argtypes = [_vp]
-    L.gs_group_create.argtypes = [ctypes.POINTER(_vp), _vp, _vp, ctypes.c_int, ctypes.c_int, _sz, _sz]
+    L.gs_group_create.argtypes = [ctypes.POINTER(_vp), _vp, _vp, ctypes.c_int, ctypes.c_int, _sz]
     L.gs_group_fold_device.argtypes = [_vp, _vp, _vp, _sz]
     L.gs_group_finish.argtypes = [_vp]
     L.gs_group_stats.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_u64)]
@@ -218,6 +222,12 @@ class Summary:
         _check(lib().gs_find(self._h, int(v), ctypes.byref(lab), ctypes.byref(found)))
         return lab.value if found.value else None
 
+    def find_labels_device(self, v, label, found=None, n=None):
+        """Batched find (gs_find_labels_device): label[i] = canonical label of the
+        DEVICE id v[i]; found[i] = 0 for an id never seen. Asynchronous on self.stream."""
+        n = v.numel() if n is None else n
+        _check(lib().gs_find_labels_device(self._h, _ptr(v), int(n), _ptr(label), _ptr(found)))
+
     def labels(self):
         """(vertex, canonical label) numpy arrays, sorted by vertex."""
         n = self.num_vertices()
@@ -282,21 +292,29 @@ class Summary:
     def set_delta_tracking(self, on=True):
         _check(lib().gs_set_delta_tracking(self._h, 1 if on else 0))
 
+    def delta_capacity(self):
+        """Rows the delta list holds between two takes / stages (gs_delta_capacity)."""
+        n = _u64()
+        _check(lib().gs_delta_capacity(self._h, ctypes.byref(n)))
+        return n.value
+
     def take_delta_records(self, rec, cap, count):
         """Pack the delta since the last take into `rec` (device int64 [cap, 3]) and
         its record count into `count` (device int64 [1]); asynchronous on self.stream."""
         _check(lib().gs_take_delta_records(self._h, _ptr(rec), int(cap), _ptr(count)))
 
-    def delta_stage(self, send, cap):
-        """Stage the delta into `send` (device int64 [cap + 1, 3]: header row
-        {sent, queued, skip} + up to cap records; the rest stays queued);
-        asynchronous on self.stream."""
-        _check(lib().gs_delta_stage(self._h, _ptr(send), int(cap)))
+    def delta_stage(self, send, cap, count, width=3):
+        """Stage every pending record into `send` (device int64 [cap, width]) and the
+        count word (| 2^62 when a signed verdict failed) into `count` (device int64
+        [1]); asynchronous on self.stream. cap >= delta_capacity()."""
+        _check(lib().gs_delta_stage(self._h, _ptr(send), int(cap), int(width), _ptr(count)))
 
-    def fold_exchange(self, recv, world, rows, skip_rank):
-        """Fold a gathered exchange buffer (world x rows records, row 0 of each
-        rank = header), skipping `skip_rank`'s rows."""
-        _check(lib().gs_fold_exchange_device(self._h, _ptr(recv), int(world), int(rows), int(skip_rank)))
+    def fold_exchange(self, recv, counts, world, rows, skip_rank, width=3):
+        """Fold a gathered exchange buffer: `world` blocks of `rows` rows of `width`
+        int64, block r live for its first counts[r] rows (device count words),
+        skipping block `skip_rank`."""
+        _check(lib().gs_fold_exchange_device(self._h, _ptr(recv), _ptr(counts), int(world), int(rows), int(width),
+                                             int(skip_rank)))
 
     def fold_records(self, rec, n, track=False):
         """Fold n device records {a, b, w} (another replica's delta)."""
@@ -346,9 +364,16 @@ class Summary:
         _check(lib().gs_table_capacity(self._h, ctypes.byref(n)))
         return n.value
 
+    def capacity_stats(self):
+        """(waits, syncs, wait_ms) of the host capacity checks (gs_capacity_stats)."""
+        w, s_ = _u64(), _u64()
+        ms = ctypes.c_double()
+        _check(lib().gs_capacity_stats(self._h, ctypes.byref(w), ctypes.byref(s_), ctypes.byref(ms)))
+        return {"waits": w.value, "syncs": s_.value, "wait_ms": ms.value}
+
 
 # ---------------------------------------------------------------- native multi-GPU group
-GROUP_ID_BYTES = 128
+GROUP_ID_BYTES = 256  # two RCCL unique ids (count and data communicators)
 
 
 def group_unique_id():
@@ -360,14 +385,14 @@ def group_unique_id():
 
 class Group:
     """Native multi-GPU combine (include/gs_group.h): per global micro-batch,
-    fold this rank's edges, all-gather the staged delta over RCCL on the
-    summary's stream, fold the other ranks' records. Collective calls."""
+    fold this rank's edges, all-gather the delta counts and then exactly the live
+    records over RCCL, fold the other ranks' records. Collective calls."""
 
-    def __init__(self, summary, uid, nranks, rank, batch_edges, first_cap=0):
+    def __init__(self, summary, uid, nranks, rank, batch_edges):
         g = _vp()
         buf = ctypes.create_string_buffer(bytes(uid), GROUP_ID_BYTES)
         _check(lib().gs_group_create(ctypes.byref(g), summary.handle, buf, int(nranks), int(rank),
-                                     int(batch_edges), int(first_cap)))
+                                     int(batch_edges)))
         self._g = g
         self.summary = summary
 
@@ -389,7 +414,7 @@ class Group:
     def stats(self):
         e, s, c = _u64(), _u64(), _u64()
         _check(lib().gs_group_stats(self._g, ctypes.byref(e), ctypes.byref(s), ctypes.byref(c)))
-        return {"exchanges": e.value, "records_sent": s.value, "cap": c.value}
+        return {"exchanges": e.value, "records_sent": s.value, "rows_received": c.value}
 
     def close(self):
         if getattr(self, "_g", None):

@@ -1,20 +1,15 @@
-#include <atomic>
-#include <chrono>
-#include <condition_variable>
-#include <deque>
-#include <map>
-#include <mutex>
-#include <unistd.h>
-// gs_capi.cpp -- implementation of the C ABI in include/gs_summary.h.
+// gs_capi.cpp -- implementation of the summary C ABI (include/gs_summary.h).
 //
 // One handle = one GPU-resident summary: the slot table (relabel + forest), the
-// sharded counters, the active-edge lists, the optional delta lists, pinned
-// staging for host-pointer folds, and the handle's own HIP stream. All device
-// work is enqueued on that stream; the host only synchronises when it must return
-// data (counts, exports) or when the vertex table may need to grow.
+// vertex list, the sharded counters, the optional delta list, pinned staging for
+// host-pointer folds, the combine export scratch and the handle's own HIP stream.
+// All device work is enqueued on that stream (or on its pipelining lanes / the
+// group's side stream); the host only synchronises when it must return data
+// (counts, exports) or when the vertex table may need to grow.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -22,11 +17,9 @@
 #include <vector>
 
 #include "gs_ingest.h"
-#include "gs_ingest.hpp"
-#include "gs_kernels.hpp"
-#include "gs_summary.h"
+#include "gs_internal.hpp"
 
-namespace {
+namespace gsi {
 
 thread_local std::string g_err;
 
@@ -35,169 +28,13 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
-#define GS_HIP(call)                                                                                  \
-  do {                                                                                                \
-    hipError_t e_ = (call);                                                                           \
-    if (e_ != hipSuccess)                                                                             \
-      return fail(GS_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));                     \
-  } while (0)
-
-constexpr uint32_t kMaxChunk = 1u << 22;     // edges per k_fold launch
-constexpr uint32_t kStageChunk = 1u << 20;   // edges per pinned staging buffer
-constexpr double kMaxLoad = 0.70;            // grow the table past this load factor
-constexpr uint64_t kMaxCap = 1ull << 30;     // link holds slot << 1 in 32 bits
-
-enum { KID_FOLD = 0, KID_HOOK = 1, KID_EXPORT = 2, KID_INIT = 3, KID_N = 4 };
+namespace {
 
 uint64_t next_pow2(uint64_t x) {
   uint64_t p = 1;
   while (p < x) p <<= 1;
   return p;
 }
-
-}  // namespace
-
-struct gs_summary {
-  int device = 0;
-  int kind = GS_KIND_CC;
-  hipStream_t stream = nullptr;
-  // table
-  gs::Slot* tab = nullptr;  // [hotcap | cap | 2 reserved]
-  uint64_t cap = 0;
-  int logcap = 0;
-  // hot level (gs_device.hpp): open while fewer than hot_target vertices are known;
-  // the count is read back asynchronously (pinned copy + event), never synchronously
-  uint64_t hotcap = 0;
-  int loghot = 0;
-  bool hot_open = false;
-  uint64_t hot_target = 0;
-  uint32_t* h_nv = nullptr;  // pinned copy of the new-vertex counter block
-  uint32_t* h_flags = nullptr;  // pinned: error / overflow flags
-  hipEvent_t nv_ev = nullptr;
-  bool nv_pending = false;
-  uint32_t* ctr = nullptr;
-  uint64_t nv_ub = 0;  // host upper bound of the vertex count
-  uint64_t cap_waits = 0, cap_syncs = 0;  // capacity checks that waited for reports / joined every stream
-  // capacity reports (k_report after every capacity-checked fold): a ring of packed
-  // words in host-coherent memory, read without any HIP call
-  static constexpr int kRepRing = 16;
-  unsigned long long* rep = nullptr;      // host pointer
-  unsigned long long* rep_dev = nullptr;  // its device mapping
-  uint64_t rep_seq = 0;
-  static constexpr int kRepEvery = 4;  // each stream reports every 4th capacity-checked chunk (a report costs a launch)
-  static constexpr int kRepStreams = 6;  // handle stream, 4 lanes, side stream
-  int rep_skip[kRepStreams] = {};
-  uint64_t rep_pending[kRepStreams] = {};  // per stream: edges of chunks queued since its last report
-  uint64_t rep_pending_edges = 0;      // sum of rep_pending: edges of capacity-checked chunks not yet reported
-  uint64_t e_launched = 0;  // edges of capacity-checked folds since reset / rebuild
-  uint64_t nv_exact = 0, e_exact = 0;  // an exact count and the edges complete when it was read
-  // lists
-  uint2* act = nullptr;
-  uint32_t act_shard_cap = 0;
-  bool track = false;
-  // two delta sets, so that a fold can record into one while the previous fold's
-  // set is staged (a group's pipelined exchange); everything else uses set 0
-  int64_t* drec = nullptr;  // [2][kShards][delta_shard_cap][3]
-  uint32_t delta_shard_cap = 0;
-  int dset = 0;             // the set folds record into
-  int force_lane = -1;      // >= 0: the next fold goes to this lane (a group's pipelined own fold)
-  // exchange record queue (ping-pong): packed records not yet sent
-  int64_t* q[2] = {nullptr, nullptr};
-  unsigned long long* qn = nullptr;  // [2] device counts
-  uint64_t qcap = 0;
-  int qsel = 0;
-  uint64_t delta_fill_ub[2] = {0, 0};  // worst-case per-shard fill of each set since its last stage
-  // hook policy (DESIGN.md "Kernels"): FUSED hooks in k_fold; DEFER hooks waves
-  // with <= inline_max active edges in place and hands the rest to the next
-  // k_fold launch (triple-buffered active sets); COMPACT runs k_hook per chunk.
-  enum Mode { FUSED = 0, DEFER = 1, COMPACT = 2 } mode = FUSED;
-  int inline_max = 4;
-  int ept = 1;        // edges per k_fold thread
-  uint64_t epoch = 0; // k_fold launches since reset (selects the active set)
-  int pending = -1;   // active set still waiting to be drained
-  bool pending_track = false;  // tracking state of the fold that deferred it
-  // staging for host folds
-  int64_t* d_stage = nullptr;  // [2][2][kStageChunk]
-  uint8_t* d_wstage = nullptr; // [2][kStageChunk]
-  int64_t* h_stage = nullptr;  // pinned, same shape
-  uint8_t* h_wstage = nullptr;
-  hipEvent_t stage_ev[2] = {nullptr, nullptr};
-  int stage_next = 0;
-  int64_t* d_scratch = nullptr;  // small scratch (find_one)
-  // pipelined folds (gs_set_pipelining): consecutive device folds alternate over
-  // two lane streams so that fold b+1 may start while fold b drains; every other
-  // entry point joins the lanes onto `stream` first (join_lanes).
-  // text ingest (gs_fold_text): pinned + device text chunks, parsed edges, scratch
-  char* h_text = nullptr;  // pinned [2][kTextChunk]
-  uint64_t* h_tres = nullptr;  // pinned [2][2] parse results
-  hipEvent_t text_ev[2] = {nullptr, nullptr};
-  char* d_text = nullptr;
-  int64_t* d_tsrc = nullptr;
-  int64_t* d_tdst = nullptr;
-  void* d_tscratch = nullptr;
-  gs::ParseScratch tscratch;
-  int pipe_depth = 1;
-  static constexpr int kLanes = 4;
-  hipStream_t lane[kLanes] = {};
-  hipEvent_t lane_ev[kLanes] = {};
-  hipEvent_t main_ev = nullptr;
-  int lane_next = 0;
-  bool lanes_dirty = false;
-  // side stream (a multi-GPU group's apply stream): folds of remote rows run there,
-  // overlapping this rank's own folds; every reader joins it (join_lanes), the
-  // handle's own folds do not (union commutes)
-  hipStream_t side = nullptr;
-  hipEvent_t side_ev = nullptr;
-  bool side_dirty = false;
-  // profiling
-  bool profiling = false;
-  struct Pending {
-    int kid;
-    hipEvent_t a, b;
-  };
-  std::vector<Pending> prof_pending;
-  std::vector<hipEvent_t> ev_pool;
-  uint64_t launches[KID_N] = {0, 0, 0, 0};
-  double total_ms[KID_N] = {0, 0, 0, 0};
-
-  gs::Table table() const {
-    gs::Table t;
-    t.tab = tab;
-    t.ctr = ctr;
-    t.hotcap = (uint32_t)hotcap;
-    t.hotmask = hotcap ? (uint32_t)(hotcap - 1) : 0u;
-    t.hotshift = hotcap ? 64 - loghot : 0;
-    t.hot_open = hot_open ? 1 : 0;
-    t.cap = (uint32_t)cap;
-    t.mask = (uint32_t)(cap - 1);
-    t.shift = 64 - logcap;
-    t.r0 = (uint32_t)(hotcap + cap);
-    return t;
-  }
-  gs::Lists lists(int set = -1) const {
-    if (set < 0) set = dset;
-    gs::Lists L;
-    L.act = act;
-    L.act_shard_cap = act_shard_cap;
-    L.drec = drec ? drec + (size_t)set * gs::kShards * delta_shard_cap * 3 : nullptr;
-    L.delta_shard_cap = delta_shard_cap;
-    L.dctr = (uint32_t)(gs::CTR_DELTA + set * gs::kShards);
-    return L;
-  }
-};
-
-namespace {
-
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int d) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != d) (void)hipSetDevice(d);
-  }
-  ~DeviceGuard() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
 
 hipEvent_t take_event(gs_summary* h) {
   if (!h->ev_pool.empty()) {
@@ -210,21 +47,22 @@ hipEvent_t take_event(gs_summary* h) {
   return e;
 }
 
-// Bracket one launch with events when profiling.
+// Bracket one launch with events on stream st when profiling.
 struct Prof {
   gs_summary* h;
   int kid;
+  hipStream_t st;
   hipEvent_t a = nullptr;
-  Prof(gs_summary* h_, int k) : h(h_), kid(k) {
+  Prof(gs_summary* h_, int k, hipStream_t s = nullptr) : h(h_), kid(k), st(s ? s : h_->stream) {
     if (h->profiling) {
       a = take_event(h);
-      (void)hipEventRecord(a, h->stream);
+      (void)hipEventRecord(a, st);
     }
   }
   ~Prof() {
     if (h->profiling) {
       hipEvent_t b = take_event(h);
-      (void)hipEventRecord(b, h->stream);
+      (void)hipEventRecord(b, st);
       h->prof_pending.push_back({kid, a, b});
     }
   }
@@ -254,63 +92,58 @@ int join_pipe_lanes(gs_summary* h) {
   return GS_OK;
 }
 
-// can folds be launched on the side stream (plain fused folds, no profiling)
-bool side_ok(const gs_summary* h) {
-  return h->side && h->mode == gs_summary::FUSED && h->hotcap == 0 && !h->profiling;
+// An export into the combine scratch must wait until the last consumer of the
+// previous export (another summary's fold) has read it.
+int wait_x_consumer(gs_summary* h) {
+  if (!h->x_pending) return GS_OK;
+  GS_HIP(hipStreamWaitEvent(h->stream, h->x_used, 0));
+  h->x_pending = false;
+  return GS_OK;
 }
 
-// can a (tracked) fold run on a lane stream of its own (plain fused folds, no profiling)
-bool lane_fold_ok(const gs_summary* h) {
-  return h->pipe_depth >= 2 && h->mode == gs_summary::FUSED && h->hotcap == 0 && !h->profiling;
-}
-
-int join_lanes(gs_summary* h) {
-  if (int rc = join_pipe_lanes(h)) return rc;
-  if (h->side_dirty) {
-    GS_HIP(hipEventRecord(h->side_ev, h->side));
-    GS_HIP(hipStreamWaitEvent(h->stream, h->side_ev, 0));
-    h->side_dirty = false;
+// Combine scratch of at least `rows` rows (v, label, parity), allocated on growth only.
+int ensure_x(gs_summary* h, uint64_t rows) {
+  if (!h->x_cnt) {
+    GS_HIP(hipMalloc(&h->x_cnt, 16));
+    GS_HIP(hipEventCreateWithFlags(&h->x_ready, hipEventDisableTiming));
+    GS_HIP(hipEventCreateWithFlags(&h->x_used, hipEventDisableTiming));
   }
-  return GS_OK;
-}
-
-// Error flags, read with ONE host synchronisation (pinned copies queued behind the
-// handle's work, then a single stream sync).
-int check_device_flags(gs_summary* h) {
-  uint32_t* f = h->h_flags;
-  GS_HIP(hipMemcpyAsync(&f[0], h->ctr + gs::ctr_index(gs::CTR_ERR), 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipMemcpyAsync(&f[1], h->ctr + gs::ctr_index(gs::CTR_OVF), 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
-  if (f[0]) return fail(GS_ERR_CAPACITY, "vertex table overflow (device probe limit)");
-  if (f[1]) return fail(GS_ERR_CAPACITY, "delta/active list overflow: take the delta after each fold");
-  return GS_OK;
-}
-
-int read_nv(gs_summary* h, uint64_t* nv) {
-  if (int rc = join_lanes(h)) return rc;
-  std::vector<uint32_t> c(gs::CTR_COUNT * gs::kCtrStride);
-  GS_HIP(hipMemcpyAsync(c.data(), h->ctr, c.size() * 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
-  uint64_t s = 0;
-  for (int i = 0; i < gs::kShards; ++i) s += c[gs::ctr_index(gs::CTR_NV + i)];
-  *nv = s;
-  return GS_OK;
-}
-
-// After a reset or rebuild: `nv` vertices exactly, no fold in flight (the caller
-// joined every stream), the device's completed-edges counter zeroed with the rest.
-int reset_capacity_tracking(gs_summary* h, uint64_t nv) {
-  if (h->rep) {
-    // reports of earlier folds may still be landing: wait for them, then clear
-    if (h->stream) GS_HIP(hipStreamSynchronize(h->stream));
-    memset(h->rep, 0, gs_summary::kRepRing * 8);
+  if (h->x_cap >= rows) return GS_OK;
+  if (h->x_v) {
+    if (int rc = wait_x_consumer(h)) return rc;
+    GS_HIP(hipStreamSynchronize(h->stream));
+    (void)hipFree(h->x_v);
+    (void)hipFree(h->x_l);
+    (void)hipFree(h->x_p);
+    h->x_v = h->x_l = nullptr;
+    h->x_p = nullptr;
   }
+  const uint64_t c = std::max<uint64_t>(rows, (uint64_t)(kMaxLoad * (double)h->cap) + 2);
+  GS_HIP(hipMalloc(&h->x_v, c * 8));
+  GS_HIP(hipMalloc(&h->x_l, c * 8));
+  GS_HIP(hipMalloc(&h->x_p, c));
+  h->x_cap = c;
+  return GS_OK;
+}
+
+// After a reset or rebuild: `nv` vertices exactly, no fold in flight of this epoch.
+// Reports of earlier folds that land late carry an older epoch tag and are ignored.
+void reset_capacity_tracking(gs_summary* h, uint64_t nv) {
+  h->rep_epoch++;
   h->nv_ub = nv;
   h->nv_exact = nv;
   h->e_exact = 0;
   h->e_launched = 0;
+  h->e_lost = 0;
   for (int i = 0; i < gs_summary::kRepStreams; ++i) h->rep_skip[i] = 0, h->rep_pending[i] = 0;
   h->rep_pending_edges = 0;
+}
+
+int alloc_vlist(gs_summary* h) {
+  (void)hipFree(h->vlist);
+  h->vlist = nullptr;
+  h->vshard_cap = (uint32_t)(h->cap / gs::kShards + 1024);
+  GS_HIP(hipMalloc(&h->vlist, (size_t)gs::kShards * h->vshard_cap * 4));
   return GS_OK;
 }
 
@@ -319,12 +152,8 @@ int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
   h->cap = cap;
   h->logcap = 0;
   while ((1ull << h->logcap) < cap) ++h->logcap;
-  h->loghot = 0;
-  while (h->hotcap && (1ull << h->loghot) < h->hotcap) ++h->loghot;
-  h->hot_open = h->hotcap > 0;
-  h->hot_target = h->hotcap / 2;
-  h->nv_pending = false;
-  GS_HIP(hipMalloc(&h->tab, (h->hotcap + cap + 2) * sizeof(gs::Slot)));
+  GS_HIP(hipMalloc(&h->tab, (cap + 1) * sizeof(gs::Slot)));
+  if (int rc = alloc_vlist(h)) return rc;
   if (keep_delta) {
     GS_HIP(hipMemsetAsync(h->ctr, 0, gs::ctr_index(gs::CTR_DELTA) * 4, h->stream));
     GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 0,
@@ -334,54 +163,11 @@ int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
   }
   {
     Prof p(h, KID_INIT);
-    gs::launch_init(h->tab, h->hotcap + cap + 2, h->stream);
+    gs::launch_init(h->tab, cap + 1, h->stream);
   }
   GS_HIP(hipGetLastError());
+  h->vlist_ok = true;
   reset_capacity_tracking(h, 0);
-  h->epoch = 0;
-  h->pending = -1;
-  return GS_OK;
-}
-
-struct ExchangeLayout {
-  uint32_t rows = 0;  // > 0: gathered exchange buffer, rows per rank
-  int skip_rank = -1;
-  const int64_t* base = nullptr;
-  bool on_side = false;  // launch on h->side (a group's apply stream) instead of h->stream
-};
-int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
-                     size_t stride, size_t w_stride, bool track, bool check_cap = true,
-                     const ExchangeLayout& xl = ExchangeLayout(), bool allow_pipe = false);
-
-// Hook the deferred active edges (DEFER mode) so the forest is complete.
-int flush_hooks(gs_summary* h) {
-  if (h->pending < 0) return GS_OK;
-  {
-    Prof p(h, KID_HOOK);
-    gs::launch_hook(h->kind == GS_KIND_SIGNED, h->pending_track, h->table(), h->lists(), h->pending,
-                    gs::kShards * 16, h->stream);
-  }
-  GS_HIP(hipGetLastError());
-  h->pending = -1;
-  return GS_OK;
-}
-
-// Export every (vertex, label, parity) into device arrays; returns count.
-int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n, int part = 0,
-                       int nparts = 1) {
-  if (int rc = join_lanes(h)) return rc;
-  if (int rc = flush_hooks(h)) return rc;
-  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, h->stream));
-  {
-    Prof pr(h, KID_EXPORT);
-    gs::launch_export(h->kind == GS_KIND_SIGNED, h->table(), v, l, p, cap, h->stream, part, nparts);
-  }
-  GS_HIP(hipGetLastError());
-  uint32_t cnt = 0;
-  GS_HIP(hipMemcpyAsync(&cnt, h->ctr + gs::ctr_index(gs::CTR_EXPORT), 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
-  *n = cnt;
-  if (cnt > cap) return fail(GS_ERR_TRUNCATED, "output capacity " + std::to_string(cap) + " < " + std::to_string(cnt));
   return GS_OK;
 }
 
@@ -394,50 +180,62 @@ int grow(gs_summary* h, uint64_t new_cap) {
   int64_t *v = nullptr, *l = nullptr;
   uint8_t* p = nullptr;
   const size_t m = nv + 1;
-  GS_HIP(hipMalloc(&v, m * 8));
-  GS_HIP(hipMalloc(&l, m * 8));
-  GS_HIP(hipMalloc(&p, m));
+  auto release = [&] {
+    (void)hipFree(v);
+    (void)hipFree(l);
+    (void)hipFree(p);
+  };
+  if (hipMalloc(&v, m * 8) != hipSuccess || hipMalloc(&l, m * 8) != hipSuccess || hipMalloc(&p, m) != hipSuccess) {
+    release();
+    return fail(GS_ERR_HIP, "table rebuild: out of device memory");
+  }
   size_t got = 0;
-  rc = export_device_impl(h, v, l, p, m, &got);
-  if (rc) return rc;
   uint32_t fail_flag = 0;
-  GS_HIP(hipMemcpyAsync(&fail_flag, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
-  GS_HIP(hipFree(h->tab));
+  rc = export_device_impl(h, v, l, p, m, &got);
+  if (!rc && hipMemcpyAsync(&fail_flag, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream) !=
+                 hipSuccess)
+    rc = fail(GS_ERR_HIP, "table rebuild: flag read failed");
+  if (!rc && hipStreamSynchronize(h->stream) != hipSuccess) rc = fail(GS_ERR_HIP, "table rebuild: sync failed");
+  if (rc) {
+    release();
+    return rc;
+  }
+  (void)hipFree(h->tab);
   h->tab = nullptr;
   const bool track = h->track;
   h->track = false;  // the rebuild is not a delta
   rc = alloc_table(h, new_cap, /*keep_delta=*/true);
-  if (rc) return rc;
-  if (fail_flag) GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, h->stream));
-  reset_capacity_tracking(h, got);
-  rc = fold_device_impl(h, v, l, p, got, 1, 1, /*track=*/false, /*check_cap=*/false);
+  if (!rc && fail_flag && hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, h->stream) != hipSuccess)
+    rc = fail(GS_ERR_HIP, "table rebuild: flag write failed");
+  if (!rc && h->changes) rc = change_tracking_reset(h, /*full=*/true);
+  if (!rc) {
+    reset_capacity_tracking(h, got);
+    rc = fold_device_impl(h, v, l, p, got, 1, 1, /*track=*/false, /*check_cap=*/false);
+  }
   h->track = track;
-  if (rc) return rc;
-  GS_HIP(hipStreamSynchronize(h->stream));
-  GS_HIP(hipFree(v));
-  GS_HIP(hipFree(l));
-  GS_HIP(hipFree(p));
-  return GS_OK;
+  if (!rc && hipStreamSynchronize(h->stream) != hipSuccess) rc = fail(GS_ERR_HIP, "table rebuild: sync failed");
+  release();
+  return rc;
 }
 
 // Upper bound of the vertex count once `e_launched` edges have been folded: the
-// last exact count, or any capacity report, plus 2 new vertices per edge not yet
-// covered. Also returns whether every launched fold has reported.
+// last exact count, or any capacity report of this epoch, plus 2 new vertices per
+// edge not covered. Also returns whether every issued report has landed.
 uint64_t capacity_bound(gs_summary* h, bool* all_reported) {
+  const uint64_t m31 = (1ull << 31) - 1;
+  const uint64_t live = h->e_launched - h->e_lost;  // launched edges a report may still claim
   uint64_t best = h->nv_exact + 2 * (h->e_launched - h->e_exact);
   uint64_t max_done = h->e_exact;
   for (int i = 0; i < gs_summary::kRepRing; ++i) {
     const unsigned long long w = __atomic_load_n(&h->rep[i], __ATOMIC_ACQUIRE);
-    if (!w) continue;
-    const uint64_t low = w & ((1ull << 33) - 1), c = w >> 33;
-    const uint64_t behind = (h->e_launched - low) & ((1ull << 33) - 1);  // edges launched after that report
-    if (behind > h->e_launched) continue;  // not from this epoch
+    if (!w || ((w >> 31) & 7u) != (h->rep_epoch & 7u)) continue;
+    const uint64_t low = w & m31, c = w >> 34;
+    const uint64_t behind = (live - low) & m31;  // claimable edges launched after that report
+    if (behind > live) continue;
     best = std::min<uint64_t>(best, c + 2 * behind);
     max_done = std::max<uint64_t>(max_done, h->e_launched - behind);
   }
-  // edges waiting on the handle stream for its next report will not be claimed by
-  // waiting: count them as reported for the decision to stop waiting
+  // edges waiting on a stream for its next report will not be claimed by waiting
   if (all_reported) *all_reported = max_done + h->rep_pending_edges >= h->e_launched;
   return best;
 }
@@ -445,9 +243,9 @@ uint64_t capacity_bound(gs_summary* h, bool* all_reported) {
 int ensure_capacity(gs_summary* h, size_t n) {
   const double limit = kMaxLoad * (double)h->cap;
   bool all = false;
-  // (the ring holds reports of capacity-checked folds only; e_launched counts them)
-  if ((double)(capacity_bound(h, nullptr) + 2 * (uint64_t)n) <= limit) {
-    h->nv_ub = capacity_bound(h, nullptr) + 2 * (uint64_t)n;
+  uint64_t b = capacity_bound(h, nullptr);
+  if ((double)(b + 2 * (uint64_t)n) <= limit) {
+    h->nv_ub = b + 2 * (uint64_t)n;
     h->e_launched += n;
     return GS_OK;
   }
@@ -455,8 +253,9 @@ int ensure_capacity(gs_summary* h, size_t n) {
   h->cap_waits++;
   const auto t0 = std::chrono::steady_clock::now();
   while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200)) {
-    const uint64_t b = capacity_bound(h, &all);
+    b = capacity_bound(h, &all);
     if ((double)(b + 2 * (uint64_t)n) <= limit) {
+      h->cap_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       h->nv_ub = b + 2 * (uint64_t)n;
       h->e_launched += n;
       return GS_OK;
@@ -464,14 +263,19 @@ int ensure_capacity(gs_summary* h, size_t n) {
     if (all) break;
     std::this_thread::yield();
   }
+  h->cap_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   uint64_t nv = 0;
   h->cap_syncs++;
-  int rc = read_nv(h, &nv);  // exact (joins every stream)
+  int rc = read_nv(h, &nv);  // exact (joins every stream: every issued report has landed)
   if (rc) return rc;
   h->nv_exact = nv;
   h->e_exact = h->e_launched;
-  h->rep_pending_edges = 0;  // covered by e_exact (never claimed by a report: ring bounds stay conservative)
+  // edges queued since their stream's last report are complete and counted in nv, but
+  // no report will claim them: keep them out of later reports' "behind" 
+  h->e_lost += h->rep_pending_edges;
+  h->rep_pending_edges = 0;
   for (int i = 0; i < gs_summary::kRepStreams; ++i) h->rep_skip[i] = 0, h->rep_pending[i] = 0;
+  memset(h->rep, 0, gs_summary::kRepRing * 8);  // every report of this epoch has landed
   h->nv_ub = nv + 2 * (uint64_t)n;
   if ((double)h->nv_ub > limit) {
     uint64_t nc = h->cap;
@@ -484,77 +288,110 @@ int ensure_capacity(gs_summary* h, size_t n) {
   return GS_OK;
 }
 
+int check(gs_handle h) {
+  if (!h) return fail(GS_ERR_INVALID, "null handle");
+  return GS_OK;
+}
+
+}  // namespace
+
+bool side_ok(const gs_summary* h) { return h->side && !h->profiling; }
+
+int join_lanes(gs_summary* h) {
+  if (int rc = join_pipe_lanes(h)) return rc;
+  if (h->side_dirty) {
+    GS_HIP(hipEventRecord(h->side_ev, h->side));
+    GS_HIP(hipStreamWaitEvent(h->stream, h->side_ev, 0));
+    h->side_dirty = false;
+  }
+  return GS_OK;
+}
+
+// Error flags, read with ONE host synchronisation. Also refreshes whether the
+// vertex list is complete.
+int check_device_flags(gs_summary* h) {
+  uint32_t* f = h->h_flags;
+  GS_HIP(hipMemcpyAsync(&f[0], h->ctr + gs::ctr_index(gs::CTR_ERR), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipMemcpyAsync(&f[1], h->ctr + gs::ctr_index(gs::CTR_OVF), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipMemcpyAsync(&f[2], h->ctr + gs::ctr_index(gs::CTR_VOVF), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  if (f[2]) h->vlist_ok = false;
+  if (f[0]) return fail(GS_ERR_CAPACITY, "vertex table overflow (device probe limit)");
+  if (f[1]) return fail(GS_ERR_CAPACITY, "delta list overflow: stage or take the delta records after each fold");
+  return GS_OK;
+}
+
+int read_nv(gs_summary* h, uint64_t* nv) {
+  if (int rc = join_lanes(h)) return rc;
+  std::vector<uint32_t> c(gs::CTR_COUNT * gs::kCtrStride);
+  GS_HIP(hipMemcpyAsync(c.data(), h->ctr, c.size() * 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  uint64_t s = 0;
+  for (int i = 0; i < gs::kShards; ++i) s += c[gs::ctr_index(gs::CTR_NV + i)];
+  if (c[gs::ctr_index(gs::CTR_VOVF)]) h->vlist_ok = false;
+  *nv = s;
+  return GS_OK;
+}
+
+// Sparse tables export / reset over the vertex list; dense ones scan the table.
+bool use_vertex_list(gs_summary* h, uint64_t nv_bound) { return h->vlist_ok && nv_bound * 4 < h->cap; }
+
 int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
-                     size_t stride, size_t w_stride, bool track, bool check_cap, const ExchangeLayout& xl,
-                     bool allow_pipe) {
+                     size_t stride, size_t w_stride, bool track, bool check_cap, const FoldSource& fs) {
   if (n == 0) return GS_OK;
-  // Capacity units (each may add 2 vertices): one per edge, or for a gathered exchange
-  // buffer one per record row of the ranks actually folded -- the header rows, the
-  // skipped (own) block and the padding past each header's count add no vertex. The
-  // valid rows may sit in any chunk, so an exchange fold claims all its units with
-  // its last chunk's report.
-  uint64_t units = n;
-  if (xl.rows) {
-    const uint64_t blocks = n / xl.rows;
-    const uint64_t folded = blocks - (xl.skip_rank >= 0 && (uint64_t)xl.skip_rank < blocks ? 1 : 0);
-    units = folded * (xl.rows - 1);
-  }
+  // Capacity units (each may add 2 vertices): one per edge, or for a gathered
+  // exchange buffer the caller's count of live rows it will fold. The valid rows may
+  // sit in any chunk, so an exchange fold claims all its units with its last chunk.
+  const uint64_t units = fs.rows ? fs.units : n;
   if (check_cap && units) {
-    int rc = ensure_capacity(h, units);
-    if (rc) return rc;
+    if (int rc = ensure_capacity(h, units)) return rc;
   }
-  // Pipelined: plain fused folds (no delta tracking, no exchange layout, no hot
-  // level, not profiling) may overlap the previous fold. Union is associative and
-  // commutative, so the forest after both is the same; readers join the lanes.
-  // A group's own tracked fold may be forced onto a lane (h->force_lane): it records
-  // into its own delta set, staged on the same lane, so the next fold overlaps it.
-  const bool forced = h->force_lane >= 0 && xl.rows == 0 && lane_fold_ok(h);
-  const bool pipe = forced || (allow_pipe && h->pipe_depth > 1 && h->mode == gs_summary::FUSED && !track &&
-                               xl.rows == 0 && h->hotcap == 0 && !h->profiling);
+  // Pipelined: plain folds (no delta tracking, no exchange layout, not profiling) may
+  // overlap the previous fold. Union is associative and commutative, so the forest
+  // after both is the same; readers join the lanes.
+  const bool pipe = fs.allow_pipe && h->pipe_depth > 1 && !track && fs.rows == 0 && !h->profiling && !h->changes;
   // remote rows of a group exchange: on the side stream, overlapping own folds
-  const bool side = xl.on_side && side_ok(h) && !track;
+  const bool side = fs.on_side && side_ok(h) && !track;
   if (!pipe && !side) {
     if (int rc = join_pipe_lanes(h)) return rc;  // the side stream is NOT joined: union commutes
   }
   const bool sign = h->kind == GS_KIND_SIGNED;
   for (size_t off = 0; off < n; off += kMaxChunk) {
     const uint32_t c = (uint32_t)std::min<size_t>(kMaxChunk, n - off);
-    const uint32_t per_block = gs::kFoldBS * (uint32_t)h->ept;
-    const uint32_t blocks = (c + per_block - 1) / per_block;
-    const uint32_t per_shard_edges = ((blocks + gs::kShards - 1) / gs::kShards) * per_block;
+    const uint32_t blocks = (c + gs::kFoldBS - 1) / gs::kFoldBS;
     if (track) {
-      h->delta_fill_ub[h->dset] += (uint64_t)per_shard_edges * 3;
-      if (h->delta_fill_ub[h->dset] > h->delta_shard_cap)
-        return fail(GS_ERR_CAPACITY, "delta list full: call gs_take_delta_records after each fold of <= 2^22 edges");
-    }
-    const int cur = (int)(h->epoch % gs::kActSets);
-    const int zero = (int)((h->epoch + 1) % gs::kActSets);
-    const int inline_max = h->mode == gs_summary::FUSED ? 64 : (h->mode == gs_summary::COMPACT ? 0 : h->inline_max);
-    const int drain = h->mode == gs_summary::DEFER ? h->pending : -1;
-    if (h->hot_open && h->nv_pending && hipEventQuery(h->nv_ev) == hipSuccess) {
-      uint64_t nv = 0;
-      for (int i = 0; i < gs::kShards; ++i) nv += h->h_nv[gs::ctr_index(gs::CTR_NV + i)];
-      h->nv_pending = false;
-      if (nv >= h->hot_target) h->hot_open = false;
+      h->delta_fill_ub += per_shard_edges(c);
+      if (!h->drec || h->delta_fill_ub > h->delta_shard_cap)
+        return fail(GS_ERR_CAPACITY, "delta list full: stage or take the delta records after at most " +
+                                         std::to_string(h->delta_edges) + " folded edges");
     }
     hipStream_t st = side ? h->side : h->stream;
     if (side) h->side_dirty = true;
     if (pipe) {  // the lane waits for the caller's work on the handle stream, not for the other lane
       GS_HIP(hipEventRecord(h->main_ev, h->stream));
-      if (forced) {
-        st = h->lane[h->force_lane];
-      } else {
-        st = h->lane[h->lane_next];
-        h->lane_next = (h->lane_next + 1) % h->pipe_depth;
-      }
+      st = h->lane[h->lane_next];
+      h->lane_next = (h->lane_next + 1) % h->pipe_depth;
       GS_HIP(hipStreamWaitEvent(st, h->main_ev, 0));
       h->lanes_dirty = true;
     }
+    gs::FoldLaunch f;
+    f.src = src + off * stride;
+    f.dst = dst + off * stride;
+    f.w = w ? w + off * w_stride : nullptr;
+    f.n = c;
+    f.stride = (uint32_t)stride;
+    f.w_stride = (uint32_t)w_stride;
+    f.rows = fs.rows;
+    f.skip_rank = fs.skip_rank;
+    f.counts = fs.counts;
+    f.base = (uint32_t)off;
+    f.n_dev = fs.n_dev;
+    f.fail_in = off == 0 ? fs.fail_in : nullptr;
+    f.shard0 = h->shard0;
+    h->shard0 = (h->shard0 + blocks) & (gs::kShards - 1);
     {
-      Prof p(h, KID_FOLD);
-      gs::launch_fold(sign, track, h->ept, h->table(), h->lists(), src + off * stride, dst + off * stride,
-                      w ? w + off * w_stride : nullptr, c, (uint32_t)stride, (uint32_t)w_stride, cur, drain, zero,
-                      inline_max, xl.rows, xl.skip_rank, xl.base, (uint32_t)off, st);
+      Prof p(h, KID_FOLD, st);
+      gs::launch_fold(sign, track, h->table(), h->delta(), f, st);
     }
     GS_HIP(hipGetLastError());
     if (check_cap && units) {
@@ -567,7 +404,7 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       if (st == h->side) rs = gs_summary::kRepStreams - 1;
       for (int i = 0; i < gs_summary::kLanes; ++i)
         if (st == h->lane[i]) rs = 1 + i;
-      const uint64_t cu = xl.rows ? (off + c >= n ? units : 0) : c;
+      const uint64_t cu = fs.rows ? (off + c >= n ? units : 0) : c;
       h->rep_pending[rs] += cu;
       h->rep_pending_edges += cu;
       // off the handle stream a report is not a gap between folds: report every chunk
@@ -575,47 +412,78 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       const bool tight = rs != 0 && (double)(h->nv_ub + 4ull * gs_summary::kRepEvery * c) > kMaxLoad * (double)h->cap;
       if (++h->rep_skip[rs] >= gs_summary::kRepEvery || tight) {
         const uint64_t claim = h->rep_pending[rs];
-        gs::launch_report(h->ctr, claim, h->rep_dev + (h->rep_seq++ % gs_summary::kRepRing), st);
+        gs::launch_report(h->ctr, claim, h->rep_dev + (h->rep_seq++ % gs_summary::kRepRing),
+                          (unsigned)(h->rep_epoch & 7u), st);
         GS_HIP(hipGetLastError());
         h->rep_pending_edges -= claim;
         h->rep_pending[rs] = 0;
         h->rep_skip[rs] = 0;
       }
     }
-    if (h->hot_open && !h->nv_pending) {  // vertex count for the next hot-level decision
-      GS_HIP(hipMemcpyAsync(h->h_nv, h->ctr + gs::ctr_index(gs::CTR_NV), gs::kShards * gs::kCtrStride * 4,
-                            hipMemcpyDeviceToHost, h->stream));
-      GS_HIP(hipEventRecord(h->nv_ev, h->stream));
-      h->nv_pending = true;
-    }
-    h->epoch++;
-    h->pending = h->mode == gs_summary::FUSED ? -1 : cur;
-    h->pending_track = track;
-    if (h->mode == gs_summary::COMPACT) {
-      const int sub = (int)std::min<uint32_t>((blocks + gs::kShards - 1) / gs::kShards, 16u);
-      {
-        Prof p(h, KID_HOOK);
-        gs::launch_hook(sign, track, h->table(), h->lists(), cur, gs::kShards * sub, h->stream);
-      }
-      GS_HIP(hipGetLastError());
-      h->pending = -1;
-    }
   }
   return GS_OK;
 }
 
-int check(gs_handle h) {
-  if (!h) return fail(GS_ERR_INVALID, "null handle");
+// Export every (vertex, label, parity) into device arrays; returns the count.
+int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n, int part,
+                       int nparts) {
+  if (int rc = join_lanes(h)) return rc;
+  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, h->stream));
+  {
+    Prof pr(h, KID_EXPORT);
+    if (nparts == 1 && use_vertex_list(h, h->nv_ub))
+      gs::launch_export_list(h->table(), v, l, p, cap, h->nv_ub, h->stream);
+    else
+      gs::launch_export(h->table(), v, l, p, cap, h->stream, part, nparts);
+  }
+  GS_HIP(hipGetLastError());
+  uint32_t cnt = 0;
+  GS_HIP(hipMemcpyAsync(&cnt, h->ctr + gs::ctr_index(gs::CTR_EXPORT), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  *n = cnt;
+  if (cnt > cap) return fail(GS_ERR_TRUNCATED, "output capacity " + std::to_string(cap) + " < " + std::to_string(cnt));
   return GS_OK;
 }
 
-}  // namespace
+int ensure_delta_list(gs_summary* h, uint64_t edges) {
+  edges = std::max<uint64_t>(edges, kMaxChunk);
+  if (h->drec && edges <= h->delta_edges) return GS_OK;
+  uint64_t per = 256;  // slack
+  for (uint64_t off = 0; off < edges; off += kMaxChunk) per += per_shard_edges(std::min<uint64_t>(kMaxChunk, edges - off));
+  if (per > 0xFFFFFFFFull) return fail(GS_ERR_INVALID, "delta list too large");
+  if (h->drec) {
+    GS_HIP(hipStreamSynchronize(h->stream));
+    (void)hipFree(h->drec);
+    h->drec = nullptr;
+  }
+  GS_HIP(hipMalloc(&h->drec, (size_t)gs::kShards * per * 24));
+  h->delta_shard_cap = (uint32_t)per;
+  h->delta_edges = edges;
+  return GS_OK;
+}
+
+int stage_delta(gs_summary* h, int64_t* out, uint64_t cap, int width, unsigned long long* count_out, bool with_fail,
+                hipStream_t st) {
+  if (!h->drec) return fail(GS_ERR_INVALID, "delta tracking was never enabled");
+  st = st ? st : h->stream;
+  {
+    Prof p(h, KID_STAGE, st);
+    gs::launch_stage(h->table(), h->delta(), out, cap, width, count_out, with_fail, st);
+  }
+  GS_HIP(hipGetLastError());
+  h->delta_fill_ub = 0;
+  return GS_OK;
+}
+
+}  // namespace gsi
+
+using namespace gsi;
 
 extern "C" {
 
 const char* gs_last_error(void) { return g_err.c_str(); }
 
-int gs_version(void) { return 100; }
+int gs_version(void) { return 20000; }
 
 int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   if (!out) return fail(GS_ERR_INVALID, "out is null");
@@ -628,23 +496,8 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   gs_summary* h = new gs_summary();
   h->device = device;
   h->kind = kind;
-  if (const char* m = getenv("GS_HOOK_MODE")) {
-    if (!strcmp(m, "defer")) h->mode = gs_summary::DEFER;
-    if (!strcmp(m, "compact")) h->mode = gs_summary::COMPACT;
-  }
-  if (const char* m = getenv("GS_INLINE_MAX")) h->inline_max = std::max(0, std::min(64, atoi(m)));
-  if (const char* m = getenv("GS_EPT")) h->ept = atoi(m) == 2 ? 2 : 1;
-  // hot level (opt-in, GS_HOT_LOG2 = log2 slots): measured slower on RMAT-26 at every
-  // size from 2^16 to 2^23 slots, so it is off by default
-  {
-    if (const char* m = getenv("GS_HOT_LOG2")) {
-      const int lg = atoi(m);
-      h->hotcap = (lg > 0 && lg <= 26) ? (1ull << lg) : 0;
-    }
-  }
   uint64_t cap = next_pow2(std::max<uint64_t>(2 * std::max<uint64_t>(capacity_hint, 1), 1024));
   if (cap > kMaxCap) cap = kMaxCap;
-  int rc = GS_OK;
   auto bail = [&](int code) {
     gs_destroy(h);
     return code;
@@ -653,14 +506,12 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
     return bail(fail(GS_ERR_HIP, "hipStreamCreate failed"));
   if (hipMalloc(&h->ctr, gs::CTR_COUNT * gs::kCtrStride * 4) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipMalloc(counters) failed"));
-  h->act_shard_cap = ((kMaxChunk / 256 + gs::kShards - 1) / gs::kShards) * 256;
-  if (hipMalloc(&h->act, sizeof(uint2) * gs::kActSets * gs::kShards * (size_t)h->act_shard_cap) != hipSuccess)
-    return bail(fail(GS_ERR_HIP, "hipMalloc(active list) failed"));
   if (hipMalloc(&h->d_stage, sizeof(int64_t) * 4 * kStageChunk) != hipSuccess ||
       hipMalloc(&h->d_wstage, 2 * kStageChunk) != hipSuccess || hipMalloc(&h->d_scratch, 64) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipMalloc(staging) failed"));
   if (hipHostMalloc(&h->h_stage, sizeof(int64_t) * 4 * kStageChunk, hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&h->h_wstage, 2 * kStageChunk, hipHostMallocDefault) != hipSuccess)
+      hipHostMalloc(&h->h_wstage, 2 * kStageChunk, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&h->h_flags, 16, hipHostMallocDefault) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipHostMalloc(staging) failed"));
   for (int i = 0; i < 2; ++i)
     if (hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming) != hipSuccess)
@@ -675,12 +526,7 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
       hipHostGetDevicePointer(reinterpret_cast<void**>(&h->rep_dev), h->rep, 0) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "capacity report buffer allocation failed"));
   memset(h->rep, 0, gs_summary::kRepRing * 8);
-  if (hipEventCreateWithFlags(&h->nv_ev, hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc(&h->h_nv, gs::kShards * gs::kCtrStride * 4, hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&h->h_flags, 16, hipHostMallocDefault) != hipSuccess)
-    return bail(fail(GS_ERR_HIP, "hot-level bookkeeping allocation failed"));
-  rc = alloc_table(h, cap);
-  if (rc) return bail(rc);
+  if (int rc = alloc_table(h, cap)) return bail(rc);
   if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "init failed"));
   *out = h;
   return GS_OK;
@@ -698,32 +544,23 @@ int gs_destroy(gs_handle h) {
   }
   if (h->main_ev) (void)hipEventDestroy(h->main_ev);
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
     if (h->stage_ev[i]) (void)hipEventDestroy(h->stage_ev[i]);
-  if (h->nv_ev) (void)hipEventDestroy(h->nv_ev);
-  if (h->h_nv) (void)hipHostFree(h->h_nv);
+    if (h->text_ev[i]) (void)hipEventDestroy(h->text_ev[i]);
+  }
+  if (h->x_ready) (void)hipEventDestroy(h->x_ready);
+  if (h->x_used) (void)hipEventDestroy(h->x_used);
   if (h->rep) (void)hipHostFree(h->rep);
   if (h->h_flags) (void)hipHostFree(h->h_flags);
   if (h->h_text) (void)hipHostFree(h->h_text);
   if (h->h_tres) (void)hipHostFree(h->h_tres);
-  for (int i = 0; i < 2; ++i)
-    if (h->text_ev[i]) (void)hipEventDestroy(h->text_ev[i]);
-  (void)hipFree(h->d_text);
-  (void)hipFree(h->d_tsrc);
-  (void)hipFree(h->d_tdst);
-  (void)hipFree(h->d_tscratch);
-  (void)hipFree(h->tab);
-  (void)hipFree(h->ctr);
-  (void)hipFree(h->act);
-  (void)hipFree(h->drec);
-  (void)hipFree(h->q[0]);
-  (void)hipFree(h->q[1]);
-  (void)hipFree(h->qn);
-  (void)hipFree(h->d_stage);
-  (void)hipFree(h->d_wstage);
-  (void)hipFree(h->d_scratch);
   if (h->h_stage) (void)hipHostFree(h->h_stage);
   if (h->h_wstage) (void)hipHostFree(h->h_wstage);
+  for (void* p : {(void*)h->d_text, (void*)h->d_tsrc, (void*)h->d_tdst, h->d_tscratch, (void*)h->tab, (void*)h->ctr,
+                  (void*)h->vlist, (void*)h->drec, (void*)h->nxt, (void*)h->chg_scratch, (void*)h->d_stage,
+                  (void*)h->d_wstage, (void*)h->d_scratch, (void*)h->x_v, (void*)h->x_l, (void*)h->x_p,
+                  (void*)h->x_cnt})
+    (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return GS_OK;
@@ -733,19 +570,21 @@ int gs_reset(gs_handle h) {
   if (int rc = check(h)) return rc;
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
   {
     Prof p(h, KID_INIT);
-    gs::launch_init(h->tab, h->hotcap + h->cap + 2, h->stream);
+    if (use_vertex_list(h, h->nv_ub)) {  // O(vertices): only the touched slots (no host sync)
+      gs::launch_reset_list(h->table(), h->nxt, h->nv_ub, h->stream);
+    } else {
+      gs::launch_init(h->tab, h->cap + 1, h->stream);
+    }
   }
-  h->hot_open = h->hotcap > 0;
-  h->nv_pending = false;
   GS_HIP(hipGetLastError());
-  if (h->qn) GS_HIP(hipMemsetAsync(h->qn, 0, 16, h->stream));
-  if (int rc = reset_capacity_tracking(h, 0)) return rc;
-  h->epoch = 0;
-  h->pending = -1;
-  h->delta_fill_ub[0] = h->delta_fill_ub[1] = 0;
+  if (h->changes && !use_vertex_list(h, h->nv_ub))
+    if (int rc = change_tracking_reset(h, /*full=*/false)) return rc;
+  GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
+  h->vlist_ok = true;
+  reset_capacity_tracking(h, 0);
+  h->delta_fill_ub = 0;
   return GS_OK;
 }
 
@@ -787,7 +626,9 @@ int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const ui
   if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
   if (stride == 0) return fail(GS_ERR_INVALID, "stride must be >= 1");
   DeviceGuard g(h->device);
-  return fold_device_impl(h, src, dst, w, n, stride, 1, h->track, true, ExchangeLayout(), /*allow_pipe=*/true);
+  FoldSource fs;
+  fs.allow_pipe = true;
+  return fold_device_impl(h, src, dst, w, n, stride, 1, h->track, true, fs);
 }
 
 int gs_fold_records_device(gs_handle h, const int64_t* rec, size_t n, int track) {
@@ -803,7 +644,6 @@ int gs_sync(gs_handle h) {
   if (int rc = check(h)) return rc;
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  if (int rc = flush_hooks(h)) return rc;
   return check_device_flags(h);  // its one stream sync completes all queued work
 }
 
@@ -811,7 +651,6 @@ int gs_num_vertices(gs_handle h, uint64_t* n) {
   if (int rc = check(h)) return rc;
   if (!n) return fail(GS_ERR_INVALID, "n is null");
   DeviceGuard g(h->device);
-  if (int rc_ = join_lanes(h)) return rc_;
   int rc = read_nv(h, n);
   if (rc) return rc;
   return check_device_flags(h);
@@ -822,7 +661,6 @@ int gs_find(gs_handle h, int64_t v, int64_t* label, int* found) {
   if (!label || !found) return fail(GS_ERR_INVALID, "null output");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  if (int rc = flush_hooks(h)) return rc;
   gs::launch_find_one(h->table(), v, h->d_scratch, h->stream);
   GS_HIP(hipGetLastError());
   int64_t out[2];
@@ -833,11 +671,21 @@ int gs_find(gs_handle h, int64_t v, int64_t* label, int* found) {
   return GS_OK;
 }
 
+int gs_find_labels_device(gs_handle h, const int64_t* v, size_t n, int64_t* label, uint8_t* found) {
+  if (int rc = check(h)) return rc;
+  if (n && (!v || !label)) return fail(GS_ERR_INVALID, "null arrays");
+  DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
+  if (!n) return GS_OK;
+  gs::launch_find_batch(h->table(), v, n, label, found, nullptr, h->stream);
+  GS_HIP(hipGetLastError());
+  return GS_OK;
+}
+
 int gs_export_labels_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* parity, size_t cap, size_t* n) {
   if (int rc = check(h)) return rc;
   if (!n) return fail(GS_ERR_INVALID, "n is null");
   DeviceGuard g(h->device);
-  if (int rc_ = join_lanes(h)) return rc_;
   return export_device_impl(h, v, label, parity, cap, n);
 }
 
@@ -847,10 +695,10 @@ int gs_export_labels_part_device(gs_handle h, int part, int nparts, int64_t* v, 
   if (!n) return fail(GS_ERR_INVALID, "n is null");
   if (nparts < 1 || part < 0 || part >= nparts) return fail(GS_ERR_INVALID, "bad part");
   DeviceGuard g(h->device);
-  if (int rc_ = join_lanes(h)) return rc_;
   return export_device_impl(h, v, label, parity, cap, n, part, nparts);
 }
 
+// Export to host arrays through the combine scratch (no allocation per call).
 static int export_host(gs_handle h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n) {
   uint64_t nv = 0;
   int rc = read_nv(h, &nv);
@@ -858,31 +706,23 @@ static int export_host(gs_handle h, int64_t* v, int64_t* l, uint8_t* p, size_t c
   *n = nv;
   if (cap < nv) return fail(GS_ERR_TRUNCATED, "output capacity " + std::to_string(cap) + " < " + std::to_string(nv));
   if (nv == 0) return GS_OK;
-  int64_t *dv = nullptr, *dl = nullptr;
-  uint8_t* dp = nullptr;
-  GS_HIP(hipMalloc(&dv, nv * 8));
-  GS_HIP(hipMalloc(&dl, nv * 8));
-  GS_HIP(hipMalloc(&dp, nv));
+  if ((rc = ensure_x(h, nv + 1))) return rc;
+  if ((rc = wait_x_consumer(h))) return rc;
   size_t got = 0;
-  rc = export_device_impl(h, dv, dl, dp, nv, &got);
-  if (rc == GS_OK) {
-    if (v) GS_HIP(hipMemcpyAsync(v, dv, got * 8, hipMemcpyDeviceToHost, h->stream));
-    if (l) GS_HIP(hipMemcpyAsync(l, dl, got * 8, hipMemcpyDeviceToHost, h->stream));
-    if (p) GS_HIP(hipMemcpyAsync(p, dp, got, hipMemcpyDeviceToHost, h->stream));
-    GS_HIP(hipStreamSynchronize(h->stream));
-    *n = got;
-  }
-  (void)hipFree(dv);
-  (void)hipFree(dl);
-  (void)hipFree(dp);
-  return rc;
+  rc = export_device_impl(h, h->x_v, h->x_l, h->x_p, h->x_cap, &got);
+  if (rc) return rc;
+  if (v) GS_HIP(hipMemcpyAsync(v, h->x_v, got * 8, hipMemcpyDeviceToHost, h->stream));
+  if (l) GS_HIP(hipMemcpyAsync(l, h->x_l, got * 8, hipMemcpyDeviceToHost, h->stream));
+  if (p) GS_HIP(hipMemcpyAsync(p, h->x_p, got, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  *n = got;
+  return GS_OK;
 }
 
 int gs_export_labels(gs_handle h, int64_t* v, int64_t* label, size_t cap, size_t* n) {
   if (int rc = check(h)) return rc;
   if (!n) return fail(GS_ERR_INVALID, "n is null");
   DeviceGuard g(h->device);
-  if (int rc_ = join_lanes(h)) return rc_;
   return export_host(h, v, label, nullptr, cap, n);
 }
 
@@ -891,7 +731,6 @@ int gs_bip_status(gs_handle h, int* ok) {
   if (!ok) return fail(GS_ERR_INVALID, "ok is null");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  if (int rc = flush_hooks(h)) return rc;
   uint32_t f = 0;
   GS_HIP(hipMemcpyAsync(&f, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream));
   GS_HIP(hipStreamSynchronize(h->stream));
@@ -910,7 +749,6 @@ int gs_export_colouring(gs_handle h, int64_t* comp, int64_t* v, uint8_t* sign, s
     return GS_OK;
   }
   DeviceGuard g(h->device);
-  if (int rc_ = join_lanes(h)) return rc_;
   rc = export_host(h, v, comp, sign, cap, n);
   if (rc) return rc;
   if (sign)
@@ -918,59 +756,66 @@ int gs_export_colouring(gs_handle h, int64_t* comp, int64_t* v, uint8_t* sign, s
   return GS_OK;
 }
 
+// CombineCC.reduce / combineFunction.reduce: export `src` into its own scratch on
+// its stream (O(vertices) over the vertex list of a sparse table), then fold those
+// rows into `dst` on dst's stream behind an event. The fold reads the exported
+// count and src's verdict on the device: no host synchronisation and no allocation
+// once the scratch is sized.
 int gs_combine(gs_handle dst, gs_handle src) {
   if (int rc = check(dst)) return rc;
   if (int rc = check(src)) return rc;
   if (dst == src) return GS_OK;
   if (dst->kind != src->kind) return fail(GS_ERR_INVALID, "summaries of different kinds");
-  uint64_t nv = 0;
-  int64_t *sv = nullptr, *sl = nullptr;
-  uint8_t* sp = nullptr;
-  size_t got = 0;
-  uint32_t sfail = 0;
+  const bool sign = dst->kind == GS_KIND_SIGNED;
+  uint64_t bound = 0;
   {
     DeviceGuard g(src->device);
-    if (int rc_ = join_lanes(src)) return rc_;
-    int rc = read_nv(src, &nv);
-    if (rc) return rc;
-    GS_HIP(hipMemcpyAsync(&sfail, src->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, src->stream));
-    GS_HIP(hipStreamSynchronize(src->stream));
-    if (nv) {
-      GS_HIP(hipMalloc(&sv, nv * 8));
-      GS_HIP(hipMalloc(&sl, nv * 8));
-      GS_HIP(hipMalloc(&sp, nv));
-      rc = export_device_impl(src, sv, sl, sp, nv, &got);
-      if (rc) return rc;
+    if (int rc = join_lanes(src)) return rc;
+    bound = std::min<uint64_t>(src->nv_ub, src->cap + 1);
+    if (int rc = ensure_x(src, bound + 1)) return rc;
+    if (int rc = wait_x_consumer(src)) return rc;
+    GS_HIP(hipMemsetAsync(src->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, src->stream));
+    GS_HIP(hipMemsetAsync(src->x_cnt, 0, 16, src->stream));
+    {
+      Prof pr(src, KID_EXPORT);
+      if (use_vertex_list(src, bound))
+        gs::launch_export_list(src->table(), src->x_v, src->x_l, src->x_p, src->x_cap, bound, src->stream);
+      else
+        gs::launch_export(src->table(), src->x_v, src->x_l, src->x_p, src->x_cap, src->stream);
     }
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(src->x_cnt, src->ctr + gs::ctr_index(gs::CTR_EXPORT), 4, hipMemcpyDeviceToDevice,
+                          src->stream));
+    GS_HIP(hipMemcpyAsync(src->x_cnt + 1, src->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToDevice,
+                          src->stream));
+    GS_HIP(hipEventRecord(src->x_ready, src->stream));
   }
   DeviceGuard g(dst->device);
-  if (int rc_ = join_lanes(dst)) return rc_;
-  int rc = GS_OK;
-  if (sfail) {
-    GS_HIP(hipMemsetAsync(dst->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, dst->stream));
-  } else if (got) {
-    int64_t *dv = sv, *dl = sl;
-    uint8_t* dp = sp;
-    if (dst->device != src->device) {
-      GS_HIP(hipMalloc(&dv, got * 8));
-      GS_HIP(hipMalloc(&dl, got * 8));
-      GS_HIP(hipMalloc(&dp, got));
-      GS_HIP(hipMemcpyPeerAsync(dv, dst->device, sv, src->device, got * 8, dst->stream));
-      GS_HIP(hipMemcpyPeerAsync(dl, dst->device, sl, src->device, got * 8, dst->stream));
-      GS_HIP(hipMemcpyPeerAsync(dp, dst->device, sp, src->device, got, dst->stream));
+  if (int rc = join_lanes(dst)) return rc;
+  GS_HIP(hipStreamWaitEvent(dst->stream, src->x_ready, 0));
+  gs_summary* rows = src;
+  if (dst->device != src->device) {  // rows to dst's own scratch over xGMI
+    if (int rc = ensure_x(dst, bound + 1)) return rc;
+    if (int rc = wait_x_consumer(dst)) return rc;
+    GS_HIP(hipMemcpyPeerAsync(dst->x_cnt, dst->device, src->x_cnt, src->device, 16, dst->stream));
+    if (bound) {
+      GS_HIP(hipMemcpyPeerAsync(dst->x_v, dst->device, src->x_v, src->device, bound * 8, dst->stream));
+      GS_HIP(hipMemcpyPeerAsync(dst->x_l, dst->device, src->x_l, src->device, bound * 8, dst->stream));
+      GS_HIP(hipMemcpyPeerAsync(dst->x_p, dst->device, src->x_p, src->device, bound, dst->stream));
     }
-    rc = fold_device_impl(dst, dv, dl, dp, got, 1, 1, dst->track);
-    GS_HIP(hipStreamSynchronize(dst->stream));
-    if (dv != sv) {
-      (void)hipFree(dv);
-      (void)hipFree(dl);
-      (void)hipFree(dp);
-    }
+    GS_HIP(hipEventRecord(src->x_used, dst->stream));  // src's scratch is free again
+    src->x_pending = true;
+    rows = dst;
   }
-  (void)hipFree(sv);
-  (void)hipFree(sl);
-  (void)hipFree(sp);
-  return rc;
+  FoldSource fs;
+  fs.n_dev = rows->x_cnt;
+  fs.fail_in = sign ? reinterpret_cast<const uint32_t*>(rows->x_cnt + 1) : nullptr;
+  // at least one thread reads the verdict of an empty failed summary (Candidates(false))
+  const size_t n = std::max<uint64_t>(bound, sign ? 1 : 0);
+  if (int rc = fold_device_impl(dst, rows->x_v, rows->x_l, rows->x_p, n, 1, 1, dst->track, true, fs)) return rc;
+  GS_HIP(hipEventRecord(rows->x_used, dst->stream));
+  rows->x_pending = true;
+  return GS_OK;
 }
 
 int gs_combine_exported_device(gs_handle h, const int64_t* v, const int64_t* label, const uint8_t* parity, size_t n,
@@ -992,7 +837,6 @@ int gs_serialize(gs_handle h, void* buf, size_t cap, size_t* len) {
   if (int rc = check(h)) return rc;
   if (!len) return fail(GS_ERR_INVALID, "len is null");
   DeviceGuard g(h->device);
-  if (int rc_ = join_lanes(h)) return rc_;
   uint64_t nv = 0;
   int rc = read_nv(h, &nv);
   if (rc) return rc;
@@ -1036,7 +880,6 @@ int gs_deserialize(gs_handle h, const void* buf, size_t len) {
   int rc = gs_reset(h);
   if (rc) return rc;
   DeviceGuard g(h->device);
-  if (int rc_ = join_lanes(h)) return rc_;
   if (!hdr[2]) {
     GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, h->stream));
     return gs_sync(h);
@@ -1053,43 +896,18 @@ int gs_set_delta_tracking(gs_handle h, int on) {
   if (int rc = check(h)) return rc;
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  if (int rc = flush_hooks(h)) return rc;  // deferred hooks belong to the previous tracking state
-  if (on && !h->drec) {
-    // worst case between two takes: one fold chunk of kMaxChunk edges
-    h->delta_shard_cap = ((kMaxChunk / 256 + gs::kShards - 1) / gs::kShards) * 256 * 3;
-    const size_t m = (size_t)gs::kShards * h->delta_shard_cap;
-    GS_HIP(hipMalloc(&h->drec, 2 * m * 24));
-  }
-  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, 2 * gs::kShards * gs::kCtrStride * 4, h->stream));
-  if (h->qn) GS_HIP(hipMemsetAsync(h->qn, 0, 16, h->stream));
-  h->delta_fill_ub[0] = h->delta_fill_ub[1] = 0;
-  h->dset = 0;
+  if (on)
+    if (int rc = ensure_delta_list(h, kMaxChunk)) return rc;
+  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, gs::kShards * gs::kCtrStride * 4, h->stream));
+  h->delta_fill_ub = 0;
   h->track = on != 0;
   return GS_OK;
 }
 
-static int ensure_queue(gs_summary* h) {
-  if (h->q[0]) return GS_OK;
-  h->qcap = (uint64_t)gs::kShards * h->delta_shard_cap;  // one full delta list
-  GS_HIP(hipMalloc(&h->q[0], h->qcap * 24));
-  GS_HIP(hipMalloc(&h->q[1], h->qcap * 24));
-  GS_HIP(hipMalloc(&h->qn, 16));
-  GS_HIP(hipMemsetAsync(h->qn, 0, 16, h->stream));
-  h->qsel = 0;
-  return GS_OK;
-}
-
-// backlog q[qsel] + delta set `set` -> send rows (first cap) and q[qsel ^ 1] (the
-// rest), on stream st (default: the handle's stream). Stages must run in queue order.
-static int stage(gs_summary* h, int64_t* send, uint64_t cap, int width = 3, hipStream_t st = nullptr, int set = 0) {
-  if (int rc = flush_hooks(h)) return rc;
-  if (int rc = ensure_queue(h)) return rc;
-  const int a = h->qsel, b = h->qsel ^ 1;
-  gs::launch_stage(h->table(), h->lists(set), h->q[a], h->qn + a, h->q[b], h->qn + b, h->qcap, send, cap,
-                   st ? st : h->stream, nullptr, width);
-  GS_HIP(hipGetLastError());
-  h->qsel = b;
-  h->delta_fill_ub[set] = 0;
+int gs_delta_capacity(gs_handle h, uint64_t* rows) {
+  if (int rc = check(h)) return rc;
+  if (!rows) return fail(GS_ERR_INVALID, "rows is null");
+  *rows = (uint64_t)gs::kShards * h->delta_shard_cap;
   return GS_OK;
 }
 
@@ -1099,39 +917,37 @@ int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count
   if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  // one launch: backlog + fresh delta straight into rec (first cap), total -> *count
-  if (int rc = flush_hooks(h)) return rc;
-  if (int rc = ensure_queue(h)) return rc;
-  const int a = h->qsel, b = h->qsel ^ 1;
-  gs::launch_stage(h->table(), h->lists(0), h->q[a], h->qn + a, h->q[b], h->qn + b, h->qcap, rec, cap, h->stream,
-                   reinterpret_cast<unsigned long long*>(count));
-  GS_HIP(hipGetLastError());
-  h->qsel = b;
-  h->delta_fill_ub[0] = 0;
-  return GS_OK;
+  return stage_delta(h, rec, cap, 3, reinterpret_cast<unsigned long long*>(count), false);
 }
 
-int gs_delta_stage(gs_handle h, int64_t* send, size_t cap) {
+int gs_delta_stage(gs_handle h, int64_t* send, size_t cap, int width, uint64_t* count) {
   if (int rc = check(h)) return rc;
-  if (!send) return fail(GS_ERR_INVALID, "send is null");
+  if (!send || !count) return fail(GS_ERR_INVALID, "null argument");
   if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
+  if (width != 2 && width != 3) return fail(GS_ERR_INVALID, "width must be 2 or 3");
+  if (cap < (uint64_t)gs::kShards * h->delta_shard_cap)
+    return fail(GS_ERR_INVALID, "cap below the delta capacity (gs_delta_capacity)");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  return stage(h, send, cap);
+  return stage_delta(h, send, cap, width, reinterpret_cast<unsigned long long*>(count),
+                     h->kind == GS_KIND_SIGNED);
 }
 
-int gs_fold_exchange_device(gs_handle h, const int64_t* recv, size_t world, size_t rows, int skip_rank) {
+int gs_fold_exchange_device(gs_handle h, const int64_t* recv, const uint64_t* counts, size_t world, size_t rows,
+                            int width, int skip_rank) {
   if (int rc = check(h)) return rc;
-  if (!recv || rows == 0) return fail(GS_ERR_INVALID, "empty exchange buffer");
+  if (!recv || !counts || rows == 0 || world == 0) return fail(GS_ERR_INVALID, "empty exchange buffer");
+  if (width != 2 && width != 3) return fail(GS_ERR_INVALID, "width must be 2 or 3");
   if (world * rows > 0xFFFFFFFFull) return fail(GS_ERR_INVALID, "exchange buffer too large");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  ExchangeLayout xl;
-  xl.rows = (uint32_t)rows;
-  xl.skip_rank = skip_rank;
-  xl.base = recv;
-  return fold_device_impl(h, recv, recv + 1, reinterpret_cast<const uint8_t*>(recv + 2), world * rows, 3, 24,
-                          /*track=*/false, true, xl);
+  FoldSource fs;
+  fs.rows = (uint32_t)rows;
+  fs.skip_rank = skip_rank;
+  fs.counts = reinterpret_cast<const unsigned long long*>(counts);
+  fs.units = world * rows;  // the counts live on the device: charge every row
+  const uint8_t* w = width == 3 ? reinterpret_cast<const uint8_t*>(recv + 2) : nullptr;
+  return fold_device_impl(h, recv, recv + 1, w, world * rows, width, 8 * width, /*track=*/false, true, fs);
 }
 
 int gs_get_stream(gs_handle h, void** stream) {
@@ -1175,17 +991,16 @@ int gs_counters(gs_handle h, uint64_t* out8) {
   if (!out8) return fail(GS_ERR_INVALID, "out is null");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  if (int rc = flush_hooks(h)) return rc;
   std::vector<uint32_t> c(gs::CTR_COUNT * gs::kCtrStride);
   GS_HIP(hipMemcpyAsync(c.data(), h->ctr, c.size() * 4, hipMemcpyDeviceToHost, h->stream));
   GS_HIP(hipStreamSynchronize(h->stream));
   uint64_t nv = 0;
   for (int i = 0; i < gs::kShards; ++i) nv += c[gs::ctr_index(gs::CTR_NV + i)];
-  auto u64 = [&](int idx) { return (uint64_t)c[gs::ctr_index(idx)] | ((uint64_t)c[gs::ctr_index(idx) + 1] << 32); };
+  auto u64 = [&](int idx) { return (uint64_t)c[gs::ctr_index(idx)] | ((uint64_t)c[gs::ctr_index(idx + 1)] << 32); };
   out8[0] = nv;
   out8[1] = c[gs::ctr_index(gs::CTR_FAIL)];
   out8[2] = c[gs::ctr_index(gs::CTR_ERR)];
-  out8[3] = c[gs::ctr_index(gs::CTR_OVF)];
+  out8[3] = c[gs::ctr_index(gs::CTR_OVF)] | (c[gs::ctr_index(gs::CTR_VOVF)] ? 2u : 0u);
   out8[4] = u64(gs::CTR_SENT);
   out8[5] = c[gs::ctr_index(gs::CTR_DBG_HOOKS)];
   out8[6] = c[gs::ctr_index(gs::CTR_DBG_ITERS)];
@@ -1193,13 +1008,20 @@ int gs_counters(gs_handle h, uint64_t* out8) {
   return GS_OK;
 }
 
+int gs_capacity_stats(gs_handle h, uint64_t* waits, uint64_t* syncs, double* wait_ms) {
+  if (int rc = check(h)) return rc;
+  if (waits) *waits = h->cap_waits;
+  if (syncs) *syncs = h->cap_syncs;
+  if (wait_ms) *wait_ms = h->cap_wait_s * 1e3;
+  return GS_OK;
+}
+
 // ---- text ingest (include/gs_ingest.h) ----
 namespace {
 constexpr size_t kTextChunk = 16u << 20;  // bytes of text per parse + fold
-}
 
 // Copy into pinned staging with a few threads (one core's memcpy is far below PCIe).
-static void staged_copy(char* dst, const char* src, size_t n) {
+void staged_copy(char* dst, const char* src, size_t n) {
   const int nt = n >= (4u << 20) ? 8 : 1;
   if (nt == 1) {
     memcpy(dst, src, n);
@@ -1215,12 +1037,13 @@ static void staged_copy(char* dst, const char* src, size_t n) {
 
 // End of the chunk that starts at off: after the last '\n' within kTextChunk bytes
 // (the whole rest when it fits); 0 = a single line longer than a chunk.
-static size_t chunk_end(const char* text, size_t len, size_t off) {
+size_t chunk_end(const char* text, size_t len, size_t off) {
   if (len - off <= kTextChunk) return len;
   size_t end = off + kTextChunk;
   while (end > off && text[end - 1] != '\n') --end;
   return end == off ? 0 : end;
 }
+}  // namespace
 
 int gs_fold_text(gs_handle h, const char* text, size_t len, int sep, uint64_t* n_edges, int64_t* bad_line) {
   if (int rc = check(h)) return rc;
@@ -1295,739 +1118,7 @@ int gs_set_pipelining(gs_handle h, int depth) {
 int gs_table_capacity(gs_handle h, uint64_t* slots) {
   if (int rc = check(h)) return rc;
   if (!slots) return fail(GS_ERR_INVALID, "slots is null");
-  *slots = h->hotcap + h->cap;
-  return GS_OK;
-}
-
-}  // extern "C"
-
-// ============================================================================
-// Native multi-GPU group (include/gs_group.h): RCCL all-gather of staged deltas on
-// the summary's own stream. RCCL is dlopen'ed on first use (librccl.so.1; in a
-// process that already loaded torch this resolves to torch's copy).
-// ============================================================================
-#include <dlfcn.h>
-
-#include "gs_group.h"
-
-namespace {
-
-struct RcclApi {
-  void* lib = nullptr;
-  int (*getUniqueId)(void*) = nullptr;
-  int (*allGather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
-  int (*commDestroy)(void*) = nullptr;
-  int (*send)(const void*, size_t, int, int, void*, hipStream_t) = nullptr;
-  int (*recv)(void*, size_t, int, int, void*, hipStream_t) = nullptr;
-  int (*groupStart)() = nullptr;
-  int (*groupEnd)() = nullptr;
-  const char* (*getErrorString)(int) = nullptr;
-  void* initRankSym = nullptr;  // ncclCommInitRank takes ncclUniqueId (128 B) by value: see Id128
-};
-
-struct Id128 {
-  char b[GS_GROUP_ID_BYTES];
-};
-
-RcclApi g_rccl;
-
-int rccl_load() {
-  if (g_rccl.lib) return GS_OK;
-  void* l = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-  if (!l) l = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-  if (!l) return fail(GS_ERR_HIP, std::string("cannot load RCCL: ") + dlerror());
-  g_rccl.getUniqueId = (int (*)(void*))dlsym(l, "ncclGetUniqueId");
-  g_rccl.initRankSym = dlsym(l, "ncclCommInitRank");
-  g_rccl.allGather = (int (*)(const void*, void*, size_t, int, void*, hipStream_t))dlsym(l, "ncclAllGather");
-  g_rccl.commDestroy = (int (*)(void*))dlsym(l, "ncclCommDestroy");
-  g_rccl.getErrorString = (const char* (*)(int))dlsym(l, "ncclGetErrorString");
-  g_rccl.send = (int (*)(const void*, size_t, int, int, void*, hipStream_t))dlsym(l, "ncclSend");
-  g_rccl.recv = (int (*)(void*, size_t, int, int, void*, hipStream_t))dlsym(l, "ncclRecv");
-  g_rccl.groupStart = (int (*)())dlsym(l, "ncclGroupStart");
-  g_rccl.groupEnd = (int (*)())dlsym(l, "ncclGroupEnd");
-  if (!g_rccl.getUniqueId || !g_rccl.initRankSym || !g_rccl.allGather || !g_rccl.commDestroy)
-    return fail(GS_ERR_HIP, "RCCL is missing ncclGetUniqueId/ncclCommInitRank/ncclAllGather/ncclCommDestroy");
-  g_rccl.lib = l;
-  return GS_OK;
-}
-
-int rccl_fail(const char* what, int r) {
-  return fail(GS_ERR_HIP, std::string(what) + ": " + (g_rccl.getErrorString ? g_rccl.getErrorString(r) : "rccl error"));
-}
-
-constexpr int kNcclInt64 = 4;  // ncclInt64 (rccl.h)
-constexpr int kNcclUint8 = 1;  // ncclUint8 (rccl.h)
-
-// ---------------------------------------------------------------------------
-// In-process emulation of the four RCCL calls the group uses, selected with
-// GS_GROUP_FAKE_COMM=1: N threads of ONE process, each driving one rank's summary
-// on the same GPU, meet at host barriers; the data moves with device copies
-// ordered by events. Test infrastructure only (RCCL refuses two ranks on one GPU,
-// and the GPU box has one): it runs the group's N-rank code paths -- exchange
-// layout with real remote rows, per-rank headers, retune, backlog drain, side-stream
-// apply, the binomial tree -- exactly as with RCCL.
-struct FakeShared {
-  int n = 0, refs = 0;
-  std::mutex m;
-  std::condition_variable cv;
-  int arrived = 0;
-  uint64_t gen = 0;
-  std::vector<const void*> src;
-  std::vector<hipEvent_t> ev;
-  struct Msg {
-    const void* buf;
-    size_t bytes;
-    hipEvent_t ready, copied;
-    bool done = false;
-  };
-  std::map<std::pair<int, int>, std::deque<Msg*>> box;  // (from, to) -> messages
-};
-struct FakeComm {
-  FakeShared* s;
-  int rank;
-  hipEvent_t ready = nullptr, done = nullptr;
-  std::vector<hipEvent_t> spare;  // message events, destroyed with the comm
-};
-std::mutex g_fake_mu;
-std::map<std::string, FakeShared*> g_fake_reg;
-
-void fake_barrier(FakeShared* s) {
-  std::unique_lock<std::mutex> lk(s->m);
-  const uint64_t g0 = s->gen;
-  if (++s->arrived == s->n) {
-    s->arrived = 0;
-    s->gen++;
-    s->cv.notify_all();
-  } else {
-    s->cv.wait(lk, [&] { return s->gen != g0; });
-  }
-}
-size_t fake_elem(int dtype) { return dtype == kNcclUint8 ? 1 : 8; }
-int fake_unique_id(void* id) {
-  static std::atomic<uint64_t> ctr{1};
-  memset(id, 0, GS_GROUP_ID_BYTES);
-  const uint64_t v[2] = {(uint64_t)getpid(), ctr++};
-  memcpy(id, v, sizeof v);
-  return 0;
-}
-int fake_init(void** comm, int n, Id128 id, int rank) {
-  std::lock_guard<std::mutex> lk(g_fake_mu);
-  FakeShared*& s = g_fake_reg[std::string(id.b, GS_GROUP_ID_BYTES)];
-  if (!s) {
-    s = new FakeShared();
-    s->n = n;
-    s->src.resize(n);
-    s->ev.resize(n);
-  }
-  s->refs++;
-  FakeComm* c = new FakeComm{s, rank};
-  if (hipEventCreateWithFlags(&c->ready, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess)
-    return 1;
-  *comm = c;
-  return 0;
-}
-int fake_destroy(void* comm) {
-  FakeComm* c = (FakeComm*)comm;
-  (void)hipEventDestroy(c->ready);
-  (void)hipEventDestroy(c->done);
-  for (hipEvent_t e : c->spare) (void)hipEventDestroy(e);
-  std::lock_guard<std::mutex> lk(g_fake_mu);
-  if (--c->s->refs == 0) {
-    for (auto it = g_fake_reg.begin(); it != g_fake_reg.end(); ++it)
-      if (it->second == c->s) {
-        g_fake_reg.erase(it);
-        break;
-      }
-    delete c->s;
-  }
-  delete c;
-  return 0;
-}
-int fake_all_gather(const void* send, void* recv, size_t count, int dtype, void* comm, hipStream_t st) {
-  FakeComm* c = (FakeComm*)comm;
-  FakeShared* s = c->s;
-  const size_t bytes = count * fake_elem(dtype);
-  if (hipEventRecord(c->ready, st) != hipSuccess) return 1;
-  {
-    std::lock_guard<std::mutex> lk(s->m);
-    s->src[c->rank] = send;
-    s->ev[c->rank] = c->ready;
-  }
-  fake_barrier(s);  // every rank's send buffer is staged (in its stream order)
-  for (int q = 0; q < s->n; ++q) {
-    if (hipStreamWaitEvent(st, s->ev[q], 0) != hipSuccess) return 1;
-    if (hipMemcpyAsync((char*)recv + (size_t)q * bytes, s->src[q], bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
-      return 1;
-  }
-  if (hipEventRecord(c->done, st) != hipSuccess) return 1;
-  fake_barrier(s);  // (the ready events were captured by every stream's wait)
-  {
-    std::lock_guard<std::mutex> lk(s->m);
-    s->ev[c->rank] = c->done;
-  }
-  fake_barrier(s);
-  // the collective completes on this rank once every rank has read its send buffer
-  for (int q = 0; q < s->n; ++q)
-    if (q != c->rank && hipStreamWaitEvent(st, s->ev[q], 0) != hipSuccess) return 1;
-  fake_barrier(s);  // slots and events may be reused after this
-  return 0;
-}
-int fake_send(const void* buf, size_t count, int dtype, int peer, void* comm, hipStream_t st) {
-  FakeComm* c = (FakeComm*)comm;
-  FakeShared* s = c->s;
-  FakeShared::Msg msg{buf, count * fake_elem(dtype), nullptr, nullptr};
-  if (hipEventCreateWithFlags(&msg.ready, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&msg.copied, hipEventDisableTiming) != hipSuccess || hipEventRecord(msg.ready, st))
-    return 1;
-  c->spare.push_back(msg.ready);
-  c->spare.push_back(msg.copied);
-  std::unique_lock<std::mutex> lk(s->m);
-  s->box[{c->rank, peer}].push_back(&msg);
-  s->cv.notify_all();
-  s->cv.wait(lk, [&] { return msg.done; });  // the receiver has queued its copy
-  return hipStreamWaitEvent(st, msg.copied, 0) == hipSuccess ? 0 : 1;
-}
-int fake_recv(void* buf, size_t count, int dtype, int peer, void* comm, hipStream_t st) {
-  FakeComm* c = (FakeComm*)comm;
-  FakeShared* s = c->s;
-  std::unique_lock<std::mutex> lk(s->m);
-  auto& q = s->box[{peer, c->rank}];
-  s->cv.wait(lk, [&] { return !q.empty(); });
-  FakeShared::Msg* msg = q.front();
-  q.pop_front();
-  int r = 0;
-  if (msg->bytes != count * fake_elem(dtype)) r = 1;
-  if (!r && (hipStreamWaitEvent(st, msg->ready, 0) != hipSuccess ||
-             hipMemcpyAsync(buf, msg->buf, msg->bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-             hipEventRecord(msg->copied, st) != hipSuccess))
-    r = 1;
-  msg->done = true;
-  s->cv.notify_all();
-  return r;
-}
-int fake_noop() { return 0; }
-const char* fake_error(int) { return "in-process comm emulation error"; }
-
-RcclApi make_fake_api() {
-  RcclApi a;
-  a.lib = (void*)&g_fake_reg;
-  a.getUniqueId = fake_unique_id;
-  a.allGather = fake_all_gather;
-  a.commDestroy = fake_destroy;
-  a.send = fake_send;
-  a.recv = fake_recv;
-  a.groupStart = fake_noop;
-  a.groupEnd = fake_noop;
-  a.getErrorString = fake_error;
-  a.initRankSym = (void*)&fake_init;
-  return a;
-}
-const RcclApi g_fake = make_fake_api();
-
-// the communication API a new group (or id) uses
-int comm_api(const RcclApi** api) {
-  const char* f = getenv("GS_GROUP_FAKE_COMM");
-  if (f && atoi(f) != 0) {
-    *api = &g_fake;
-    return GS_OK;
-  }
-  if (int rc = rccl_load()) return rc;
-  *api = &g_rccl;
-  return GS_OK;
-}
-
-constexpr uint64_t kHdrLag = 2;  // default lag: a retune reads the headers of the exchange `lag` batches back
-// (2, with a retune every exchange: the all-gather size follows RMAT's decaying record
-// counts -- mean cap at 8 emulated ranks, 2^22-edge batches 891 K -> 531 K rows)
-constexpr uint64_t kHdrSlots = 8;  // > lag: header copies of every retune period stay distinct
-
-}  // namespace
-
-struct gs_group {
-  gs_summary* h = nullptr;
-  const RcclApi* api = nullptr;  // RCCL, or the in-process emulation (GS_GROUP_FAKE_COMM=1, tests)
-  void* comm = nullptr;
-  int nranks = 1, rank = 0;
-  int width = 3;  // int64 per exchange row: {a, b} for CC (16 B), {a, b, parity} for the signed kind
-  bool self_apply = false;  // test knob (GS_GROUP_SELF_APPLY=1): also fold this rank's own rows back
-  uint64_t max_cap = 0, first_cap = 0, cap = 0, retune = 1;
-  int margin = 3;  // GS_GROUP_MARGIN: a retuned cap is queued + queued >> margin + 1024 (>= 64: no margin)
-  uint64_t lag = kHdrLag;  // GS_GROUP_LAG (1..7)
-  // double-buffered exchange: exchange b stages into send[b % 2] and gathers into
-  // recv[b % 2] on the communication stream `xs` while the summary stream folds the
-  // next batch; its rows are folded during the next exchange (or finish)
-  int64_t* send[2] = {nullptr, nullptr};  // [(max_cap + 1) * 3]
-  int64_t* recv[2] = {nullptr, nullptr};  // [nranks * (max_cap + 1) * 3]
-  hipStream_t xs = nullptr;
-  hipEvent_t staged[2] = {nullptr, nullptr};    // on h->stream after the stage of an exchange
-  hipEvent_t gathered[2] = {nullptr, nullptr};  // on xs after its all-gather
-  hipEvent_t applied[2] = {nullptr, nullptr};   // after the fold of its rows (side or summary stream)
-  bool used[2] = {false, false};                // buffer k holds an exchange (events valid)
-  hipStream_t as = nullptr;                     // apply stream (installed as the summary's side stream)
-  hipEvent_t as_ev = nullptr;
-  // rank headers of kept exchanges, a ring of kHdrSlots: slot b % kHdrSlots holds
-  // the headers of exchange hdr_batch[slot] once hdr_ev[slot] has completed
-  int64_t* hdr_host = nullptr;  // pinned, host-mapped [kHdrSlots][nranks * 3]
-  long long* hdr_dev = nullptr;  // its device mapping (k_headers writes it)
-  hipEvent_t hdr_ev[kHdrSlots] = {};
-  int64_t hdr_batch[kHdrSlots] = {-1, -1, -1, -1, -1, -1, -1, -1};
-  uint64_t b = 0;            // exchanges since create / finish
-  int pend = -1;             // buffer of the gathered-but-not-folded exchange, -1: none
-  uint64_t pend_rows = 0;
-  uint64_t last_rows = 0;    // rows per rank of the last exchange
-  int last_k = 0;            // its buffer
-  uint64_t exchanges = 0;
-  // pipelined own folds: exchange b's fold AND stage run on lane b % 2 of the summary,
-  // recording into delta set b % 2, so fold b + 1 (other lane, other set) overlaps
-  // fold b and stage b; stages stay in order through the staged[] events
-  bool lanes = false;        // decided per exchange (lane_fold_ok)
-  // GS_GROUP_LANES=1 enables the lane pipeline. Off by default: measured slower at one
-  // rank
-  bool no_lanes = true;
-  // GS_GROUP_HOSTPROF=1: host seconds per phase of the exchange loop, printed at destroy
-  bool hostprof = false;
-  double hp[6] = {};  // retune, own fold, stage+events, collective, headers, remote fold
-  uint64_t hp_calls = 0;
-  double cap_sum = 0;
-};
-
-namespace {
-struct HostTimer {
-  double* acc;
-  std::chrono::steady_clock::time_point t0;
-  explicit HostTimer(double* a) : acc(a), t0(a ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point()) {}
-  void lap(double* next) {  // charge the time so far to acc, continue on next
-    if (!acc) return;
-    const auto t = std::chrono::steady_clock::now();
-    *acc += std::chrono::duration<double>(t - t0).count();
-    t0 = t;
-    acc = next;
-  }
-  ~HostTimer() { lap(nullptr); }
-};
-}  // namespace
-
-namespace {
-
-// Fold the other ranks' rows of a gathered exchange behind its all-gather (event),
-// without host synchronisation, on the summary's side stream (the group's apply
-// stream) when possible, so this rank's next own fold does not wait for the remote
-// rows (union commutes).
-int group_apply(gs_group* g, int k, uint64_t rows) {
-  gs_summary* h = g->h;
-  const bool use_side = side_ok(h);
-  hipStream_t s = use_side ? h->side : h->stream;
-  if (g->nranks > 1 || g->self_apply) {
-    GS_HIP(hipStreamWaitEvent(s, g->gathered[k], 0));
-    ExchangeLayout xl;
-    xl.rows = (uint32_t)rows;
-    xl.skip_rank = g->self_apply ? -1 : g->rank;
-    xl.base = g->recv[k];
-    xl.on_side = use_side;
-    const uint8_t* w = g->width == 3 ? reinterpret_cast<const uint8_t*>(g->recv[k] + 2) : nullptr;
-    if (int rc = fold_device_impl(h, g->recv[k], g->recv[k] + 1, w, g->nranks * rows, g->width, 8 * g->width,
-                                  /*track=*/false, true, xl))
-      return rc;
-  }
-  GS_HIP(hipEventRecord(g->applied[k], s));
-  return GS_OK;
-}
-
-// stage (summary stream) -> all-gather (communication stream) -> fold the PREVIOUS
-// exchange's rows (summary stream, overlapping this all-gather). apply_now also
-// folds this exchange's rows (finish).
-int group_exchange(gs_group* g, uint64_t cap, bool keep_header, bool apply_now) {
-  gs_summary* h = g->h;
-  const uint64_t rows = cap + 1;
-  const int k = (int)(g->b & 1u);
-  HostTimer ht(g->hostprof ? &g->hp[2] : nullptr);
-  // the stage runs where this exchange's own fold ran (lane k, delta set k), or on
-  // the handle's stream (set 0) when folds cannot run on lanes
-  hipStream_t ss = g->lanes ? h->lane[k] : h->stream;
-  if (g->used[k]) {
-    // buffer k last served exchange b - 2: its all-gather must have read send[k]
-    // before this stage rewrites it, and its rows must have been folded before this
-    // all-gather rewrites recv[k] (both long done in steady state)
-    GS_HIP(hipStreamWaitEvent(ss, g->gathered[k], 0));
-    GS_HIP(hipStreamWaitEvent(g->xs, g->applied[k], 0));
-  }
-  // stages consume the backlog queue in order: behind the previous exchange's stage
-  if (g->used[k ^ 1]) GS_HIP(hipStreamWaitEvent(ss, g->staged[k ^ 1], 0));
-  g->used[k] = true;
-  if (int rc = stage(h, g->send[k], cap, g->width, ss, g->lanes ? k : 0)) return rc;
-  GS_HIP(hipEventRecord(g->staged[k], ss));
-  if (g->lanes) h->lanes_dirty = true;
-  GS_HIP(hipStreamWaitEvent(g->xs, g->staged[k], 0));
-  ht.lap(g->hostprof ? &g->hp[3] : nullptr);
-  const int r = g->api->allGather(g->send[k], g->recv[k], rows * g->width, kNcclInt64, g->comm, g->xs);
-  if (r != 0) return rccl_fail("ncclAllGather", r);
-  ht.lap(g->hostprof ? &g->hp[4] : nullptr);
-  if (keep_header) {  // rank headers (row 0 of each rank's block) -> pinned host memory
-    const int slot = (int)(g->b % kHdrSlots);
-    gs::launch_headers(g->recv[k], rows * g->width, g->nranks, g->hdr_dev + (size_t)slot * g->nranks * 3,
-                       (long long)g->b, g->xs);
-    GS_HIP(hipGetLastError());
-    GS_HIP(hipEventRecord(g->hdr_ev[slot], g->xs));
-    g->hdr_batch[slot] = (int64_t)g->b;
-  }
-  GS_HIP(hipEventRecord(g->gathered[k], g->xs));
-  ht.lap(g->hostprof ? &g->hp[5] : nullptr);
-  if (g->pend >= 0) {
-    if (int rc = group_apply(g, g->pend, g->pend_rows)) return rc;
-    g->pend = -1;
-  }
-  if (apply_now) {
-    if (int rc = group_apply(g, k, rows)) return rc;
-  } else {
-    g->pend = k;
-    g->pend_rows = rows;
-  }
-  g->last_rows = rows;
-  g->last_k = k;
-  g->b++;
-  g->exchanges++;
-  return GS_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-// GS_GROUP_XS_PRIO=1 gives the communication stream the device's highest priority,
-// so the collective's kernel (or copy) need not wait for back-to-back fold launches
-// to release CUs. Off by default: it only helps the lane pipeline at one rank, and
-// the multi-rank emulation (all ranks in one process) ran 2-3x slower with it
-// (DESIGN.md section 5).
-static hipError_t create_comm_stream(hipStream_t* st) {
-  const char* e = getenv("GS_GROUP_XS_PRIO");
-  int least = 0, greatest = 0;
-  if (!(e && atoi(e) != 0) || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
-    return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
-  return hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest);
-}
-
-int gs_group_unique_id(void* id) {
-  if (!id) return fail(GS_ERR_INVALID, "id is null");
-  const RcclApi* api = nullptr;
-  if (int rc = comm_api(&api)) return rc;
-  const int r = api->getUniqueId(id);
-  return r ? rccl_fail("ncclGetUniqueId", r) : GS_OK;
-}
-
-int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, int rank, size_t batch_edges,
-                    size_t first_cap) {
-  if (!out || !id) return fail(GS_ERR_INVALID, "null argument");
-  *out = nullptr;
-  if (int rc = check(h)) return rc;
-  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(GS_ERR_INVALID, "bad group shape");
-  const RcclApi* api = nullptr;
-  if (int rc = comm_api(&api)) return rc;
-  DeviceGuard dg(h->device);
-  const bool exchange = batch_edges != 0;  // 0: tree-combine-only group
-  if (exchange)
-    if (int rc = gs_set_delta_tracking(h, 1)) return rc;
-  gs_group* g = new gs_group();
-  g->h = h;
-  g->api = api;
-  g->nranks = nranks;
-  g->rank = rank;
-  g->width = h->kind == GS_KIND_SIGNED ? 3 : 2;
-  g->max_cap = std::min<uint64_t>(3ull * batch_edges, (uint64_t)gs::kShards * h->delta_shard_cap);
-  g->first_cap = std::min<uint64_t>(first_cap ? first_cap : batch_edges, g->max_cap);
-  g->cap = g->first_cap;
-  if (const char* m = getenv("GS_GROUP_RETUNE")) g->retune = std::max(1, atoi(m));
-  if (const char* m = getenv("GS_GROUP_LAG")) g->lag = (uint64_t)std::max(1, std::min((int)kHdrSlots - 1, atoi(m)));
-  if (const char* m = getenv("GS_GROUP_MARGIN")) g->margin = std::max(0, atoi(m));
-  if (const char* m = getenv("GS_GROUP_SELF_APPLY")) g->self_apply = atoi(m) != 0;
-  if (const char* m = getenv("GS_GROUP_LANES")) g->no_lanes = atoi(m) == 0;  // default: off
-  if (const char* m = getenv("GS_GROUP_HOSTPROF")) g->hostprof = atoi(m) != 0;
-  auto bail = [&](int code) {
-    gs_group_destroy(g);
-    return code;
-  };
-  const size_t rows = g->max_cap + 1;
-  if (exchange) {
-    bool ok = hipHostMalloc(&g->hdr_host, (size_t)kHdrSlots * nranks * 24, hipHostMallocMapped | hipHostMallocCoherent) ==
-                  hipSuccess &&
-              hipHostGetDevicePointer(reinterpret_cast<void**>(&g->hdr_dev), g->hdr_host, 0) == hipSuccess &&
-              create_comm_stream(&g->xs) == hipSuccess;
-    for (int k = 0; k < (int)kHdrSlots && ok; ++k)
-      ok = hipEventCreateWithFlags(&g->hdr_ev[k], hipEventDisableTiming) == hipSuccess;
-    for (int k = 0; k < 2 && ok; ++k)
-      ok = hipMalloc(&g->send[k], rows * 24) == hipSuccess &&
-           hipMalloc(&g->recv[k], (size_t)nranks * rows * 24) == hipSuccess &&
-           hipEventCreateWithFlags(&g->staged[k], hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&g->gathered[k], hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&g->applied[k], hipEventDisableTiming) == hipSuccess;
-    if (!ok) return bail(fail(GS_ERR_HIP, "group buffer allocation failed"));
-    for (int k = 0; k < (int)kHdrSlots; ++k) g->hdr_host[(size_t)k * nranks * 3 + 2] = -1;  // no exchange yet
-    if (int rc = join_lanes(h)) return bail(rc);
-    if (h->pipe_depth < 2) h->pipe_depth = 2;  // own folds alternate over lanes 0 and 1
-    // GS_GROUP_SIDE=0: fold remote rows on the summary stream (no overlap)
-    const char* sv = getenv("GS_GROUP_SIDE");
-    if (!(sv && atoi(sv) == 0)) {
-      if (h->side) return bail(fail(GS_ERR_INVALID, "the summary already belongs to an exchange group"));
-      if (hipStreamCreateWithFlags(&g->as, hipStreamNonBlocking) != hipSuccess ||
-          hipEventCreateWithFlags(&g->as_ev, hipEventDisableTiming) != hipSuccess)
-        return bail(fail(GS_ERR_HIP, "group stream creation failed"));
-      if (int rc = join_lanes(h)) return bail(rc);
-      h->side = g->as;
-      h->side_ev = g->as_ev;
-      h->side_dirty = false;
-    }
-  }
-  Id128 uid;
-  memcpy(uid.b, id, GS_GROUP_ID_BYTES);
-  typedef int (*InitRank)(void**, int, Id128, int);
-  const int r = ((InitRank)api->initRankSym)(&g->comm, nranks, uid, rank);
-  if (r != 0) return bail(rccl_fail("ncclCommInitRank", r));
-  *out = g;
-  return GS_OK;
-}
-
-int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n) {
-  if (!g) return fail(GS_ERR_INVALID, "null group");
-  gs_summary* h = g->h;
-  DeviceGuard dg(h->device);
-  if (!g->send[0]) return fail(GS_ERR_INVALID, "tree-combine-only group (created with batch_edges 0)");
-  if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
-  const uint64_t b = g->b;
-  g->hp_calls++;
-  HostTimer ht(g->hostprof ? &g->hp[0] : nullptr);
-  // every `retune` exchanges all ranks re-derive the capacity from the same headers:
-  // those of exchange b - lag, read BEFORE this exchange may copy its own
-  const uint64_t lag = g->lag;
-  const int lag_slot = (int)((b - lag) % kHdrSlots);
-  if (b % g->retune == 0 && b >= lag && g->hdr_batch[lag_slot] == (int64_t)(b - lag)) {
-    // k_headers writes the exchange number into word 2 of the slot after the headers:
-    // poll it (an event synchronisation costs ~40 us of host time even when complete)
-    const int64_t* hh = g->hdr_host + (size_t)lag_slot * g->nranks * 3;
-    const auto t0 = std::chrono::steady_clock::now();
-    while (__atomic_load_n(&hh[2], __ATOMIC_ACQUIRE) != (int64_t)(b - lag)) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
-        GS_HIP(hipEventSynchronize(g->hdr_ev[lag_slot]));  // long wait: block instead of spinning
-        if (__atomic_load_n(&hh[2], __ATOMIC_ACQUIRE) != (int64_t)(b - lag))
-          return fail(GS_ERR_HIP, "exchange header sequence mismatch");
-        break;
-      }
-    }
-    int64_t queued = 0;
-    for (int r = 0; r < g->nranks; ++r) queued = std::max(queued, hh[r * 3 + 1]);
-    const uint64_t q = (uint64_t)queued;
-    g->cap = std::min<uint64_t>(g->max_cap, std::max<uint64_t>(4096, q + (g->margin < 64 ? q >> g->margin : 0) + 1024));
-  }
-  // own fold: with GS_GROUP_LANES=1, on lane b % 2 into delta set b % 2 when possible
-  // (overlaps the previous exchange's fold and stage); default: the handle's stream
-  ht.lap(g->hostprof ? &g->hp[1] : nullptr);
-  g->lanes = lane_fold_ok(h) && !g->no_lanes;
-  if (g->lanes) {
-    h->force_lane = (int)(b & 1u);
-    h->dset = (int)(b & 1u);
-  }
-  const int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, /*track=*/true);
-  h->force_lane = -1;
-  h->dset = 0;
-  if (rc) return rc;
-  ht.lap(nullptr);
-  g->cap_sum += (double)g->cap;
-  const bool keep = (b + lag) % g->retune == 0;
-  return group_exchange(g, g->cap, keep, /*apply_now=*/false);
-}
-
-int gs_group_fold_batches_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n, size_t batch) {
-  if (!g) return fail(GS_ERR_INVALID, "null group");
-  if (batch == 0) return fail(GS_ERR_INVALID, "batch is 0");
-  for (size_t off = 0; off < n; off += batch)
-    if (int rc = gs_group_fold_device(g, src + off, dst + off, std::min(batch, n - off))) return rc;
-  return GS_OK;
-}
-
-int gs_group_finish(gs_group_t g) {
-  if (!g) return fail(GS_ERR_INVALID, "null group");
-  gs_summary* h = g->h;
-  DeviceGuard dg(h->device);
-  if (g->pend >= 0) {
-    if (int rc = group_apply(g, g->pend, g->pend_rows)) return rc;
-    g->pend = -1;
-  }
-  while (g->last_rows) {
-    // headers of the last exchange -> remaining backlog on any rank (identical on every rank)
-    GS_HIP(hipStreamSynchronize(g->xs));
-    GS_HIP(hipMemcpy2DAsync(g->hdr_host, 24, g->recv[g->last_k], g->last_rows * 8 * g->width, 16, g->nranks,
-                            hipMemcpyDeviceToHost, h->stream));
-    GS_HIP(hipStreamSynchronize(h->stream));
-    int64_t remaining = 0;
-    for (int r = 0; r < g->nranks; ++r) remaining = std::max(remaining, g->hdr_host[r * 3 + 1] - g->hdr_host[r * 3]);
-    if (remaining <= 0) break;
-    g->lanes = lane_fold_ok(h) && !g->no_lanes;
-    if (int rc = group_exchange(g, std::min<uint64_t>((uint64_t)remaining, g->max_cap), false, /*apply_now=*/true))
-      return rc;
-  }
-  if (int rc = gs_sync(h)) return rc;
-  GS_HIP(hipStreamSynchronize(g->xs));
-  g->b = 0;
-  g->used[0] = g->used[1] = false;
-  g->last_rows = 0;
-  for (int k = 0; k < (int)kHdrSlots; ++k) {
-    g->hdr_batch[k] = -1;
-    __atomic_store_n(&g->hdr_host[(size_t)k * g->nranks * 3 + 2], (int64_t)-1, __ATOMIC_RELEASE);
-  }
-  g->cap = g->first_cap;
-  return GS_OK;
-}
-
-namespace {
-
-// device arrays of one exported summary (v, label, parity), freed on scope exit
-struct ExportedArrays {
-  int64_t* v = nullptr;
-  int64_t* l = nullptr;
-  uint8_t* p = nullptr;
-  int alloc(size_t n) {
-    if (!n) return GS_OK;
-    GS_HIP(hipMalloc(&v, n * 8));
-    GS_HIP(hipMalloc(&l, n * 8));
-    GS_HIP(hipMalloc(&p, n));
-    return GS_OK;
-  }
-  ~ExportedArrays() {
-    (void)hipFree(v);
-    (void)hipFree(l);
-    (void)hipFree(p);
-  }
-};
-
-// one tree edge, sending side: header {count, failed}, then the three arrays
-int tree_send(gs_group* g, int peer, int64_t* hdr) {
-  gs_summary* h = g->h;
-  uint64_t nv = 0;
-  if (int rc = read_nv(h, &nv)) return rc;
-  ExportedArrays a;
-  if (int rc = a.alloc(nv + 1)) return rc;
-  size_t got = 0;
-  if (int rc = export_device_impl(h, a.v, a.l, a.p, nv + 1, &got)) return rc;
-  uint32_t failed = 0;
-  GS_HIP(hipMemcpyAsync(&failed, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
-  const int64_t hv[2] = {(int64_t)got, (int64_t)((failed & 0xff) != 0)};
-  GS_HIP(hipMemcpyAsync(hdr, hv, 16, hipMemcpyHostToDevice, h->stream));
-  int r = g->api->send(hdr, 2, kNcclInt64, peer, g->comm, h->stream);
-  if (r) return rccl_fail("ncclSend", r);
-  if (got) {
-    g->api->groupStart();
-    r = g->api->send(a.v, got, kNcclInt64, peer, g->comm, h->stream);
-    if (!r) r = g->api->send(a.l, got, kNcclInt64, peer, g->comm, h->stream);
-    if (!r) r = g->api->send(a.p, got, kNcclUint8, peer, g->comm, h->stream);
-    const int e = g->api->groupEnd();
-    if (r || e) return rccl_fail("ncclSend", r ? r : e);
-  }
-  GS_HIP(hipStreamSynchronize(h->stream));  // the arrays are freed on return
-  return GS_OK;
-}
-
-// one tree edge, receiving side: fold the peer's exported summary into this one
-int tree_recv(gs_group* g, int peer, int64_t* hdr) {
-  gs_summary* h = g->h;
-  int r = g->api->recv(hdr, 2, kNcclInt64, peer, g->comm, h->stream);
-  if (r) return rccl_fail("ncclRecv", r);
-  int64_t hv[2] = {0, 0};
-  GS_HIP(hipMemcpyAsync(hv, hdr, 16, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
-  const size_t got = (size_t)hv[0];
-  ExportedArrays a;
-  if (int rc = a.alloc(got)) return rc;
-  if (got) {
-    g->api->groupStart();
-    r = g->api->recv(a.v, got, kNcclInt64, peer, g->comm, h->stream);
-    if (!r) r = g->api->recv(a.l, got, kNcclInt64, peer, g->comm, h->stream);
-    if (!r) r = g->api->recv(a.p, got, kNcclUint8, peer, g->comm, h->stream);
-    const int e = g->api->groupEnd();
-    if (r || e) return rccl_fail("ncclRecv", r ? r : e);
-  }
-  const bool track = h->track;
-  h->track = false;  // a bulk combine is not a structural delta of this rank's own fold
-  const int rc = gs_combine_exported_device(h, a.v, a.l, a.p, got, (int)hv[1]);
-  h->track = track;
-  if (rc) return rc;
-  GS_HIP(hipStreamSynchronize(h->stream));
-  return GS_OK;
-}
-
-}  // namespace
-
-int gs_group_tree_combine(gs_group_t g) {
-  if (!g) return fail(GS_ERR_INVALID, "null group");
-  if (!g->api || !g->api->send || !g->api->recv || !g->api->groupStart || !g->api->groupEnd)
-    return fail(GS_ERR_HIP, "RCCL is missing ncclSend/ncclRecv/ncclGroupStart/ncclGroupEnd");
-  gs_summary* h = g->h;
-  DeviceGuard dg(h->device);
-  if (int rc = join_lanes(h)) return rc;
-  int64_t* hdr = nullptr;  // device {count, failed}
-  GS_HIP(hipMalloc(&hdr, 16));
-  int rc = GS_OK;
-  // binomial tree (SummaryTreeReduce.enhance pairs partitions by f0/2, :107): at level l
-  // rank r with r mod 2^(l+1) == 2^l sends to r - 2^l and leaves the tree
-  for (int step = 1; step < g->nranks && rc == GS_OK; step <<= 1) {
-    const int pos = g->rank % (2 * step);
-    if (pos == step) {
-      rc = tree_send(g, g->rank - step, hdr);
-      break;
-    }
-    if (pos == 0 && g->rank + step < g->nranks) rc = tree_recv(g, g->rank + step, hdr);
-  }
-  (void)hipFree(hdr);
-  return rc;
-}
-
-int gs_group_stats(gs_group_t g, uint64_t* exchanges, uint64_t* records_sent, uint64_t* current_cap) {
-  if (!g) return fail(GS_ERR_INVALID, "null group");
-  gs_summary* h = g->h;
-  DeviceGuard dg(h->device);
-  uint64_t sent = 0;
-  GS_HIP(hipMemcpyAsync(&sent, h->ctr + gs::ctr_index(gs::CTR_SENT), 8, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
-  if (exchanges) *exchanges = g->exchanges;
-  if (records_sent) *records_sent = sent;
-  if (current_cap) *current_cap = g->cap;
-  return GS_OK;
-}
-
-int gs_group_destroy(gs_group_t g) {
-  if (!g) return GS_OK;
-  if (g->hostprof && g->hp_calls) {
-    const char* nm[6] = {"retune", "own fold", "stage+events", "collective", "headers", "remote fold"};
-    fprintf(stderr, "[gs_group rank %d] host us per batch over %llu batches:", g->rank, (unsigned long long)g->hp_calls);
-    for (int i = 0; i < 6; ++i) fprintf(stderr, " %s %.1f", nm[i], g->hp[i] * 1e6 / (double)g->hp_calls);
-    fprintf(stderr, "; mean cap %.0f rows; capacity waits %llu, syncs %llu\n", g->cap_sum / (double)g->hp_calls,
-            (unsigned long long)g->h->cap_waits, (unsigned long long)g->h->cap_syncs);
-  }
-  DeviceGuard dg(g->h->device);
-  (void)hipStreamSynchronize(g->h->stream);
-  if (g->comm && g->api && g->api->commDestroy) g->api->commDestroy(g->comm);
-  if (g->xs) (void)hipStreamSynchronize(g->xs);
-  if (g->as) {
-    (void)hipStreamSynchronize(g->as);
-    if (g->h->side == g->as) {
-      g->h->side = nullptr;
-      g->h->side_ev = nullptr;
-      g->h->side_dirty = false;
-    }
-    (void)hipStreamDestroy(g->as);
-  }
-  if (g->as_ev) (void)hipEventDestroy(g->as_ev);
-  for (int k = 0; k < 2; ++k) {
-    if (g->applied[k]) (void)hipEventDestroy(g->applied[k]);
-    (void)hipFree(g->send[k]);
-    (void)hipFree(g->recv[k]);
-    if (g->staged[k]) (void)hipEventDestroy(g->staged[k]);
-    if (g->gathered[k]) (void)hipEventDestroy(g->gathered[k]);
-  }
-  if (g->xs) (void)hipStreamDestroy(g->xs);
-  if (g->hdr_host) (void)hipHostFree(g->hdr_host);
-  for (int k = 0; k < (int)kHdrSlots; ++k)
-    if (g->hdr_ev[k]) (void)hipEventDestroy(g->hdr_ev[k]);
-  delete g;
+  *slots = h->cap;
   return GS_OK;
 }
 

@@ -9,16 +9,21 @@
 // same load that proves it is a root. Slot `cap` (one past the hashed range) is
 // reserved for the one id that collides with the empty marker, INT64_MIN.
 //
+// Beside the table: the VERTEX LIST (the dense ids in insertion order, 64 shards,
+// so exports, resets and combines cost O(vertices) instead of O(table) on sparse
+// tables), the sharded delta-record lists (multi-GPU exchange, change emission) and
+// the member lists of change tracking (gs_changes.hip).
+//
 // Concurrency model (MI355X: per-CU L1 and per-XCD L2 are not coherent inside a
 // launch). Correctness never depends on a plain load being fresh:
 //   * a key changes once, EMPTY -> k, by 64-bit CAS; a stale EMPTY read is settled by
-//     the CAS (insert) or by an atomic re-read (hook path);
+//     a fresh (agent-scope) re-read before any CAS, and by the CAS itself;
 //   * links only move "up": every parent pointer points to a strictly smaller key,
 //     so any historical link is still an ancestor and finds terminate;
 //   * only roots are hooked (32-bit CAS expecting `self<<1`); a failed CAS returns
 //     the live link and the hook loop continues from it, so each failure strictly
 //     lowers that side's key -> the loop terminates without re-reading stale lines;
-//   * path halving writes only to non-roots (never CAS targets) and only writes
+//   * path splitting writes only to non-roots (never CAS targets) and only writes
 //     ancestors with the composed parity -> benign races.
 // Reference semantics replaced: DisjointSet.union/find (DisjointSet.java:66-118),
 // Candidates.merge (Candidates.java:77-192) -- see DESIGN.md for the contract.
@@ -29,36 +34,28 @@
 namespace gs {
 
 constexpr int64_t kEmpty = INT64_MIN;
-constexpr int64_t kSealed = INT64_MIN + 1;  // hot-level slot closed to inserts (the id itself lives in slot r0 + 1)
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
-#ifndef GS_HOT_BUCKET
-#define GS_HOT_BUCKET 4
-#endif
-constexpr uint32_t kHotBucket = GS_HOT_BUCKET;  // hot-level bucket: slots loaded in one round trip
-#ifndef GS_FOLD_BS
-#define GS_FOLD_BS 256
-#endif
-constexpr uint32_t kFoldBS = GS_FOLD_BS;  // k_fold threads per block
-#ifndef GS_INSERT_TTAS
-#define GS_INSERT_TTAS 1
-#endif
-constexpr bool kInsertTTAS = GS_INSERT_TTAS != 0;  // fresh key load before an insert CAS (lookup_resolve)
-constexpr int kShards = 64;      // sharded append counters (one 128-B line each)
-constexpr int kCtrStride = 32;   // u32 per counter line
-constexpr int kActSets = 3;     // active-edge lists: appended at epoch e, drained at e+1, zeroed at e+2
+constexpr uint32_t kFoldBS = 256;  // k_fold threads per block (one edge per thread)
+constexpr int kShards = 64;        // sharded append counters (one 128-B line each)
+constexpr int kCtrStride = 32;     // u32 per counter line
+constexpr uint64_t kFailBit = 1ull << 62;  // exchange count word: the sender's verdict failed
 enum CounterBlock : int {
-  CTR_NV = 0,                    // [kShards] new-vertex counts
-  CTR_ACT = kShards,             // [kActSets][kShards] active-edge counts
-  CTR_DELTA = (1 + kActSets) * kShards,  // [2][kShards] delta counts (two delta sets)
-  CTR_FAIL = (3 + kActSets) * kShards,   // sticky bipartiteness failure
+  CTR_NV = 0,                    // [kShards] new-vertex counts (= vertex-list fill per shard)
+  CTR_DELTA = kShards,           // [kShards] delta-record counts
+  CTR_FAIL = 2 * kShards,        // sticky bipartiteness failure
   CTR_ERR,                       // device-side error (table overflow)
   CTR_EXPORT,                    // export append counter
-  CTR_OVF,                       // delta / active list overflow
-  CTR_STAGE_N,                   // records staged by the running k_stage (u32 pair = u64)
-  CTR_STAGE_N_HI,
+  CTR_OVF,                       // delta list overflow
+  CTR_VOVF,                      // vertex list overflow (exports / resets fall back to table scans)
   CTR_STAGE_DONE,                // k_stage block ticket
-  CTR_SENT,                      // records sent by all stages since reset (u64)
+  CTR_SENT,                      // records staged since reset (u64)
+  CTR_SENT_HI,
   CTR_EDONE,                     // edges of completed folds since reset (u64, k_report)
+  CTR_EDONE_HI,
+  CTR_EMIT,                      // change-emission output rows (u64)
+  CTR_EMIT_HI,
+  CTR_BIG,                       // change emission: hooked roots too large to walk
+  CTR_SCAN_ALL,                  // change emission: emit every vertex (after a table rebuild)
   CTR_DBG_HOOKS,                 // debug build (-DGS_DEBUG_COUNTERS): hook calls,
   CTR_DBG_ITERS,                 //   hook-loop iterations,
   CTR_DBG_CASFAIL,               //   failed hook CASes
@@ -66,62 +63,36 @@ enum CounterBlock : int {
 };
 __host__ __device__ constexpr int ctr_index(int c) { return c * kCtrStride; }
 
-#ifdef GS_DIAG_WAVES
-// Diagnostic build only (tools/diag_fold.hip): per-thread event counts of k_fold
-// {find steps, hook iterations, failed hook CASes, probe steps, key settles}.
-constexpr uint32_t kDiagThreads = 1u << 22;
-extern __device__ uint32_t gs_diag_cnt[kDiagThreads * 5];
-#define GS_DIAG(k)                                                              \
-  do {                                                                          \
-    const uint32_t dtid_ = blockIdx.x * blockDim.x + threadIdx.x;               \
-    if (dtid_ < kDiagThreads) gs_diag_cnt[dtid_ * 5 + (k)]++;                   \
-  } while (0)
-#else
-#define GS_DIAG(k) ((void)0)
-#endif
+// aux bits of a slot
+constexpr uint32_t kAuxPresent = 1u;  // reserved slot only: INT64_MIN is a vertex
+constexpr uint32_t kAuxNew = 2u;      // change tracking: inserted since the last emission
 
 struct alignas(16) Slot {
   int64_t key;
   uint32_t link;  // parent slot << 1 | parity(v) ^ parity(parent)
-  uint32_t aux;   // bit 0: reserved slot present
+  uint32_t aux;
 };
 
-// Slot index space: [0, hotcap) hot level | [hotcap, hotcap + cap) cold level |
-// r0 = hotcap + cap (id INT64_MIN) | r0 + 1 (id INT64_MIN + 1). The hot level holds
-// the vertices inserted while it is open -- in a skewed stream the early, high-
-// degree ones -- densely enough to stay resident in the Infinity Cache.
 struct Table {
   Slot* tab;
   uint32_t* ctr;
-  uint32_t hotcap;  // 0: no hot level
-  uint32_t hotmask;
-  int hotshift;
-  int hot_open;     // inserts may go to the hot level
-  uint32_t cap;     // cold level size (power of two)
-  uint32_t mask;    // cap - 1
-  int shift;        // 64 - log2(cap)
-  uint32_t r0;      // reserved slots r0 (INT64_MIN) and r0 + 1 (INT64_MIN + 1)
+  uint32_t cap;        // hashed slots (power of two)
+  uint32_t mask;       // cap - 1
+  int shift;           // 64 - log2(cap)
+  uint32_t r0;         // reserved slot of INT64_MIN (== cap)
+  uint32_t* vlist;     // vertex list [kShards][vshard_cap] (dense ids), or null
+  uint32_t vshard_cap;
+  int mark_new;        // change tracking: fresh inserts set kAuxNew
 };
 
-struct Lists {
-  uint2* act;            // active (root<<1|parity, root) entries, [kActSets][kShards][act_shard_cap]
-  uint32_t act_shard_cap;
-  int64_t* drec;         // delta records {a, b, parity} of this set, [kShards][delta_shard_cap][3]
-  uint32_t delta_shard_cap;
-  uint32_t dctr;         // counter index of this set's shard 0 (CTR_DELTA + set * kShards)
+struct Delta {
+  int64_t* drec;       // records {a, b, parity} [kShards][shard_cap][3], or null (not tracking)
+  uint32_t shard_cap;
 };
 
 __device__ __forceinline__ uint32_t hash_slot(int64_t key, int shift) {
   return (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ull) >> shift);
 }
-
-// Slot of a key's first probe: its hot bucket's first slot if there is a hot level
-// (buckets are kHotBucket aligned slots), else the cold level.
-__device__ __forceinline__ uint32_t first_probe_slot(const Table& t, int64_t key) {
-  return t.hotcap ? (hash_slot(key, t.hotshift) & ~(kHotBucket - 1)) : hash_slot(key, t.shift);
-}
-
-__device__ __forceinline__ bool is_reserved_key(int64_t key) { return key == kEmpty || key == kSealed; }
 
 __device__ __forceinline__ void load_slot(const Slot* p, int64_t& key, uint32_t& link) {
   // one 16-B load (global_load_dwordx4): key + link in the same request
@@ -137,97 +108,34 @@ __device__ __forceinline__ uint32_t load_link_fresh(const Slot* p) {
 // A key read as EMPTY for an occupied slot is a stale line: settle it at the
 // memory-side atomic unit (rare path).
 __device__ __forceinline__ int64_t settle_key(const Table& t, uint32_t s, int64_t k) {
-  if (k == kEmpty && s != t.r0) {
-    GS_DIAG(4);
-    k = (int64_t)atomicOr((unsigned long long*)&t.tab[s].key, 0ull);
-  }
+  if (k == kEmpty && s != t.r0) k = (int64_t)atomicOr((unsigned long long*)&t.tab[s].key, 0ull);
   return k;
 }
 
-// Hot level: a key lives in its bucket (kHotBucket aligned slots) or not at all.
-// The whole bucket is read at once (independent 16-B loads, one round trip) and
-// scanned in registers. While the level is open an EMPTY slot is claimed by CAS;
-// once closed, the first EMPTY slot of the bucket is sealed (CAS EMPTY -> kSealed)
-// so nothing can be inserted there later: a lookup that meets a seal, or a full
-// bucket of other keys, continues in the cold level. A key is therefore in at most
-// one level. Returns the slot, or kNoSlot to continue in the cold level.
-struct HotBucket {
-  int64_t k[kHotBucket];
-  uint32_t l[kHotBucket];
-};
-
-__device__ __forceinline__ void load_bucket(const Table& t, uint32_t b0, HotBucket& hb) {
-#pragma unroll
-  for (uint32_t i = 0; i < kHotBucket; ++i) load_slot(t.tab + b0 + i, hb.k[i], hb.l[i]);
-}
-
-// (the bucket at b0 was loaded into hb by the caller)
-__device__ __forceinline__ uint32_t hot_resolve(const Table& t, int64_t key, uint32_t b0, const HotBucket& hb,
-                                                uint32_t& link, bool& fresh) {
-  const int64_t* k = hb.k;
-  const uint32_t* l = hb.l;
-#pragma unroll
-  for (uint32_t i = 0; i < kHotBucket; ++i) {
-    if (k[i] == key) {
-      link = l[i];
-      return b0 + i;
-    }
-  }
-  for (uint32_t i = 0; i < kHotBucket; ++i) {
-    int64_t ki = k[i];
-    if (ki == kEmpty) {
-      const int64_t want = t.hot_open ? key : kSealed;
-      const unsigned long long old = atomicCAS((unsigned long long*)&t.tab[b0 + i].key, (unsigned long long)kEmpty,
-                                               (unsigned long long)want);
-      if (old == (unsigned long long)kEmpty) {
-        if (!t.hot_open) return kNoSlot;
-        fresh = true;
-        link = (b0 + i) << 1;
-        return b0 + i;
-      }
-      ki = (int64_t)old;
-      if (ki == key) {
-        link = t.tab[b0 + i].link;
-        return b0 + i;
-      }
-    }
-    if (ki == kSealed) return kNoSlot;
-  }
-  return kNoSlot;  // bucket full of other keys
-}
-
-// Insert-or-find of one id. Its first probe was already loaded by the caller
-// (callers issue both endpoints' first loads back to back so they overlap): with a
-// hot level the bucket at h into hb, else the cold slot h into (k, l). Returns the
-// slot (dense id), its observed link and whether this call inserted it.
+// Insert-or-find of one id. Its first probe (slot h, loaded into k, l) was issued by
+// the caller (callers issue both endpoints' first loads back to back so they
+// overlap). Returns the slot (dense id), its observed link and whether this call
+// inserted it.
 __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, uint32_t h, int64_t k, uint32_t l,
-                                                   const HotBucket& hb, uint32_t& link, bool& fresh) {
+                                                   uint32_t& link, bool& fresh) {
   fresh = false;
-  if (is_reserved_key(key)) {
-    const uint32_t r = t.r0 + (key == kSealed ? 1u : 0u);
-    const uint32_t old = atomicOr(&t.tab[r].aux, 1u);
-    fresh = (old & 1u) == 0;
-    link = t.tab[r].link;
-    return r;
-  }
-  if (t.hotcap) {
-    const uint32_t s = hot_resolve(t, key, h, hb, link, fresh);
-    if (s != kNoSlot) return s;
-    h = t.hotcap + hash_slot(key, t.shift);
-    load_slot(t.tab + h, k, l);
+  if (key == kEmpty) {
+    const uint32_t old = atomicOr(&t.tab[t.r0].aux, kAuxPresent);
+    fresh = (old & kAuxPresent) == 0;
+    if (fresh && t.mark_new) atomicOr(&t.tab[t.r0].aux, kAuxNew);
+    link = t.tab[t.r0].link;
+    return t.r0;
   }
   for (uint32_t probes = 0; probes <= t.mask; ++probes) {
-    GS_DIAG(3);
     if (k == key) {
       link = l;
       return h;
     }
-    if (k == kEmpty && kInsertTTAS) {
+    if (k == kEmpty) {
       // test-and-test-and-set: an EMPTY read may be a stale line of a hub's slot that
       // another XCD has filled; a fresh load settles it without queueing a CAS on
       // that address (all of a hub's occurrences in a batch would otherwise CAS it)
-      k = (int64_t)__hip_atomic_load((unsigned long long*)&t.tab[h].key, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
+      k = (int64_t)__hip_atomic_load((unsigned long long*)&t.tab[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (k == key) {
         link = load_link_fresh(t.tab + h);
         return h;
@@ -238,15 +146,16 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
           atomicCAS((unsigned long long*)&t.tab[h].key, (unsigned long long)kEmpty, (unsigned long long)key);
       if (old == (unsigned long long)kEmpty) {
         fresh = true;
+        if (t.mark_new) t.tab[h].aux = kAuxNew;  // only the inserting thread writes a fresh slot's aux
         link = h << 1;  // table init: every slot is its own root
         return h;
       }
       if ((int64_t)old == key) {
-        link = t.tab[h].link;
+        link = load_link_fresh(t.tab + h);
         return h;
       }
     }
-    h = t.hotcap + ((h - t.hotcap + 1) & t.mask);
+    h = (h + 1) & t.mask;
     load_slot(t.tab + h, k, l);
   }
   atomicOr(&t.ctr[ctr_index(CTR_ERR)], 1u);
@@ -254,41 +163,47 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
 }
 
 __device__ __forceinline__ uint32_t lookup_insert(const Table& t, int64_t key, uint32_t& link, bool& fresh) {
-  const uint32_t h = first_probe_slot(t, key);
-  int64_t k = 0;
-  uint32_t l = 0;
-  HotBucket hb;
-  if (t.hotcap)
-    load_bucket(t, h, hb);
-  else
-    load_slot(t.tab + h, k, l);
-  return lookup_resolve(t, key, h, k, l, hb, link, fresh);
+  const uint32_t h = hash_slot(key, t.shift);
+  int64_t k;
+  uint32_t l;
+  load_slot(t.tab + h, k, l);
+  return lookup_resolve(t, key, h, k, l, link, fresh);
 }
 
-// Read-only lookup (no insert, no seal): slot or kNoSlot.
+// Read-only lookup (no insert): slot or kNoSlot.
 __device__ __forceinline__ uint32_t lookup_find(const Table& t, int64_t key, uint32_t& link) {
-  if (is_reserved_key(key)) {
-    const uint32_t r = t.r0 + (key == kSealed ? 1u : 0u);
-    link = t.tab[r].link;
-    return (t.tab[r].aux & 1u) ? r : kNoSlot;
+  if (key == kEmpty) {
+    link = t.tab[t.r0].link;
+    return (t.tab[t.r0].aux & kAuxPresent) ? t.r0 : kNoSlot;
   }
   int64_t k;
-  if (t.hotcap) {
-    const uint32_t b0 = hash_slot(key, t.hotshift) & ~(kHotBucket - 1);
-    for (uint32_t i = 0; i < kHotBucket; ++i) {
-      load_slot(t.tab + b0 + i, k, link);
-      if (k == key) return b0 + i;
-      if (k == kEmpty || k == kSealed) break;
-    }
-  }
-  uint32_t h = t.hotcap + hash_slot(key, t.shift);
+  uint32_t h = hash_slot(key, t.shift);
   for (uint32_t probes = 0; probes <= t.mask; ++probes) {
     load_slot(t.tab + h, k, link);
     if (k == key) return h;
     if (k == kEmpty) return kNoSlot;
-    h = t.hotcap + ((h - t.hotcap + 1) & t.mask);
+    h = (h + 1) & t.mask;
   }
   return kNoSlot;
+}
+
+// Register fresh inserts: the shard's new-vertex count (capacity tracking) doubles
+// as the append position of the vertex list; change tracking needs nothing more
+// (lookup_resolve marked the slots).
+__device__ __forceinline__ void note_new_vertices(const Table& t, int shard, bool nu, uint32_t su, bool nv,
+                                                  uint32_t sv) {
+  const bool second = nv && sv != su;
+  const uint32_t k = (nu ? 1u : 0u) + (second ? 1u : 0u);
+  if (!k) return;
+  const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], k);
+  if (!t.vlist) return;
+  if (pos + k > t.vshard_cap) {
+    atomicOr(&t.ctr[ctr_index(CTR_VOVF)], 1u);
+    return;
+  }
+  uint32_t* vl = t.vlist + (size_t)shard * t.vshard_cap + pos;
+  if (nu) *vl++ = su;
+  if (second) *vl = sv;
 }
 
 // One step of a find with path splitting. (x, lx, kx): current slot, its link and
@@ -297,7 +212,6 @@ __device__ __forceinline__ uint32_t lookup_find(const Table& t, int64_t key, uin
 // non-root forever and the grandparent is an ancestor: a benign race).
 __device__ __forceinline__ void find_step(const Table& t, uint32_t& x, uint32_t& lx, int64_t& kx, uint32_t& acc,
                                           bool& done, int64_t kp, uint32_t lp) {
-  GS_DIAG(0);
   const uint32_t p = lx >> 1;
   const uint32_t gp = lp >> 1;
   acc ^= lx & 1u;
@@ -344,20 +258,18 @@ __device__ __forceinline__ void find_root2(const Table& t, uint32_t& xa, uint32_
   kb = settle_key(t, xb, kb);
 }
 
-// Compatibility wrapper: (root, parity, key) of slot x with observed link lx.
-template <bool FRESH>
-__device__ __forceinline__ void find_root(const Table& t, uint32_t x, uint32_t lx, int64_t kx, uint32_t& root,
-                                          uint32_t& par, int64_t& rkey) {
-  uint32_t acc = 0;
-  find_root1<FRESH>(t, x, lx, kx, acc);
-  root = x;
-  par = acc;
-  rkey = kx;
+// Read-only find (no path splitting): root slot, key and parity of slot x.
+__device__ __forceinline__ uint32_t find_ro(const Table& t, uint32_t x, uint32_t lx, int64_t& kx, uint32_t& acc) {
+  acc = 0;
+  while ((lx >> 1) != x) {
+    acc ^= lx & 1u;
+    x = lx >> 1;
+    load_slot(t.tab + x, kx, lx);
+  }
+  kx = settle_key(t, x, kx);
+  return x;
 }
 
-// Hook loop: make a and b one set with colour(a) ^ colour(b) == need (SIGNED).
-// The larger-key root is hooked under the smaller key, so every root is the
-// minimum id of its tree (the canonical label) at all times.
 #ifdef GS_DEBUG_COUNTERS
 #define GS_DBG(c) atomicAdd(&t.ctr[ctr_index(c)], 1u)
 #else
@@ -410,26 +322,34 @@ __device__ __forceinline__ void combine_hooks(bool active, uint32_t& a, int64_t&
   }
 }
 
-// Hook-loop finds with agent-scope (memory-side) link loads, or plain L2-cached
-// loads: a stale root only costs a failed CAS, which returns the live link.
-#ifndef GS_HOOK_FRESH
-#define GS_HOOK_FRESH 1
-#endif
-constexpr bool kHookFresh = GS_HOOK_FRESH != 0;
-#ifndef GS_HOOK_TTAS
-#define GS_HOOK_TTAS 1
-#endif
-constexpr bool kHookTTAS = GS_HOOK_TTAS != 0;
+// Append one delta record {a, b, w} to shard `shard` of the delta list.
+__device__ __forceinline__ void append_record(const Table& t, const Delta& D, int shard, int64_t a, int64_t b,
+                                              int64_t w) {
+  const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_DELTA + shard)], 1u);
+  if (pos < D.shard_cap) {
+    int64_t* r = D.drec + ((size_t)shard * D.shard_cap + pos) * 3;
+    r[0] = a;
+    r[1] = b;
+    r[2] = w;
+  } else {
+    atomicOr(&t.ctr[ctr_index(CTR_OVF)], 1u);
+  }
+}
 
+// Hook loop: make a and b one set with colour(a) ^ colour(b) == need (SIGNED).
+// The larger-key root is hooked under the smaller key, so every root is the
+// minimum id of its tree (the canonical label) at all times. Finds read links with
+// agent-scope loads; before its CAS the loop re-reads the target root's link
+// (test-and-test-and-set): a root a concurrent hook already moved -- the hub root
+// while a giant component forms -- is followed without queueing a CAS on its address.
 template <bool SIGNED, bool TRACK>
-__device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, uint32_t a, uint32_t la, int64_t ka,
+__device__ __forceinline__ void hook(const Table& t, const Delta& D, int shard, uint32_t a, uint32_t la, int64_t ka,
                                      uint32_t b, uint32_t lb, int64_t kb, uint32_t need) {
   GS_DBG(CTR_DBG_HOOKS);
   while (true) {
     GS_DBG(CTR_DBG_ITERS);
-    GS_DIAG(1);
     uint32_t pa = 0, pb = 0;
-    find_root2<kHookFresh>(t, a, la, ka, pa, b, lb, kb, pb);
+    find_root2<true>(t, a, la, ka, pa, b, lb, kb, pb);
     la = a << 1;
     lb = b << 1;
     need ^= pa ^ pb;
@@ -442,28 +362,14 @@ __device__ __forceinline__ void hook(const Table& t, const Lists& L, int shard, 
     const uint32_t lo = a_lo ? a : b;
     const uint32_t expect = hi << 1;
     const uint32_t desired = (lo << 1) | (SIGNED ? (need & 1u) : 0u);
-    // test-and-test-and-set: a root that a concurrent hook already moved (the hub
-    // root while a giant component forms) is seen by a cheap fresh load instead of
-    // a CAS that would queue behind every other CAS on that address
-    const uint32_t seen = kHookTTAS ? load_link_fresh(t.tab + hi) : expect;
+    const uint32_t seen = load_link_fresh(t.tab + hi);
     const uint32_t old = seen == expect ? atomicCAS(&t.tab[hi].link, expect, desired) : seen;
     if (old == expect) {
-      if (TRACK) {
-        const uint32_t pos = atomicAdd(&t.ctr[ctr_index(L.dctr + shard)], 1u);
-        if (pos < L.delta_shard_cap) {
-          int64_t* r = L.drec + ((size_t)shard * L.delta_shard_cap + pos) * 3;
-          r[0] = a_lo ? kb : ka;
-          r[1] = a_lo ? ka : kb;
-          r[2] = (int64_t)(SIGNED ? (need & 1u) : 0u);
-        } else {
-          atomicOr(&t.ctr[ctr_index(CTR_OVF)], 1u);
-        }
-      }
+      if (TRACK) append_record(t, D, shard, a_lo ? kb : ka, a_lo ? ka : kb, (int64_t)(SIGNED ? (need & 1u) : 0u));
       return;
     }
     // hi was hooked meanwhile: continue that side from its live link
     GS_DBG(CTR_DBG_CASFAIL);
-    GS_DIAG(2);
     if (a_lo)
       lb = old;
     else

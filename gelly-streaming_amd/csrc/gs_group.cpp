@@ -1,0 +1,683 @@
+// gs_group.cpp -- native multi-GPU group (include/gs_group.h).
+//
+// Each rank folds its own shard of every global micro-batch into a REPLICA of the
+// global summary, and the replicas exchange their structural deltas over RCCL:
+//
+//   exchange b:  own fold b (tracked) -> stage b: records -> send[b%2], count word
+//                -> count all-gather (communicator C, stream xc) -> k_headers: the
+//                   gathered counts in host-mapped memory
+//   then, still inside the call for exchange b, the DATA of exchange b-1:
+//                host reads b-1's counts (already landed: they were gathered while
+//                fold b ran) -> data all-gather of exactly max-count rows per rank
+//                (communicator D, stream xd) -> fold of the other ranks' live rows
+//                on the apply (side) stream, overlapping this rank's next own fold.
+//
+// Only live rows move: the collective size is the largest record count of THIS
+// exchange, known before the data collective is issued, so nothing is queued,
+// padded to a capacity agreed in advance, or drained at the end. Two communicators
+// keep each one's collectives in issue order on one stream. This replaces the
+// reference's gather of per-partition summaries into one parallelism-1 reducer
+// (SummaryBulkAggregation.java:77-83) and its Merger (SummaryAggregation.java:107-119).
+#include <dlfcn.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gs_group.h"
+#include "gs_internal.hpp"
+
+using namespace gsi;
+
+namespace {
+
+constexpr int kIdBytes = 128;  // one ncclUniqueId
+constexpr uint64_t kMaxGroupBatch = 1ull << 26;
+
+struct RcclApi {
+  void* lib = nullptr;
+  int (*getUniqueId)(void*) = nullptr;
+  int (*allGather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
+  int (*commDestroy)(void*) = nullptr;
+  int (*send)(const void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  int (*recv)(void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  int (*groupStart)() = nullptr;
+  int (*groupEnd)() = nullptr;
+  const char* (*getErrorString)(int) = nullptr;
+  void* initRankSym = nullptr;  // ncclCommInitRank takes ncclUniqueId (128 B) by value: see Id128
+};
+
+struct Id128 {
+  char b[kIdBytes];
+};
+
+RcclApi g_rccl;
+
+int rccl_load() {
+  if (g_rccl.lib) return GS_OK;
+  void* l = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!l) l = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!l) return fail(GS_ERR_HIP, std::string("cannot load RCCL: ") + dlerror());
+  g_rccl.getUniqueId = (int (*)(void*))dlsym(l, "ncclGetUniqueId");
+  g_rccl.initRankSym = dlsym(l, "ncclCommInitRank");
+  g_rccl.allGather = (int (*)(const void*, void*, size_t, int, void*, hipStream_t))dlsym(l, "ncclAllGather");
+  g_rccl.commDestroy = (int (*)(void*))dlsym(l, "ncclCommDestroy");
+  g_rccl.getErrorString = (const char* (*)(int))dlsym(l, "ncclGetErrorString");
+  g_rccl.send = (int (*)(const void*, size_t, int, int, void*, hipStream_t))dlsym(l, "ncclSend");
+  g_rccl.recv = (int (*)(void*, size_t, int, int, void*, hipStream_t))dlsym(l, "ncclRecv");
+  g_rccl.groupStart = (int (*)())dlsym(l, "ncclGroupStart");
+  g_rccl.groupEnd = (int (*)())dlsym(l, "ncclGroupEnd");
+  if (!g_rccl.getUniqueId || !g_rccl.initRankSym || !g_rccl.allGather || !g_rccl.commDestroy)
+    return fail(GS_ERR_HIP, "RCCL is missing ncclGetUniqueId/ncclCommInitRank/ncclAllGather/ncclCommDestroy");
+  g_rccl.lib = l;
+  return GS_OK;
+}
+
+int rccl_fail(const RcclApi* api, const char* what, int r) {
+  return fail(GS_ERR_HIP, std::string(what) + ": " + (api && api->getErrorString ? api->getErrorString(r) : "rccl error"));
+}
+
+constexpr int kNcclInt64 = 4;  // ncclInt64 (rccl.h)
+constexpr int kNcclUint8 = 1;  // ncclUint8 (rccl.h)
+
+// ---------------------------------------------------------------------------
+// In-process emulation of the RCCL calls the group uses, selected with
+// GS_GROUP_FAKE_COMM=1: N threads of ONE process, each driving one rank's summary
+// on the same GPU, meet at host barriers; the data moves with device copies
+// ordered by events. Test infrastructure only (RCCL refuses two ranks on one GPU,
+// and the GPU box has one): it runs the group's N-rank code paths -- count and data
+// collectives, exchange-layout fold of real remote rows on the side stream, the
+// binomial tree -- exactly as with RCCL.
+struct FakeShared {
+  int n = 0, refs = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  std::vector<const void*> src;
+  std::vector<hipEvent_t> ev;
+  struct Msg {
+    const void* buf;
+    size_t bytes;
+    hipEvent_t ready, copied;
+    bool done = false;
+  };
+  std::map<std::pair<int, int>, std::deque<Msg*>> box;  // (from, to) -> messages
+};
+struct FakeComm {
+  FakeShared* s;
+  int rank;
+  hipEvent_t ready = nullptr, done = nullptr;
+  std::vector<hipEvent_t> spare;  // message events, destroyed with the comm
+};
+std::mutex g_fake_mu;
+std::map<std::string, FakeShared*> g_fake_reg;
+
+void fake_barrier(FakeShared* s) {
+  std::unique_lock<std::mutex> lk(s->m);
+  const uint64_t g0 = s->gen;
+  if (++s->arrived == s->n) {
+    s->arrived = 0;
+    s->gen++;
+    s->cv.notify_all();
+  } else {
+    s->cv.wait(lk, [&] { return s->gen != g0; });
+  }
+}
+size_t fake_elem(int dtype) { return dtype == kNcclUint8 ? 1 : 8; }
+int fake_unique_id(void* id) {
+  static std::atomic<uint64_t> ctr{1};
+  memset(id, 0, kIdBytes);
+  const uint64_t v[2] = {(uint64_t)getpid(), ctr++};
+  memcpy(id, v, sizeof v);
+  return 0;
+}
+int fake_init(void** comm, int n, Id128 id, int rank) {
+  std::lock_guard<std::mutex> lk(g_fake_mu);
+  FakeShared*& s = g_fake_reg[std::string(id.b, kIdBytes)];
+  if (!s) {
+    s = new FakeShared();
+    s->n = n;
+    s->src.resize(n);
+    s->ev.resize(n);
+  }
+  s->refs++;
+  FakeComm* c = new FakeComm{s, rank};
+  if (hipEventCreateWithFlags(&c->ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess)
+    return 1;
+  *comm = c;
+  return 0;
+}
+int fake_destroy(void* comm) {
+  FakeComm* c = (FakeComm*)comm;
+  (void)hipEventDestroy(c->ready);
+  (void)hipEventDestroy(c->done);
+  for (hipEvent_t e : c->spare) (void)hipEventDestroy(e);
+  std::lock_guard<std::mutex> lk(g_fake_mu);
+  if (--c->s->refs == 0) {
+    for (auto it = g_fake_reg.begin(); it != g_fake_reg.end(); ++it)
+      if (it->second == c->s) {
+        g_fake_reg.erase(it);
+        break;
+      }
+    delete c->s;
+  }
+  delete c;
+  return 0;
+}
+int fake_all_gather(const void* send, void* recv, size_t count, int dtype, void* comm, hipStream_t st) {
+  FakeComm* c = (FakeComm*)comm;
+  FakeShared* s = c->s;
+  const size_t bytes = count * fake_elem(dtype);
+  if (hipEventRecord(c->ready, st) != hipSuccess) return 1;
+  {
+    std::lock_guard<std::mutex> lk(s->m);
+    s->src[c->rank] = send;
+    s->ev[c->rank] = c->ready;
+  }
+  fake_barrier(s);  // every rank's send buffer is staged (in its stream order)
+  for (int q = 0; q < s->n; ++q) {
+    if (hipStreamWaitEvent(st, s->ev[q], 0) != hipSuccess) return 1;
+    if (bytes && hipMemcpyAsync((char*)recv + (size_t)q * bytes, s->src[q], bytes, hipMemcpyDeviceToDevice, st) !=
+                     hipSuccess)
+      return 1;
+  }
+  if (hipEventRecord(c->done, st) != hipSuccess) return 1;
+  fake_barrier(s);  // (the ready events were captured by every stream's wait)
+  {
+    std::lock_guard<std::mutex> lk(s->m);
+    s->ev[c->rank] = c->done;
+  }
+  fake_barrier(s);
+  // the collective completes on this rank once every rank has read its send buffer
+  for (int q = 0; q < s->n; ++q)
+    if (q != c->rank && hipStreamWaitEvent(st, s->ev[q], 0) != hipSuccess) return 1;
+  fake_barrier(s);  // slots and events may be reused after this
+  return 0;
+}
+int fake_send(const void* buf, size_t count, int dtype, int peer, void* comm, hipStream_t st) {
+  FakeComm* c = (FakeComm*)comm;
+  FakeShared* s = c->s;
+  FakeShared::Msg msg{buf, count * fake_elem(dtype), nullptr, nullptr};
+  if (hipEventCreateWithFlags(&msg.ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&msg.copied, hipEventDisableTiming) != hipSuccess || hipEventRecord(msg.ready, st))
+    return 1;
+  c->spare.push_back(msg.ready);
+  c->spare.push_back(msg.copied);
+  std::unique_lock<std::mutex> lk(s->m);
+  s->box[{c->rank, peer}].push_back(&msg);
+  s->cv.notify_all();
+  s->cv.wait(lk, [&] { return msg.done; });  // the receiver has queued its copy
+  return hipStreamWaitEvent(st, msg.copied, 0) == hipSuccess ? 0 : 1;
+}
+int fake_recv(void* buf, size_t count, int dtype, int peer, void* comm, hipStream_t st) {
+  FakeComm* c = (FakeComm*)comm;
+  FakeShared* s = c->s;
+  std::unique_lock<std::mutex> lk(s->m);
+  auto& q = s->box[{peer, c->rank}];
+  s->cv.wait(lk, [&] { return !q.empty(); });
+  FakeShared::Msg* msg = q.front();
+  q.pop_front();
+  int r = 0;
+  if (msg->bytes != count * fake_elem(dtype)) r = 1;
+  if (!r && (hipStreamWaitEvent(st, msg->ready, 0) != hipSuccess ||
+             hipMemcpyAsync(buf, msg->buf, msg->bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+             hipEventRecord(msg->copied, st) != hipSuccess))
+    r = 1;
+  msg->done = true;
+  s->cv.notify_all();
+  return r;
+}
+int fake_noop() { return 0; }
+const char* fake_error(int) { return "in-process comm emulation error"; }
+
+RcclApi make_fake_api() {
+  RcclApi a;
+  a.lib = (void*)&g_fake_reg;
+  a.getUniqueId = fake_unique_id;
+  a.allGather = fake_all_gather;
+  a.commDestroy = fake_destroy;
+  a.send = fake_send;
+  a.recv = fake_recv;
+  a.groupStart = fake_noop;
+  a.groupEnd = fake_noop;
+  a.getErrorString = fake_error;
+  a.initRankSym = (void*)&fake_init;
+  return a;
+}
+const RcclApi g_fake = make_fake_api();
+
+// the communication API a new group (or id) uses
+int comm_api(const RcclApi** api) {
+  const char* f = getenv("GS_GROUP_FAKE_COMM");
+  if (f && atoi(f) != 0) {
+    *api = &g_fake;
+    return GS_OK;
+  }
+  if (int rc = rccl_load()) return rc;
+  *api = &g_rccl;
+  return GS_OK;
+}
+
+}  // namespace
+
+struct gs_group {
+  gs_summary* h = nullptr;
+  const RcclApi* api = nullptr;  // RCCL, or the in-process emulation (GS_GROUP_FAKE_COMM=1, tests)
+  void* comm_c = nullptr;        // count collectives (stream xc)
+  void* comm_d = nullptr;        // data collectives (stream xd) and the tree combine
+  int nranks = 1, rank = 0;
+  int width = 3;                 // int64 per exchange row: {a, b} for CC (16 B), {a, b, parity} signed
+  bool exchange = false;         // false: tree-combine-only group
+  bool self_apply = false;       // test knob (GS_GROUP_SELF_APPLY=1): also fold this rank's own rows back
+  uint64_t batch = 0, rows_cap = 0;
+  // double-buffered exchange: exchange b uses buffer set b % 2
+  int64_t* send[2] = {nullptr, nullptr};                // [rows_cap * width]
+  int64_t* recv[2] = {nullptr, nullptr};                // [nranks * rows_cap * width]
+  unsigned long long* cnt = nullptr;                    // device: [2] send counts, then [2][nranks] gathered
+  long long* hdr_host = nullptr;                        // pinned host-mapped [2][nranks + 1]
+  long long* hdr_dev = nullptr;
+  hipStream_t xc = nullptr, xd = nullptr, as = nullptr;  // counts, data, apply (the summary's side stream)
+  hipEvent_t as_ev = nullptr;
+  hipEvent_t staged[2] = {}, counted[2] = {}, gathered[2] = {}, applied[2] = {};
+  bool used[2] = {false, false};
+  uint64_t b = 0;       // exchanges since create / finish
+  bool pend = false;    // exchange b - 1 has its counts gathered but not its data
+  // statistics
+  uint64_t exchanges = 0, rows_received = 0, live_received = 0;
+  bool hostprof = false;  // GS_GROUP_HOSTPROF=1: host seconds per phase, printed at destroy
+  double hp[4] = {};      // own fold, stage + count collective, wait for counts, data collective + apply
+  uint64_t hp_calls = 0;
+
+  unsigned long long* cnt_send(int k) const { return cnt + k; }
+  unsigned long long* cnt_recv(int k) const { return cnt + 2 + (size_t)k * nranks; }
+  long long* hdr(int k) const { return hdr_host + (size_t)k * (nranks + 1); }
+};
+
+namespace {
+
+struct HostTimer {
+  double* acc;
+  std::chrono::steady_clock::time_point t0;
+  explicit HostTimer(double* a) : acc(a), t0(std::chrono::steady_clock::now()) {}
+  void lap(double* next) {  // charge the time so far to acc, continue on next
+    const auto t = std::chrono::steady_clock::now();
+    if (acc) *acc += std::chrono::duration<double>(t - t0).count();
+    t0 = t;
+    acc = next;
+  }
+  ~HostTimer() { lap(nullptr); }
+};
+
+// The data half of exchange e: wait for its gathered counts (host-mapped), gather
+// exactly max-count rows per rank, fold the other ranks' live rows on the apply
+// stream. No host synchronisation beyond the count poll.
+int finish_data(gs_group* g, uint64_t e) {
+  gs_summary* h = g->h;
+  const int k = (int)(e & 1u);
+  HostTimer ht(g->hostprof ? &g->hp[2] : nullptr);
+  volatile long long* hd = g->hdr(k);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (__atomic_load_n(&hd[g->nranks], __ATOMIC_ACQUIRE) != (long long)e) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) {  // long wait: block
+      GS_HIP(hipEventSynchronize(g->counted[k]));
+      if (__atomic_load_n(&hd[g->nranks], __ATOMIC_ACQUIRE) != (long long)e)
+        return fail(GS_ERR_HIP, "exchange count sequence mismatch");
+      break;
+    }
+  }
+  uint64_t maxc = 0, live = 0;
+  for (int r = 0; r < g->nranks; ++r) {
+    const uint64_t c = (uint64_t)hd[r] & (gs::kFailBit - 1);
+    if (c > g->rows_cap) return fail(GS_ERR_HIP, "exchange count above the delta capacity");
+    maxc = std::max(maxc, c);
+    if (r != g->rank || g->self_apply) live += c;
+  }
+  const uint64_t rows = std::max<uint64_t>(maxc, 1);  // >= 1 row: the fold reads every block's failure bit
+  ht.lap(g->hostprof ? &g->hp[3] : nullptr);
+  GS_HIP(hipStreamWaitEvent(g->xd, g->counted[k], 0));  // behind the stage (and the count collective)
+  if (g->used[k] && e >= 2) GS_HIP(hipStreamWaitEvent(g->xd, g->applied[k], 0));  // recv[k]: fold of e - 2 done
+  const int r = g->api->allGather(g->send[k], g->recv[k], rows * g->width, kNcclInt64, g->comm_d, g->xd);
+  if (r != 0) return rccl_fail(g->api, "ncclAllGather(data)", r);
+  GS_HIP(hipEventRecord(g->gathered[k], g->xd));
+  const bool use_side = side_ok(h);
+  hipStream_t s = use_side ? h->side : h->stream;
+  if (g->nranks > 1 || g->self_apply) {
+    GS_HIP(hipStreamWaitEvent(s, g->gathered[k], 0));
+    FoldSource fs;
+    fs.rows = (uint32_t)rows;
+    fs.skip_rank = g->self_apply ? -1 : g->rank;
+    fs.counts = g->cnt_recv(k);
+    fs.units = live;
+    fs.on_side = use_side;
+    const uint8_t* w = g->width == 3 ? reinterpret_cast<const uint8_t*>(g->recv[k] + 2) : nullptr;
+    if (int rc = fold_device_impl(h, g->recv[k], g->recv[k] + 1, w, (size_t)g->nranks * rows, g->width,
+                                  8 * g->width, /*track=*/false, true, fs))
+      return rc;
+  }
+  GS_HIP(hipEventRecord(g->applied[k], s));
+  g->rows_received += rows * (uint64_t)(g->nranks - 1);
+  g->live_received += live;
+  return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_group_unique_id(void* id) {
+  if (!id) return fail(GS_ERR_INVALID, "id is null");
+  const RcclApi* api = nullptr;
+  if (int rc = comm_api(&api)) return rc;
+  for (int i = 0; i < 2; ++i) {  // two communicators: counts and data
+    const int r = api->getUniqueId(static_cast<char*>(id) + i * kIdBytes);
+    if (r) return rccl_fail(api, "ncclGetUniqueId", r);
+  }
+  return GS_OK;
+}
+
+int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, int rank, size_t batch_edges) {
+  if (!out || !id) return fail(GS_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (!h) return fail(GS_ERR_INVALID, "null handle");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(GS_ERR_INVALID, "bad group shape");
+  if (batch_edges > kMaxGroupBatch) return fail(GS_ERR_INVALID, "batch_edges above 2^26");
+  const RcclApi* api = nullptr;
+  if (int rc = comm_api(&api)) return rc;
+  DeviceGuard dg(h->device);
+  gs_group* g = new gs_group();
+  g->h = h;
+  g->api = api;
+  g->nranks = nranks;
+  g->rank = rank;
+  g->width = h->kind == GS_KIND_SIGNED ? 3 : 2;
+  g->exchange = batch_edges != 0;
+  g->batch = batch_edges;
+  if (const char* m = getenv("GS_GROUP_SELF_APPLY")) g->self_apply = atoi(m) != 0;
+  if (const char* m = getenv("GS_GROUP_HOSTPROF")) g->hostprof = atoi(m) != 0;
+  auto bail = [&](int code) {
+    gs_group_destroy(g);
+    return code;
+  };
+  if (g->exchange) {
+    if (h->side) return bail(fail(GS_ERR_INVALID, "the summary already belongs to an exchange group"));
+    if (int rc = join_lanes(h)) return bail(rc);
+    if (int rc = ensure_delta_list(h, batch_edges)) return bail(rc);
+    if (int rc = gs_set_delta_tracking(h, 1)) return bail(rc);
+    g->rows_cap = (uint64_t)gs::kShards * h->delta_shard_cap;
+    bool ok = hipHostMalloc(&g->hdr_host, 2 * (size_t)(nranks + 1) * 8, hipHostMallocMapped | hipHostMallocCoherent) ==
+                  hipSuccess &&
+              hipHostGetDevicePointer(reinterpret_cast<void**>(&g->hdr_dev), g->hdr_host, 0) == hipSuccess &&
+              hipMalloc(&g->cnt, (2 + 2 * (size_t)nranks) * 8) == hipSuccess &&
+              hipStreamCreateWithFlags(&g->xc, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&g->xd, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&g->as, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&g->as_ev, hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; k < 2 && ok; ++k)
+      ok = hipMalloc(&g->send[k], g->rows_cap * g->width * 8) == hipSuccess &&
+           hipMalloc(&g->recv[k], (size_t)nranks * g->rows_cap * g->width * 8) == hipSuccess &&
+           hipEventCreateWithFlags(&g->staged[k], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&g->counted[k], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&g->gathered[k], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&g->applied[k], hipEventDisableTiming) == hipSuccess;
+    if (!ok) return bail(fail(GS_ERR_HIP, "group buffer allocation failed"));
+    for (int k = 0; k < 2; ++k) g->hdr(k)[nranks] = -1;  // no exchange yet
+    h->side = g->as;
+    h->side_ev = g->as_ev;
+    h->side_dirty = false;
+  }
+  typedef int (*InitRank)(void**, int, Id128, int);
+  Id128 uid;
+  if (g->exchange) {
+    memcpy(uid.b, id, kIdBytes);
+    const int r = ((InitRank)api->initRankSym)(&g->comm_c, nranks, uid, rank);
+    if (r != 0) return bail(rccl_fail(api, "ncclCommInitRank(counts)", r));
+  }
+  memcpy(uid.b, static_cast<const char*>(id) + kIdBytes, kIdBytes);
+  const int r = ((InitRank)api->initRankSym)(&g->comm_d, nranks, uid, rank);
+  if (r != 0) return bail(rccl_fail(api, "ncclCommInitRank(data)", r));
+  *out = g;
+  return GS_OK;
+}
+
+int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  if (!g->exchange) return fail(GS_ERR_INVALID, "tree-combine-only group (created with batch_edges 0)");
+  if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
+  if (n > g->batch) return fail(GS_ERR_INVALID, "n above the group's batch_edges");
+  const uint64_t b = g->b;
+  const int k = (int)(b & 1u);
+  g->hp_calls++;
+  HostTimer ht(g->hostprof ? &g->hp[0] : nullptr);
+  // buffer set k last served exchange b - 2: its data collective read send[k] and
+  // cnt_send[k] before this stage rewrites them
+  if (g->used[k]) GS_HIP(hipStreamWaitEvent(h->stream, g->gathered[k], 0));
+  if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, /*track=*/true)) return rc;
+  ht.lap(g->hostprof ? &g->hp[1] : nullptr);
+  if (int rc = stage_delta(h, g->send[k], g->rows_cap, g->width, g->cnt_send(k), h->kind == GS_KIND_SIGNED)) return rc;
+  GS_HIP(hipEventRecord(g->staged[k], h->stream));
+  GS_HIP(hipStreamWaitEvent(g->xc, g->staged[k], 0));
+  if (g->used[k]) GS_HIP(hipStreamWaitEvent(g->xc, g->applied[k], 0));  // cnt_recv[k]: fold of b - 2 read it
+  const int r = g->api->allGather(g->cnt_send(k), g->cnt_recv(k), 1, kNcclInt64, g->comm_c, g->xc);
+  if (r != 0) return rccl_fail(g->api, "ncclAllGather(counts)", r);
+  gs::launch_headers(g->cnt_recv(k), g->nranks, g->hdr_dev + (size_t)k * (g->nranks + 1), (long long)b, g->xc);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipEventRecord(g->counted[k], g->xc));
+  g->used[k] = true;
+  ht.lap(nullptr);
+  // the data of the previous exchange: its counts landed while this fold was queued
+  if (g->pend)
+    if (int rc = finish_data(g, b - 1)) return rc;
+  g->pend = true;
+  g->b++;
+  g->exchanges++;
+  return GS_OK;
+}
+
+int gs_group_fold_batches_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n, size_t batch) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  if (batch == 0) return fail(GS_ERR_INVALID, "batch is 0");
+  for (size_t off = 0; off < n; off += batch)
+    if (int rc = gs_group_fold_device(g, src + off, dst + off, std::min(batch, n - off))) return rc;
+  return GS_OK;
+}
+
+int gs_group_finish(gs_group_t g) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  if (g->pend) {
+    if (int rc = finish_data(g, g->b - 1)) return rc;
+    g->pend = false;
+  }
+  if (int rc = gs_sync(h)) return rc;  // joins the apply stream
+  if (g->xc) GS_HIP(hipStreamSynchronize(g->xc));
+  if (g->xd) GS_HIP(hipStreamSynchronize(g->xd));
+  g->b = 0;
+  g->used[0] = g->used[1] = false;
+  if (g->hdr_host)
+    for (int k = 0; k < 2; ++k) __atomic_store_n(&g->hdr(k)[g->nranks], (long long)-1, __ATOMIC_RELEASE);
+  return GS_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// one tree edge, sending side: header {count, failed}, then the three arrays
+int tree_send(gs_group* g, int peer, int64_t* hdr) {
+  gs_summary* h = g->h;
+  uint64_t nv = 0;
+  if (int rc = read_nv(h, &nv)) return rc;
+  int64_t *v = nullptr, *l = nullptr;
+  uint8_t* p = nullptr;
+  auto release = [&] {
+    (void)hipFree(v);
+    (void)hipFree(l);
+    (void)hipFree(p);
+  };
+  if (hipMalloc(&v, (nv + 1) * 8) != hipSuccess || hipMalloc(&l, (nv + 1) * 8) != hipSuccess ||
+      hipMalloc(&p, nv + 1) != hipSuccess) {
+    release();
+    return fail(GS_ERR_HIP, "tree combine: out of device memory");
+  }
+  size_t got = 0;
+  uint32_t failed = 0;
+  int rc = export_device_impl(h, v, l, p, nv + 1, &got);
+  if (!rc && (hipMemcpyAsync(&failed, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream) !=
+                  hipSuccess ||
+              hipStreamSynchronize(h->stream) != hipSuccess))
+    rc = fail(GS_ERR_HIP, "tree combine: flag read failed");
+  const int64_t hv[2] = {(int64_t)got, (int64_t)(failed != 0)};
+  if (!rc && hipMemcpyAsync(hdr, hv, 16, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+    rc = fail(GS_ERR_HIP, "tree combine: header copy failed");
+  if (!rc) {
+    const int r = g->api->send(hdr, 2, kNcclInt64, peer, g->comm_d, h->stream);
+    if (r) rc = rccl_fail(g->api, "ncclSend", r);
+  }
+  if (!rc && got) {
+    g->api->groupStart();
+    int r = g->api->send(v, got, kNcclInt64, peer, g->comm_d, h->stream);
+    if (!r) r = g->api->send(l, got, kNcclInt64, peer, g->comm_d, h->stream);
+    if (!r) r = g->api->send(p, got, kNcclUint8, peer, g->comm_d, h->stream);
+    const int e = g->api->groupEnd();
+    if (r || e) rc = rccl_fail(g->api, "ncclSend", r ? r : e);
+  }
+  if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(GS_ERR_HIP, "tree combine: sync failed");
+  release();  // the sends have completed
+  return rc;
+}
+
+// one tree edge, receiving side: fold the peer's exported summary into this one
+int tree_recv(gs_group* g, int peer, int64_t* hdr) {
+  gs_summary* h = g->h;
+  int r = g->api->recv(hdr, 2, kNcclInt64, peer, g->comm_d, h->stream);
+  if (r) return rccl_fail(g->api, "ncclRecv", r);
+  int64_t hv[2] = {0, 0};
+  GS_HIP(hipMemcpyAsync(hv, hdr, 16, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  const size_t got = (size_t)hv[0];
+  int64_t *v = nullptr, *l = nullptr;
+  uint8_t* p = nullptr;
+  auto release = [&] {
+    (void)hipFree(v);
+    (void)hipFree(l);
+    (void)hipFree(p);
+  };
+  int rc = GS_OK;
+  if (got && (hipMalloc(&v, got * 8) != hipSuccess || hipMalloc(&l, got * 8) != hipSuccess ||
+              hipMalloc(&p, got) != hipSuccess))
+    rc = fail(GS_ERR_HIP, "tree combine: out of device memory");
+  if (!rc && got) {
+    g->api->groupStart();
+    r = g->api->recv(v, got, kNcclInt64, peer, g->comm_d, h->stream);
+    if (!r) r = g->api->recv(l, got, kNcclInt64, peer, g->comm_d, h->stream);
+    if (!r) r = g->api->recv(p, got, kNcclUint8, peer, g->comm_d, h->stream);
+    const int e = g->api->groupEnd();
+    if (r || e) rc = rccl_fail(g->api, "ncclRecv", r ? r : e);
+  }
+  if (!rc) {
+    const bool track = h->track;
+    h->track = false;  // a bulk combine is not a structural delta of this rank's own fold
+    rc = gs_combine_exported_device(h, v, l, p, got, (int)hv[1]);
+    h->track = track;
+  }
+  if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(GS_ERR_HIP, "tree combine: sync failed");
+  release();
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_group_tree_combine(gs_group_t g) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  if (!g->api || !g->api->send || !g->api->recv || !g->api->groupStart || !g->api->groupEnd)
+    return fail(GS_ERR_HIP, "RCCL is missing ncclSend/ncclRecv/ncclGroupStart/ncclGroupEnd");
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  if (int rc = join_lanes(h)) return rc;
+  int64_t* hdr = nullptr;  // device {count, failed}
+  GS_HIP(hipMalloc(&hdr, 16));
+  int rc = GS_OK;
+  // binomial tree (SummaryTreeReduce.enhance pairs partitions by f0/2, :107): at level l
+  // rank r with r mod 2^(l+1) == 2^l sends to r - 2^l and leaves the tree
+  for (int step = 1; step < g->nranks && rc == GS_OK; step <<= 1) {
+    const int pos = g->rank % (2 * step);
+    if (pos == step) {
+      rc = tree_send(g, g->rank - step, hdr);
+      break;
+    }
+    if (pos == 0 && g->rank + step < g->nranks) rc = tree_recv(g, g->rank + step, hdr);
+  }
+  (void)hipFree(hdr);
+  return rc;
+}
+
+int gs_group_stats(gs_group_t g, uint64_t* exchanges, uint64_t* records_sent, uint64_t* rows_received) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  uint64_t sent = 0;
+  GS_HIP(hipMemcpyAsync(&sent, h->ctr + gs::ctr_index(gs::CTR_SENT), 8, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  if (exchanges) *exchanges = g->exchanges;
+  if (records_sent) *records_sent = sent;
+  if (rows_received) *rows_received = g->rows_received;
+  return GS_OK;
+}
+
+int gs_group_destroy(gs_group_t g) {
+  if (!g) return GS_OK;
+  if (g->hostprof && g->hp_calls) {
+    const char* nm[4] = {"own fold", "stage+counts", "wait counts", "data+apply"};
+    fprintf(stderr, "[gs_group rank %d] host us per exchange over %llu:", g->rank, (unsigned long long)g->hp_calls);
+    for (int i = 0; i < 4; ++i) fprintf(stderr, " %s %.1f", nm[i], g->hp[i] * 1e6 / (double)g->hp_calls);
+    fprintf(stderr, "; rows received %llu (live %llu); capacity waits %llu, syncs %llu\n",
+            (unsigned long long)g->rows_received, (unsigned long long)g->live_received,
+            (unsigned long long)g->h->cap_waits, (unsigned long long)g->h->cap_syncs);
+  }
+  DeviceGuard dg(g->h->device);
+  (void)hipStreamSynchronize(g->h->stream);
+  if (g->xc) (void)hipStreamSynchronize(g->xc);
+  if (g->xd) (void)hipStreamSynchronize(g->xd);
+  if (g->comm_c && g->api && g->api->commDestroy) g->api->commDestroy(g->comm_c);
+  if (g->comm_d && g->api && g->api->commDestroy) g->api->commDestroy(g->comm_d);
+  if (g->as) {
+    (void)hipStreamSynchronize(g->as);
+    if (g->h->side == g->as) {
+      g->h->side = nullptr;
+      g->h->side_ev = nullptr;
+      g->h->side_dirty = false;
+    }
+    (void)hipStreamDestroy(g->as);
+  }
+  if (g->as_ev) (void)hipEventDestroy(g->as_ev);
+  for (int k = 0; k < 2; ++k) {
+    for (hipEvent_t e : {g->staged[k], g->counted[k], g->gathered[k], g->applied[k]})
+      if (e) (void)hipEventDestroy(e);
+    (void)hipFree(g->send[k]);
+    (void)hipFree(g->recv[k]);
+  }
+  (void)hipFree(g->cnt);
+  if (g->xc) (void)hipStreamDestroy(g->xc);
+  if (g->xd) (void)hipStreamDestroy(g->xd);
+  if (g->hdr_host) (void)hipHostFree(g->hdr_host);
+  delete g;
+  return GS_OK;
+}
+
+}  // extern "C"

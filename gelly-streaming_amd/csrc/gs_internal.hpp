@@ -1,0 +1,199 @@
+// gs_internal.hpp -- the summary handle and the internal entry points shared by
+// gs_capi.cpp (include/gs_summary.h), gs_group.cpp (include/gs_group.h) and
+// gs_changes.cpp (per-window change emission).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "gs_ingest.hpp"
+#include "gs_kernels.hpp"
+#include "gs_summary.h"
+
+namespace gsi {
+
+int fail(int code, const std::string& msg);
+
+#define GS_HIP(call)                                                                                  \
+  do {                                                                                                \
+    hipError_t e_ = (call);                                                                           \
+    if (e_ != hipSuccess)                                                                             \
+      return ::gsi::fail(GS_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));              \
+  } while (0)
+
+constexpr uint32_t kMaxChunk = 1u << 22;     // edges per k_fold launch
+constexpr uint32_t kStageChunk = 1u << 20;   // edges per pinned staging buffer
+constexpr double kMaxLoad = 0.70;            // grow the table past this load factor
+constexpr uint64_t kMaxCap = 1ull << 30;     // link holds slot << 1 in 32 bits
+
+enum { KID_FOLD = 0, KID_STAGE = 1, KID_EXPORT = 2, KID_INIT = 3, KID_N = 4 };
+
+// per-shard edges of one k_fold launch of c edges (blocks are dealt to the 64
+// shards round-robin from a rotating first shard)
+inline uint64_t per_shard_edges(uint64_t c) {
+  const uint64_t blocks = (c + gs::kFoldBS - 1) / gs::kFoldBS;
+  return ((blocks + gs::kShards - 1) / gs::kShards) * gs::kFoldBS;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace gsi
+
+struct gs_summary {
+  int device = 0;
+  int kind = GS_KIND_CC;
+  hipStream_t stream = nullptr;
+  // table + vertex list
+  gs::Slot* tab = nullptr;  // [cap + 1]: hashed slots + the reserved slot of INT64_MIN
+  uint64_t cap = 0;
+  int logcap = 0;
+  uint32_t* ctr = nullptr;
+  uint32_t* vlist = nullptr;  // [kShards][vshard_cap]
+  uint32_t vshard_cap = 0;
+  uint32_t shard0 = 0;        // first shard of the next fold launch (rotates)
+  bool vlist_ok = true;       // false once a shard of the vertex list overflowed (until reset)
+  uint32_t* h_flags = nullptr;  // pinned: error / overflow flags
+  // capacity tracking: a host upper bound of the vertex count, refreshed without
+  // host synchronisation from k_report words (ring in host-coherent memory)
+  uint64_t nv_ub = 0;
+  uint64_t cap_waits = 0, cap_syncs = 0;  // capacity checks that waited for reports / joined every stream
+  double cap_wait_s = 0;                  // host seconds spent in those waits
+  static constexpr int kRepRing = 16;
+  unsigned long long* rep = nullptr;      // host pointer
+  unsigned long long* rep_dev = nullptr;  // its device mapping
+  uint64_t rep_seq = 0;
+  uint64_t rep_epoch = 0;  // resets since create: tags reports (k_report) so late ones are ignored
+  static constexpr int kRepEvery = 4;    // each stream reports every 4th capacity-checked chunk
+  static constexpr int kRepStreams = 6;  // handle stream, 4 lanes, side stream
+  int rep_skip[kRepStreams] = {};
+  uint64_t rep_pending[kRepStreams] = {};  // per stream: edges of chunks queued since its last report
+  uint64_t rep_pending_edges = 0;          // their sum
+  uint64_t e_launched = 0;  // edges of capacity-checked folds since reset / rebuild
+  uint64_t e_lost = 0;      // launched edges no report will ever claim (complete: dropped at a sync)
+  uint64_t nv_exact = 0, e_exact = 0;  // an exact count and the edges complete when it was read
+  // delta records (multi-GPU exchange, change emission)
+  bool track = false;
+  int64_t* drec = nullptr;  // [kShards][delta_shard_cap][3]
+  uint32_t delta_shard_cap = 0;
+  uint64_t delta_edges = 0;  // fold edges the delta list holds between two stages
+  uint64_t delta_fill_ub = 0;  // worst-case per-shard fill since the last stage
+  // change tracking (gs_changes.cpp)
+  bool changes = false;
+  uint32_t* nxt = nullptr;  // [cap + 1] circular member lists
+  unsigned long long* chg_scratch = nullptr;  // emission scratch: staged records, counters
+  uint64_t chg_scratch_rows = 0;
+  // staging for host folds
+  int64_t* d_stage = nullptr;  // [2][2][kStageChunk]
+  uint8_t* d_wstage = nullptr; // [2][kStageChunk]
+  int64_t* h_stage = nullptr;  // pinned, same shape
+  uint8_t* h_wstage = nullptr;
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  int stage_next = 0;
+  int64_t* d_scratch = nullptr;  // small scratch (find_one)
+  // combine export scratch (gs_combine source side): reused across calls
+  int64_t* x_v = nullptr;
+  int64_t* x_l = nullptr;
+  uint8_t* x_p = nullptr;
+  uint64_t x_cap = 0;
+  unsigned long long* x_cnt = nullptr;  // device: exported rows (u64) + failure flag (u32 at word 1)
+  hipEvent_t x_ready = nullptr, x_used = nullptr;
+  bool x_pending = false;  // x_used recorded by a consumer not yet waited for
+  // text ingest (gs_fold_text): pinned + device text chunks, parsed edges, scratch
+  char* h_text = nullptr;
+  uint64_t* h_tres = nullptr;
+  hipEvent_t text_ev[2] = {nullptr, nullptr};
+  char* d_text = nullptr;
+  int64_t* d_tsrc = nullptr;
+  int64_t* d_tdst = nullptr;
+  void* d_tscratch = nullptr;
+  gs::ParseScratch tscratch;
+  // pipelined folds (gs_set_pipelining): consecutive plain device folds alternate
+  // over lane streams so that fold b+1 may start while fold b drains; every other
+  // entry point joins the lanes onto `stream` first (join_lanes)
+  int pipe_depth = 1;
+  static constexpr int kLanes = 4;
+  hipStream_t lane[kLanes] = {};
+  hipEvent_t lane_ev[kLanes] = {};
+  hipEvent_t main_ev = nullptr;
+  int lane_next = 0;
+  bool lanes_dirty = false;
+  // side stream (a multi-GPU group's apply stream): folds of remote rows run there,
+  // overlapping this rank's own folds; every reader joins it (join_lanes), the
+  // handle's own folds do not (union commutes)
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev = nullptr;
+  bool side_dirty = false;
+  // profiling
+  bool profiling = false;
+  struct Pending {
+    int kid;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> prof_pending;
+  std::vector<hipEvent_t> ev_pool;
+  uint64_t launches[gsi::KID_N] = {0, 0, 0, 0};
+  double total_ms[gsi::KID_N] = {0, 0, 0, 0};
+
+  gs::Table table() const {
+    gs::Table t;
+    t.tab = tab;
+    t.ctr = ctr;
+    t.cap = (uint32_t)cap;
+    t.mask = (uint32_t)(cap - 1);
+    t.shift = 64 - logcap;
+    t.r0 = (uint32_t)cap;
+    t.vlist = vlist;
+    t.vshard_cap = vshard_cap;
+    t.mark_new = changes ? 1 : 0;
+    return t;
+  }
+  gs::Delta delta() const {
+    gs::Delta D;
+    D.drec = drec;
+    D.shard_cap = delta_shard_cap;
+    return D;
+  }
+};
+
+namespace gsi {
+
+// Where a fold's rows come from (defaults: plain edge arrays on the handle stream).
+struct FoldSource {
+  uint32_t rows = 0;  // > 0: gathered exchange buffer, world blocks of `rows` rows
+  int skip_rank = -1;
+  const unsigned long long* counts = nullptr;  // device: live rows per block (| kFailBit)
+  uint64_t units = 0;  // exchange layout: rows that may add vertices (capacity charge)
+  const unsigned long long* n_dev = nullptr;   // device element count (<= n)
+  const uint32_t* fail_in = nullptr;           // device failure flag of a combined summary
+  bool on_side = false;  // launch on h->side (a group's apply stream) instead of h->stream
+  bool allow_pipe = false;
+};
+
+int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
+                     size_t stride, size_t w_stride, bool track, bool check_cap = true,
+                     const FoldSource& fs = FoldSource());
+int join_lanes(gs_summary* h);
+bool side_ok(const gs_summary* h);
+int read_nv(gs_summary* h, uint64_t* nv);
+int check_device_flags(gs_summary* h);
+int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n, int part = 0,
+                       int nparts = 1);
+// stage every pending delta record into out (first cap rows, `width` int64 each) and
+// the count word into *count_out (device); the delta list is emptied
+int stage_delta(gs_summary* h, int64_t* out, uint64_t cap, int width, unsigned long long* count_out, bool with_fail,
+                hipStream_t st = nullptr);
+int ensure_delta_list(gs_summary* h, uint64_t edges);
+bool use_vertex_list(gs_summary* h, uint64_t nv_bound);
+int change_tracking_reset(gs_summary* h, bool full);  // gs_changes.cpp: after reset / rebuild
+
+}  // namespace gsi

@@ -1,20 +1,18 @@
 /*
  * gs_group.h -- native multi-GPU combine for the summary of include/gs_summary.h.
  *
- * One process (or thread) per GPU; each rank holds a replica of the global
- * summary and folds its own shard of every global micro-batch. After its fold a
- * rank stages its structural delta (gs_delta_stage), the ranks all-gather the
- * staged records over RCCL (xGMI) on the summary's own HIP stream, and every rank
- * folds the other ranks' records (gs_fold_exchange_device) -- all queued on one
- * stream, no host synchronisation per batch. This replaces the reference's gather
- * of per-partition summaries into one parallelism-1 reducer
+ * One process (or thread) per GPU; each rank holds a REPLICA of the global summary
+ * and folds its own shard of every global micro-batch. After its fold a rank
+ * stages its structural delta (at most one record per folded edge), the ranks
+ * all-gather the record COUNTS, then exactly max-count rows per rank over RCCL
+ * (xGMI), and every rank folds the other ranks' live records on a side stream
+ * that overlaps its next own fold -- no host synchronisation per batch beyond
+ * reading the gathered counts from host-mapped memory. This replaces the
+ * reference's gather of per-partition summaries into one parallelism-1 reducer
  * (SummaryBulkAggregation.java:77-83) and its Merger (SummaryAggregation.java:107-119):
- * after gs_group_finish every replica equals the union of all ranks' folds.
- *
- * The per-batch collective size is agreed without communication: it starts at
- * `first_cap` records and every `retune` batches is re-derived from gathered
- * headers all ranks hold identically; records past it stay queued on the device
- * and ride with the next exchange. RCCL (librccl.so.1) is loaded on first use.
+ * after gs_group_finish every replica equals the union of all ranks' folds, and a
+ * signed replica's verdict is the AND of every rank's (the count word carries it).
+ * RCCL (librccl.so.1) is loaded on first use.
  */
 #ifndef GS_GROUP_H
 #define GS_GROUP_H
@@ -30,29 +28,25 @@ extern "C" {
 
 typedef struct gs_group* gs_group_t;
 
-#define GS_GROUP_ID_BYTES 128
+#define GS_GROUP_ID_BYTES 256 /* two RCCL unique ids: count and data communicators */
 
-/* Create the communicator id on one rank and hand its 128 bytes to every rank
- * (any host channel: MPI, TCP, torch.distributed, a file). */
+/* Create the communicator id on one rank and hand its GS_GROUP_ID_BYTES bytes to
+ * every rank (any host channel: MPI, TCP, torch.distributed, a file). */
 int gs_group_unique_id(void* id);
 
 /* Join the group as `rank` of `nranks` and bind it to summary `h` (its device and
- * stream). `batch_edges` = maximum edges one gs_group_fold_device call folds;
- * `first_cap` = records per rank in the first exchanges (0: batch_edges). Turns
- * delta tracking on. batch_edges == 0 creates a tree-combine-only group (no
- * exchange buffers, tracking untouched: fold partials with gs_fold[_device], then
- * gs_group_tree_combine). Collective: every rank must call it.
- * Sizing: the summary's host-side capacity bound charges 2 vertices per record row
- * of every gathered exchange still in flight ((nranks - 1) x cap rows each), so give
- * the summary headroom above the final vertex count (bench.py: 2x the vertex hint at
- * 2^22-edge batches, 8 ranks), or a fold waits for the GPU to drain. */
-int gs_group_create(gs_group_t* g, gs_handle h, const void* id, int nranks, int rank, size_t batch_edges,
-                    size_t first_cap);
+ * stream). `batch_edges` = maximum edges one gs_group_fold_device call folds (at
+ * most 2^26; sizes the delta list and the exchange buffers). Turns delta tracking
+ * on. batch_edges == 0 creates a tree-combine-only group (no exchange buffers,
+ * tracking untouched: fold partials with gs_fold[_device], then
+ * gs_group_tree_combine). Collective: every rank must call it. */
+int gs_group_create(gs_group_t* g, gs_handle h, const void* id, int nranks, int rank, size_t batch_edges);
 
 /* One global micro-batch on this rank: fold n DEVICE edges (as gs_fold_device,
- * stride 1), exchange the delta, fold the other ranks' records. Asynchronous.
- * Collective: every rank calls it the same number of times (n may differ,
- * including 0). */
+ * stride 1; n <= batch_edges), stage the delta and all-gather its count, then
+ * move and fold the PREVIOUS micro-batch's records (whose counts landed while this
+ * fold was queued). Asynchronous. Collective: every rank calls it the same number
+ * of times (n may differ, including 0). */
 int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n);
 
 /* ceil(n / batch) consecutive gs_group_fold_device calls over src[0..n) in
@@ -60,8 +54,8 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
  * Collective: every rank must issue the same number of micro-batches. */
 int gs_group_fold_batches_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n, size_t batch);
 
-/* Drain every rank's queued records (synchronous rounds) and synchronise; then all
- * replicas are identical. Collective. */
+/* Move and fold the last micro-batch's records and synchronise; then all replicas
+ * are identical. Collective. */
 int gs_group_finish(gs_group_t g);
 
 /* Log-depth tree combine of PER-RANK PARTIAL summaries: the reference's
@@ -77,9 +71,9 @@ int gs_group_finish(gs_group_t g);
  * equal by delta exchange) this is the bulk path: O(V) per level. */
 int gs_group_tree_combine(gs_group_t g);
 
-/* Exchange statistics: exchanges run, records this rank has sent, the current
- * per-rank capacity of one exchange (synchronises the stream). */
-int gs_group_stats(gs_group_t g, uint64_t* exchanges, uint64_t* records_sent, uint64_t* current_cap);
+/* Exchange statistics: exchanges run, records this rank has staged, rows this rank
+ * has received (max-count rows from each other rank per exchange; synchronises). */
+int gs_group_stats(gs_group_t g, uint64_t* exchanges, uint64_t* records_sent, uint64_t* rows_received);
 
 int gs_group_destroy(gs_group_t g);
 

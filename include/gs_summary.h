@@ -62,7 +62,10 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint);
 int gs_destroy(gs_handle h);
 
 /* Reset to the initial value (empty forest, verdict true). Replaces
- * `summary = initialVal` of a transient Merger (SummaryAggregation.java:113-115). */
+ * `summary = initialVal` of a transient Merger (SummaryAggregation.java:113-115)
+ * and Flink's per-window copy of the initial value (a pooled handle is reset
+ * instead of created). Asynchronous; O(vertices) on a sparse table
+ * (only the touched slots are re-initialised). */
 int gs_reset(gs_handle h);
 
 /* Fold n edges from HOST memory: for each i, union(src[i], dst[i]).
@@ -90,13 +93,17 @@ int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const ui
  * the handle (reads, exports, combine, serialize, sync, gs_get_stream) first orders
  * the handle's stream behind all pending folds. Device buffers passed to a
  * pipelined fold must stay valid until that next call. Applies to plain folds
- * (no delta tracking, hot level off, profiling off); depth 1 (default) = in order. */
+ * (no delta or change tracking, profiling off); depth 1 (default) = in order. */
 int gs_set_pipelining(gs_handle h, int depth);
 
 /* Merge summary `src` into `dst` (either may be on any device; `src` is unchanged).
  * Replaces CombineCC.reduce -> DisjointSet.merge (ConnectedComponents.java:116-126,
  * DisjointSet.java:127-131) and combineFunction.reduce -> Candidates.merge
- * (BipartitenessCheck.java:128-130, Candidates.java:77-139); the verdict is the AND. */
+ * (BipartitenessCheck.java:128-130, Candidates.java:77-139); the verdict is the AND.
+ * Asynchronous: src is exported on its stream (over its vertex list when sparse:
+ * O(vertices of src), not O(table)), dst folds the rows behind an event; the row
+ * count and verdict are read on the device. No host synchronisation and, once the
+ * reusable scratch is sized, no allocation. */
 int gs_combine(gs_handle dst, gs_handle src);
 
 /* Receiving half of a combine from EXPORTED arrays (gs_export_labels_device of
@@ -117,6 +124,11 @@ int gs_num_vertices(gs_handle h, uint64_t* n);
 /* Canonical label of one vertex: *label = min id of its component; *found = 0 if
  * the vertex was never seen (DisjointSet.find returns null, :66-69). */
 int gs_find(gs_handle h, int64_t v, int64_t* label, int* found);
+
+/* Batched find over DEVICE arrays: label[i] = canonical label of v[i]; found[i]
+ * (optional, may be NULL) = 0 for an id never seen (label[i] is then v[i]).
+ * Asynchronous on the handle's stream (DisjointSet.find, :66-80, for many ids). */
+int gs_find_labels_device(gs_handle h, const int64_t* v, size_t n, int64_t* label, uint8_t* found);
 
 /* Export every (vertex, canonical label) pair to HOST arrays of capacity `cap`,
  * unordered. *n = number of vertices (GS_ERR_TRUNCATED if cap < *n; nothing
@@ -157,43 +169,54 @@ int gs_deserialize(gs_handle h, const void* buf, size_t len);
  * While tracking is on, every fold records the structural changes it made:
  * each successful hook as (root, new parent, parity) and each new vertex seen
  * only through a self-loop as (v, v, 0) (every other new vertex is named by a
- * hook record). Folding another
- * replica's delta into this summary reproduces that replica's changes (union is
- * associative and commutative), which replaces shipping whole summaries to one
- * reducer (SummaryBulkAggregation.java:77-83).
+ * hook record): at most one record per folded edge. Folding another replica's
+ * delta into this summary reproduces that replica's changes (union is associative
+ * and commutative), which replaces shipping whole summaries to one reducer
+ * (SummaryBulkAggregation.java:77-83).
  *
- * Wire format: int64 records {a, b, w}, 24 bytes each; w bit 0 = parity,
- * w bit 7 = skip (padding). gs_take_delta_records packs the delta accumulated
- * since the previous take into DEVICE records (first `cap`) and writes the total
- * record count to the DEVICE word *count; both complete on the handle's stream
- * (no host synchronisation). gs_fold_records_device folds such records
- * (track = 0: apply another replica's delta without re-recording it).
+ * The delta list holds the records of gs_delta_capacity() rows (the folds of at
+ * least 2^22 edges, more after gs_group_create with a larger batch) between two
+ * takes/stages; a tracked fold past that fails with GS_ERR_CAPACITY.
  *
- * gs_delta_stage is the exchange form: it fills a send buffer of cap + 1
- * records -- row 0 = header {sent, queued, skip}, rows 1..sent = records (rows
- * past `sent` are left untouched) -- and keeps the records past `cap` queued for
- * the next stage, so every rank can all-gather (cap + 1) rows with a capacity
- * agreed in advance, without a host synchronisation. gs_fold_exchange_device
- * folds a gathered buffer of world x rows such records (each rank's header says
- * how many of its rows are live), skipping rank `skip_rank` (the caller's own). */
+ * gs_take_delta_records packs the delta accumulated since the previous take into
+ * DEVICE records {a, b, w} (24 bytes; w bit 0 = parity, w bit 7 = skip), first
+ * `cap` of them, and writes the total record count to the DEVICE word *count; both
+ * complete on the handle's stream (no host synchronisation). gs_fold_records_device
+ * folds such records (track = 0: apply another replica's delta without
+ * re-recording it).
+ *
+ * gs_delta_stage is the exchange form: every pending record into `send` as rows of
+ * `width` int64 ({a, b} for CC, {a, b, w} for the signed kind; cap must be at least
+ * gs_delta_capacity), and the DEVICE count word *count = rows | 2^62 when the
+ * signed verdict has failed (the exchange carries the verdict: Candidates.merge
+ * :79-81). gs_fold_exchange_device folds a gathered buffer: `world` blocks of
+ * `rows` rows of `width` int64, block r live for its first counts[r] rows (DEVICE
+ * count words as staged, failure bits ORed into the verdict), skipping block
+ * `skip_rank` (the caller's own). */
 int gs_set_delta_tracking(gs_handle h, int on);
+int gs_delta_capacity(gs_handle h, uint64_t* rows);
 int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count);
-int gs_delta_stage(gs_handle h, int64_t* send, size_t cap);
+int gs_delta_stage(gs_handle h, int64_t* send, size_t cap, int width, uint64_t* count);
 int gs_fold_records_device(gs_handle h, const int64_t* rec, size_t n, int track);
-int gs_fold_exchange_device(gs_handle h, const int64_t* recv, size_t world, size_t rows, int skip_rank);
+int gs_fold_exchange_device(gs_handle h, const int64_t* recv, const uint64_t* counts, size_t world, size_t rows,
+                            int width, int skip_rank);
 
 /* ---- introspection -----------------------------------------------------------
  * The HIP stream (hipStream_t) the handle enqueues on, and per-kernel timing:
- * when profiling is on, every launch is bracketed by HIP events on that stream;
- * gs_kernel_stats returns (launches, total milliseconds) for kernel `id`
- * (0 = fold/find, 1 = hook, 2 = export, 3 = init). */
+ * when profiling is on, every launch is bracketed by HIP events on the stream it
+ * runs on; gs_kernel_stats returns (launches, total milliseconds) for kernel `id`
+ * (0 = fold, 1 = stage, 2 = export, 3 = init/reset). gs_capacity_stats: capacity
+ * checks that had to wait for in-flight reports, those that synchronised, and the
+ * host milliseconds spent waiting. */
 int gs_get_stream(gs_handle h, void** stream);
 int gs_set_profiling(gs_handle h, int on);
 int gs_kernel_stats(gs_handle h, int id, uint64_t* launches, double* total_ms);
 int gs_table_capacity(gs_handle h, uint64_t* slots);
+int gs_capacity_stats(gs_handle h, uint64_t* waits, uint64_t* syncs, double* wait_ms);
 
 /* Device counters (synchronises): out[0] vertices, [1] bipartiteness failed,
- * [2] table-overflow error, [3] list overflow, [4] records sent by exchanges,
+ * [2] table-overflow error, [3] list overflow (bit 0 delta list, bit 1 vertex
+ * list), [4] records staged,
  * [5] hook calls, [6] hook-loop iterations, [7] failed hook CASes -- [5..7] only
  * count in the debug build (make -C gelly-streaming_amd debug). */
 int gs_counters(gs_handle h, uint64_t* out8);

@@ -4,9 +4,10 @@ micro-batch and exchanges its structural delta; afterwards every rank's replica
 must equal the whole stream folded by the oracle (bit-exact canonical labels).
 
 The device summary is replaced by `ModelReplica`, a CPU model of the C-ABI delta
-contract (include/gs_summary.h: gs_set_delta_tracking / gs_delta_stage /
-gs_fold_exchange_device):
-new vertices as (v, v, 0), successful hooks as (root, new parent, parity)."""
+contract (include/gs_summary.h: gs_set_delta_tracking / gs_delta_capacity /
+gs_delta_stage / gs_fold_exchange_device): self-loop-only new vertices as
+(v, v, 0), successful hooks as (root, new parent, parity); the stage writes every
+record and a count word, the exchange fold reads block r's first counts[r] rows."""
 import os
 import socket
 
@@ -22,10 +23,11 @@ class ModelReplica:
     device replica: records are hooks (root, new parent, 0) and self-loop-only
     new vertices (v, v, 0))."""
 
-    def __init__(self):
+    def __init__(self, capacity):
         self.parent = {}
         self.track = False
         self.delta = []
+        self.capacity = capacity  # records one batch can produce (<= 1 per edge)
 
     def _find(self, v):
         while self.parent[v] != v:
@@ -58,31 +60,26 @@ class ModelReplica:
     def set_delta_tracking(self, on=True):
         self.track = bool(on)
         self.delta = []
-        self.queue = []
 
-    def _pack(self):
-        self.queue += self.delta
+    def delta_capacity(self):
+        return self.capacity
+
+    def delta_stage(self, send, cap, count, width=3):
+        """gs_delta_stage: every record into rows 0.., the count into `count`."""
+        assert cap >= self.capacity and len(self.delta) <= cap
+        if self.delta:
+            send[:len(self.delta), :3] = torch.tensor(self.delta, dtype=torch.int64)
+        count.fill_(len(self.delta))
         self.delta = []
 
-    def delta_stage(self, send, cap):
-        """gs_delta_stage: header {sent, queued, skip}, then up to cap records."""
-        self._pack()
-        total = len(self.queue)
-        sent = min(total, cap)
-        send[0] = torch.tensor([sent, total, 0x80])
-        if sent:
-            send[1:sent + 1] = torch.tensor(self.queue[:sent], dtype=torch.int64)
-        self.queue = self.queue[sent:]
-
-    def fold_exchange(self, recv, world, rows, skip_rank):
+    def fold_exchange(self, recv, counts, world, rows, skip_rank, width=3):
         saved = self.track
         self.track = False
         for r in range(world):
             if r == skip_rank:
                 continue
-            block = recv[r * rows:(r + 1) * rows]
-            live = int(block[0, 0])
-            rec = block[1:live + 1]
+            live = int(counts[r]) & ((1 << 62) - 1)
+            rec = recv[r * rows:r * rows + live]
             rec = rec[(rec[:, 2] & 0x80) == 0]
             self.fold_device(rec[:, 0], rec[:, 1], n=len(rec))
         self.track = saved
@@ -101,7 +98,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, src, dst, batch, retune, out):
+def _worker(rank, world, port, src, dst, batch, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -110,8 +107,8 @@ def _worker(rank, world, port, src, dst, batch, retune, out):
     import gsamd  # noqa: F401  (registers gelly_streaming_amd)
     from gelly_streaming_amd.distributed import DeltaExchangeFold
 
-    rep = ModelReplica()
-    x = DeltaExchangeFold(rep, batch, torch.device("cpu"), first_cap=max(1, batch // 16), retune=retune)
+    rep = ModelReplica(batch)
+    x = DeltaExchangeFold(rep, batch, torch.device("cpu"))
     s = torch.from_numpy(src)
     d = torch.from_numpy(dst)
     g = batch * world
@@ -121,23 +118,20 @@ def _worker(rank, world, port, src, dst, batch, retune, out):
         x.step(s[lo:], d[lo:], n)
     x.finish()
     v, lab = rep.labels()
-    out[rank] = (v.tolist(), lab.tolist(), x.rows_received, list(x.cap_history))
+    out[rank] = (v.tolist(), lab.tolist(), x.rows_received, x.live_received)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,retune", [(2, 4), (3, 4), (2, 2), (3, 1)])
-def test_delta_exchange_gloo(oracle_mod, world, retune):
+@pytest.mark.parametrize("world,batch", [(2, 256), (3, 256), (2, 100), (3, 1000)])
+def test_delta_exchange_gloo(oracle_mod, world, batch):
     src, dst = oracle_mod.rmat_edges(0x5EED0026, 12, 0, 1 << 13, True)
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), src, dst, 256, retune, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), src, dst, batch, out), nprocs=world, join=True)
     ov, olab = oracle_mod.cc_labels(src, dst)
     for r in range(world):
-        v, lab, exchanged, caps = out[r]
+        v, lab, rows, live = out[r]
         assert v == ov.tolist(), "rank %d vertex set" % r
         assert lab == olab.tolist(), "rank %d labels" % r
-        assert exchanged > 0
-        # the capacity is re-derived from lagged headers (every 4 exchanges from the 4th)
-        assert caps[0] == 16 and caps[4] != 16, caps[:8]
-        assert caps == out[0][3], "ranks must agree on every exchange size"
+        assert 0 < live <= rows  # only max-count rows per rank move: padding <= rows - live

@@ -37,7 +37,7 @@ def _worker(rank, world, port, scale, nedges, batch, out):
     dst = torch.empty(nedges, dtype=torch.int64, device=dev)
     gs.gen_rmat(src, dst, 0, nedges, scale, 0x5EED0026, True)
     torch.cuda.synchronize()
-    x = DeltaExchangeFold(summ, batch, dev, first_cap=batch // 64, retune=4)
+    x = DeltaExchangeFold(summ, batch, dev)
     g = batch * world
     for o in range(0, nedges, g):
         lo = o + rank * batch

@@ -1,5 +1,5 @@
 """GPU: the native RCCL group (include/gs_group.h) at one rank: fold + stage +
-ncclAllGather + header-driven capacity + backlog drain, on the summary's stream.
+count all-gather + live-row data all-gather + side-stream apply.
 (Several ranks need several GPUs: RCCL refuses two ranks on one device; the
 multi-rank protocol itself is covered by test_gpu_distributed.py / the gloo tests.)"""
 import numpy as np
@@ -8,34 +8,29 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("first_cap,self_apply,lanes,knobs", [
-    (0, 0, "0", {}), (64, 0, "0", {}), (64, 1, "0", {}), (0, 0, "1", {}), (64, 1, "1", {}),
-    (64, 1, "1", {"GS_GROUP_XS_PRIO": "1"}), (64, 1, "0", {"GS_GROUP_LAG": "1"}),
-    (64, 0, "1", {"GS_GROUP_LAG": "7"})])
-def test_group_single_rank_matches_oracle(gs, oracle_mod, monkeypatch, first_cap, self_apply, lanes, knobs):
+@pytest.mark.parametrize("self_apply,batch", [(0, 1 << 13), (1, 1 << 13), (1, 1 << 12)])
+def test_group_single_rank_matches_oracle(gs, oracle_mod, monkeypatch, self_apply, batch):
     """self_apply: the rank also folds its own gathered rows (16-B CC rows, exchange
-    layout, lagged apply) -- the remote-fold path, exercised at one rank; folding a
-    delta twice is idempotent, so any mis-parsed row would show in the labels."""
+    layout from the gathered count words, applied one exchange late on the side
+    stream) -- the remote-fold path, exercised at one rank; folding a delta twice is
+    idempotent, so any mis-parsed row would show in the labels."""
     import torch
-    monkeypatch.setenv("GS_GROUP_RETUNE", "2")
     monkeypatch.setenv("GS_GROUP_SELF_APPLY", str(self_apply))
-    monkeypatch.setenv("GS_GROUP_LANES", lanes)
-    for k, v in knobs.items():  # opt-in knobs: stream priority, retune header lag
-        monkeypatch.setenv(k, v)
-    n, B = 1 << 17, 1 << 13
+    n, B = 1 << 17, batch
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")
     gs.gen_rmat(src, dst, 0, n, 15, 0x5EED0026, True)
     torch.cuda.synchronize()
     with gs.Summary("cc", capacity_hint=1 << 15) as s:
-        g = gs.Group(s, gs.group_unique_id(), 1, 0, B, first_cap)
+        g = gs.Group(s, gs.group_unique_id(), 1, 0, B)
         for i in range(0, n, B):
             g.fold_device(src[i:], dst[i:], B)
-        # the per-exchange capacity was re-derived from the lagged headers
-        assert g.stats()["cap"] != (first_cap or B)
+        with pytest.raises(gs.GSError):  # n above batch_edges is refused up front
+            g.fold_device(src, dst, B + 1)
         g.finish()
         st = g.stats()
-        assert st["exchanges"] >= n // B
+        assert st["exchanges"] == n // B
+        assert 0 < st["records_sent"] <= n
         v, lab = s.labels()
         g.close()
     ov, olab = oracle_mod.cc_labels(src.cpu().numpy(), dst.cpu().numpy())
@@ -68,7 +63,6 @@ def test_group_signed_rows_self_apply(gs, oracle_mod, monkeypatch, inject):
     gathered rows back (GS_GROUP_SELF_APPLY) -- verdict and colouring must equal
     the truth."""
     import torch
-    monkeypatch.setenv("GS_GROUP_RETUNE", "2")
     monkeypatch.setenv("GS_GROUP_SELF_APPLY", "1")
     n, B = 1 << 16, 1 << 12
     src = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -76,7 +70,7 @@ def test_group_signed_rows_self_apply(gs, oracle_mod, monkeypatch, inject):
     gs.gen_bip(src, dst, 0, n, 12, 0x5EED0B1B, inject=inject)
     torch.cuda.synchronize()
     with gs.Summary("signed", capacity_hint=1 << 13) as s:
-        g = gs.Group(s, gs.group_unique_id(), 1, 0, B, 256)
+        g = gs.Group(s, gs.group_unique_id(), 1, 0, B)
         for i in range(0, n, B):
             g.fold_device(src[i:], dst[i:], B)
         g.finish()

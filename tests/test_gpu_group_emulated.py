@@ -2,10 +2,10 @@
 RCCL refuses two ranks on one device, so the group's communicator is replaced by
 the library's in-process emulation (GS_GROUP_FAKE_COMM=1: host barriers + device
 copies ordered by events) and every rank is a thread of this process driving its
-own summary. Everything else -- staging, 16-/24-byte rows, the exchange-layout
-fold of real remote rows on the side stream, header-driven retune, backlog drain,
-partitioned label pass, the binomial tree combine -- is the code bench.py runs at
-N GPUs. Every replica (or rank 0 of the tree) must equal the oracle."""
+own summary. Everything else -- staging, 16-/24-byte rows, count and data
+collectives, the exchange-layout fold of real remote rows on the side stream, the
+partitioned label pass, the binomial tree combine -- is the code bench.py runs at N
+GPUs. Every replica (or rank 0 of the tree) must equal the oracle."""
 import threading
 
 import numpy as np
@@ -33,16 +33,11 @@ def _run_ranks(world, body):
     return out
 
 
-@pytest.mark.parametrize("lanes", ["0", "1"])
-@pytest.mark.parametrize("world,first_cap,retune", [(2, 0, "4"), (3, 256, "2"), (4, 64, "1")])
-def test_delta_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, world, first_cap, retune, lanes):
-    """lanes=1: each rank's own tracked folds alternate over two lane streams and two
-    delta sets (GS_GROUP_LANES), the stage of exchange b on fold b's lane."""
+@pytest.mark.parametrize("world,batch", [(2, 1 << 12), (3, 1 << 11), (4, 1 << 12)])
+def test_delta_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, world, batch):
     import torch
     monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
-    monkeypatch.setenv("GS_GROUP_LANES", lanes)
-    monkeypatch.setenv("GS_GROUP_RETUNE", retune)
-    scale, n, B = 14, 1 << 18, 1 << 12
+    scale, n, B = 14, 1 << 18, batch
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")
     gs.gen_rmat(src, dst, 0, n, scale, 0x5EED0026, True)
@@ -52,7 +47,7 @@ def test_delta_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, world, first
 
     def rank(r):
         with gs.Summary("cc", capacity_hint=1 << 10) as s:  # small hint: growth during the exchange
-            g = gs.Group(s, uid, world, r, B, first_cap)
+            g = gs.Group(s, uid, world, r, B)
             g.fold_batches(src[r * per:], dst[r * per:], per, B)
             g.finish()
             st = g.stats()
@@ -68,9 +63,13 @@ def test_delta_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, world, first
 
     res = _run_ranks(world, rank)
     ov, olab = oracle_mod.cc_labels(src.cpu().numpy(), dst.cpu().numpy())
+    sent = sum(res[r][2]["records_sent"] for r in range(world))
     for r, (v, lab, st, _) in enumerate(res):
         assert np.array_equal(v, ov) and np.array_equal(lab, olab), "rank %d replica" % r
-        assert st["exchanges"] >= per // B
+        assert st["exchanges"] == (per + B - 1) // B
+        # live rows only: every rank receives at most max-count rows per peer per exchange
+        assert st["rows_received"] <= (world - 1) * per
+    assert sent <= n
     parts = sorted(p for r in range(world) for p in res[r][3])
     assert parts == sorted(zip(ov.tolist(), olab.tolist()))
 
@@ -78,11 +77,11 @@ def test_delta_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, world, first
 _BENCH_SHAPE = {}
 
 
-@pytest.mark.parametrize("world,log_batch", [(2, 22), (4, 21)])
+@pytest.mark.parametrize("world,log_batch", [(2, 20), (4, 20), (2, 22)])
 def test_bench_exchange_shape_emulated_ranks(gs, oracle_mod, monkeypatch, world, log_batch):
-    """bench.py's N-GPU defaults at reduced scale: RMAT-20 (2^24 edges), 2^21-2^22-edge
-    exchanges per rank, a capacity hint of twice the vertex scale, the default first
-    capacity and knobs. Every replica equals the oracle."""
+    """bench.py's N-GPU shape at reduced scale: RMAT-20 (2^24 edges), 2^20-edge
+    per-rank micro-batches and 2^22, a capacity hint of twice
+    the vertex scale. Every replica equals the oracle."""
     import torch
     monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
     scale, n, B = 20, 1 << 24, 1 << log_batch
@@ -111,14 +110,18 @@ def test_bench_exchange_shape_emulated_ranks(gs, oracle_mod, monkeypatch, world,
         assert st["exchanges"] >= per // B
 
 
-@pytest.mark.parametrize("lanes", ["0", "1"])
-@pytest.mark.parametrize("inject", [(), (1 << 15,)])
-def test_signed_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, inject, lanes):
+@pytest.mark.parametrize("inject", [(), (1 << 15,), (5 << 12,), (2 << 15) + 777])
+def test_signed_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, inject):
+    """inject (1 << 15) is the first edge of rank 1's shard (its endpoints are new
+    there, so it travels as a hook record); (5 << 12) and (2 << 15) + 777 sit in the
+    MIDDLE of a shard, where the injected same-side edge joins vertices that rank
+    already connected: the odd cycle is found without any record, and only the count
+    word's failure bit tells the other replicas."""
     import torch
     monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
-    monkeypatch.setenv("GS_GROUP_LANES", lanes)
-    monkeypatch.setenv("GS_GROUP_RETUNE", "2")
     world, n, B = 3, 3 << 15, 1 << 12
+    if not isinstance(inject, tuple):
+        inject = (inject,)
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")
     gs.gen_bip(src, dst, 0, n, 12, 0x5EED0B1B, inject=inject)
@@ -128,7 +131,7 @@ def test_signed_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, inject, lan
 
     def rank(r):
         with gs.Summary("signed", capacity_hint=1 << 12) as s:
-            g = gs.Group(s, uid, world, r, B, 512)
+            g = gs.Group(s, uid, world, r, B)
             g.fold_batches(src[r * per:], dst[r * per:], per, B)
             g.finish()
             res = s.colouring()

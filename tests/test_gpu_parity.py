@@ -314,37 +314,43 @@ def test_delta_exchange_reproduces_union(gs, oracle_mod):
     assert total < len(s)
 
 
-def test_delta_stage_backlog_and_exchange_fold(gs, oracle_mod):
-    # gs_delta_stage with a small cap keeps a backlog; folding the gathered buffers
-    # (gs_fold_exchange_device) until every backlog is empty reproduces the union.
+def _stage_and_gather(gs, reps, width):
+    """Every replica stages its delta (gs_delta_stage); the buffers are concatenated
+    the way the data all-gather lays them out: world blocks of max-count rows."""
     import torch
+    world = len(reps)
+    cap = reps[0].delta_capacity()
+    sends = [torch.empty((cap, width), dtype=torch.int64, device="cuda") for _ in range(world)]
+    counts = torch.zeros(world, dtype=torch.int64, device="cuda")
+    for r in range(world):
+        reps[r].delta_stage(sends[r], cap, counts[r:r + 1], width)
+        reps[r].sync()
+    live = [int(c) & ((1 << 62) - 1) for c in counts.tolist()]
+    rows = max(1, max(live))
+    recv = torch.cat([x[:rows] for x in sends]).contiguous()
+    return recv, counts, rows, live
+
+
+@pytest.mark.parametrize("width", [2, 3])
+def test_delta_stage_and_exchange_fold(gs, oracle_mod, width):
+    # every replica stages its whole delta; folding the gathered buffer (live rows of
+    # each block from the count words) reproduces the union on every replica
     s, d = oracle_mod.rmat_edges(6, 13, 0, 1 << 15, True)
-    world, B, cap = 3, 1 << 11, 300
+    world, B = 3, 1 << 11
     reps = [gs.Summary("cc", capacity_hint=1 << 12) for _ in range(world)]
     for r in reps:
         r.set_delta_tracking(True)
-    sends = [torch.empty((cap + 1, 3), dtype=torch.int64, device="cuda") for _ in range(world)]
-
-    def exchange():
-        for r in range(world):
-            reps[r].delta_stage(sends[r], cap)
-            reps[r].sync()
-        recv = torch.cat(sends)
-        for r in range(world):
-            reps[r].fold_exchange(recv, world, cap + 1, r)
-        hdr = recv.view(world, cap + 1, 3)[:, 0, :].cpu()
-        return int((hdr[:, 1] - hdr[:, 0]).max())
-
-    backlog_seen = 0
+    assert reps[0].delta_capacity() >= 1 << 22
+    padded = 0
     for i in range(0, len(s), world * B):
         for r in range(world):
             lo = i + r * B
             reps[r].fold(s[lo:lo + B], d[lo:lo + B])
-        backlog_seen = max(backlog_seen, exchange())
-    while exchange() > 0:
-        pass
-    exchange()  # headers of a drained round are all empty
-    assert backlog_seen > 0  # the small cap forced a backlog
+        recv, counts, rows, live = _stage_and_gather(gs, reps, width)
+        assert max(live) <= B  # at most one record per folded edge
+        padded += world * rows - sum(live)
+        for r in range(world):
+            reps[r].fold_exchange(recv, counts, world, rows, r, width)
     for r in reps:
         _assert_cc_equal(r, oracle_mod, s, d)
         r.close()
@@ -353,31 +359,45 @@ def test_delta_stage_backlog_and_exchange_fold(gs, oracle_mod):
 @pytest.mark.parametrize("skip", [-1, 7])
 def test_exchange_fold_grows_table_from_remote_rows(gs, oracle_mod, skip):
     # A replica that folds nothing itself receives every vertex through exchange
-    # folds (padded 3-rank buffers, cap far above the live rows). The capacity bound
-    # charges only the folded ranks' record rows (gs_capi.cpp fold_device_impl), so
-    # the tiny table must still grow in time: labels equal the oracle's.
+    # folds; its tiny table must grow in time: labels equal the oracle's.
     # skip = -1 folds every block; skip = 7 (no such rank) must not drop a block.
-    import torch
     s, d = oracle_mod.rmat_edges(6, 12, 0, 1 << 14, True)
-    world, B, cap = 3, 1 << 10, 4000
+    world, B = 3, 1 << 10
     senders = [gs.Summary("cc", capacity_hint=1 << 13) for _ in range(world)]
     sink = gs.Summary("cc", capacity_hint=64)
     for r in senders:
         r.set_delta_tracking(True)
-    sends = [torch.empty((cap + 1, 3), dtype=torch.int64, device="cuda") for _ in range(world)]
     for i in range(0, len(s), world * B):
         for r in range(world):
             lo = i + r * B
             senders[r].fold(s[lo:lo + B], d[lo:lo + B])
-            senders[r].delta_stage(sends[r], cap)
-            senders[r].sync()
-        recv = torch.cat(sends)
-        hdr = recv.view(world, cap + 1, 3)[:, 0, :].cpu()
-        assert int((hdr[:, 1] - hdr[:, 0]).max()) == 0  # cap covers every batch: no backlog
-        sink.fold_exchange(recv, world, cap + 1, skip)
+        recv, counts, rows, live = _stage_and_gather(gs, senders, 3)
+        sink.fold_exchange(recv, counts, world, rows, skip, 3)
     _assert_cc_equal(sink, oracle_mod, s, d)
     for r in senders + [sink]:
         r.close()
+
+
+def test_exchange_count_word_carries_signed_failure(gs, oracle_mod):
+    """a rank whose replica finds an odd cycle among vertices it
+    already connected produces NO record for that edge; the count word's failure bit
+    must carry the verdict to every other replica."""
+    import torch
+    with gs.Summary("signed", capacity_hint=64) as a, gs.Summary("signed", capacity_hint=64) as b:
+        for x in (a, b):
+            x.set_delta_tracking(True)
+        a.fold(np.array([1, 2]), np.array([2, 3]))  # path 1-2-3
+        b.fold(np.array([10]), np.array([11]))
+        recv, counts, rows, live = _stage_and_gather(gs, [a, b], 3)
+        for r, x in enumerate((a, b)):
+            x.fold_exchange(recv, counts, 2, rows, r, 3)
+        a.fold(np.array([1]), np.array([3]))  # odd cycle inside a's replica: a hook-free failure
+        assert not a.ok() and b.ok()
+        recv, counts, rows, live = _stage_and_gather(gs, [a, b], 3)
+        assert live[0] == 0 and (int(counts[0]) >> 62) & 1 == 1
+        b.fold_exchange(recv, counts, 2, rows, 1, 3)
+        assert not b.ok()
+        assert [oracle_mod.canonical_candidates_string(*b.colouring())] == ["(false,{})"]
 
 
 def test_delta_records_skip_padding(gs, oracle_mod):
@@ -487,59 +507,71 @@ def test_gpu_generators_match_oracle(gs, oracle_mod):
     assert np.array_equal(s.cpu().numpy(), os_) and np.array_equal(d.cpu().numpy(), od)
 
 
-# ------------------------------------------------------------- hook policies / kernel variants
-@pytest.mark.parametrize("mode,inline_max,ept", [("fused", "64", "1"), ("fused", "64", "2"), ("defer", "0", "1"),
-                                                  ("defer", "4", "2"), ("compact", "0", "1")])
-def test_hook_policies_agree(gs, oracle_mod, monkeypatch, mode, inline_max, ept):
-    monkeypatch.setenv("GS_HOOK_MODE", mode)
-    monkeypatch.setenv("GS_INLINE_MAX", inline_max)
-    monkeypatch.setenv("GS_EPT", ept)
-    s, d = oracle_mod.rmat_edges(0x5EED0016, 16, 0, 1 << 19, True)
-    with gs.Summary("cc", capacity_hint=1 << 16) as ds:
-        for i in range(0, len(s), 1 << 15):
-            ds.fold(s[i:i + (1 << 15)], d[i:i + (1 << 15)])
-        _assert_cc_equal(ds, oracle_mod, s, d)
-    rng = np.random.default_rng(8)
-    for trial in range(6):
-        n = int(rng.integers(50, 3000))
-        m = int(rng.integers(10, 5000))
-        bs = rng.integers(-n, n, m)
-        bd = rng.integers(-n, n, m)
-        with gs.Summary("signed", capacity_hint=256) as c:
-            for i in range(0, m, 997):
-                c.fold(bs[i:i + 997], bd[i:i + 997])
-            truth = oracle_mod.canonical_candidates_string(*oracle_mod.bip_truth(bs, bd))
-            assert oracle_mod.canonical_candidates_string(*c.colouring()) == truth
-
-
-@pytest.mark.parametrize("hot_log2", ["10", "13"])
-def test_hot_level_closure_and_seals(gs, oracle_mod, monkeypatch, hot_log2):
-    # a small hot level fills up, closes (async vertex count) and gets sealed while
-    # the stream goes on: every key must still live in exactly one level
-    monkeypatch.setenv("GS_HOT_LOG2", hot_log2)
-    s, d = oracle_mod.rmat_edges(0x5EED0017, 16, 0, 1 << 19, True)
-    with gs.Summary("cc", capacity_hint=1 << 16) as ds:
-        for i in range(0, len(s), 1 << 13):
-            ds.fold(s[i:i + (1 << 13)], d[i:i + (1 << 13)])
-        _assert_cc_equal(ds, oracle_mod, s, d)
+# ------------------------------------------------------------- vertex list / resets / batched find
+@pytest.mark.parametrize("hint", [1 << 20, 1 << 10])
+def test_vertex_list_reset_and_export(gs, oracle_mod, hint):
+    """Sparse tables reset and export over the vertex list (O(vertices)); dense ones
+    scan the table. Both must leave exactly the initial table / every vertex:
+    alternate streams through one handle (a pooled window partial) and compare."""
+    with gs.Summary("cc", capacity_hint=hint) as ds:
+        for seed in range(4):
+            s, d = oracle_mod.rmat_edges(100 + seed, 12 + seed % 2, 0, 1 << (12 + seed), True)
+            s = np.concatenate([s, np.array([I64_MIN, 5], np.int64)])
+            d = np.concatenate([d, np.array([I64_MIN, I64_MIN], np.int64)])
+            ds.reset()
+            for i in range(0, len(s), 1000):
+                ds.fold(s[i:i + 1000], d[i:i + 1000])
+            _assert_cc_equal(ds, oracle_mod, s, d)
+            assert ds.find(I64_MIN) == I64_MIN and ds.find(5) == I64_MIN
+        ds.reset()
+        assert ds.num_vertices() == 0 and ds.find(5) is None
         v, lab = ds.labels()
-        for k in range(0, len(v), max(1, len(v) // 50)):
-            assert ds.find(int(v[k])) == int(lab[k])
-        assert ds.num_vertices() == len(v)
-    with gs.Summary("signed", capacity_hint=1 << 16) as c:
-        bs, bd = oracle_mod.bip_edges(21, 14, 0, 1 << 17, [1 << 16])
-        for i in range(0, len(bs), 1 << 12):
-            c.fold(bs[i:i + (1 << 12)], bd[i:i + (1 << 12)])
-        assert c.ok() == oracle_mod.bip_truth(bs, bd)[0]
+        assert len(v) == 0
 
 
-def test_reserved_ids_with_hot_level(gs, oracle_mod, monkeypatch):
-    monkeypatch.setenv("GS_HOT_LOG2", "8")
-    ids = np.array([I64_MIN, I64_MIN + 1, I64_MIN + 2, -5, 0, 7, I64_MAX], dtype=np.int64)
-    s = np.array([ids[1], ids[2], ids[3], ids[4], ids[6], ids[0], ids[5]], dtype=np.int64)
-    d = np.array([ids[2], ids[3], ids[1], ids[5], ids[6], ids[0], ids[5]], dtype=np.int64)
-    with gs.Summary("cc", capacity_hint=1 << 16) as ds:
-        ds.fold(s, d)
+def test_small_folds_rotate_shards(gs, oracle_mod):
+    """Many one-block folds: the rotating first shard spreads the vertex list over
+    all 64 shards, so no shard overflows (the list stays usable: counters bit 1 off)."""
+    s, d = oracle_mod.er_edges(0x5EED00E5, 16, 0, 1 << 15, True)
+    with gs.Summary("cc", capacity_hint=1 << 15) as ds:
+        for i in range(0, len(s), 200):
+            ds.fold(s[i:i + 200], d[i:i + 200])
+        assert (ds.counters()["ovf"] & 2) == 0
         _assert_cc_equal(ds, oracle_mod, s, d)
-        assert ds.find(I64_MIN + 1) == I64_MIN + 1
-        assert ds.find(I64_MIN) == I64_MIN
+
+
+def test_find_labels_device(gs, oracle_mod):
+    import torch
+    s, d = oracle_mod.rmat_edges(0x5EED0026, 14, 0, 1 << 16, True)
+    ov, olab = oracle_mod.cc_labels(s, d)
+    with gs.Summary("cc", capacity_hint=1 << 14) as ds:
+        ds.fold(s, d)
+        q = np.concatenate([ov, np.array([123456789, I64_MIN], np.int64)])
+        tq = torch.from_numpy(q).cuda()
+        lab = torch.empty_like(tq)
+        found = torch.empty(len(q), dtype=torch.uint8, device="cuda")
+        ds.find_labels_device(tq, lab, found)
+        ds.sync()
+        assert np.array_equal(lab.cpu().numpy()[:len(ov)], olab)
+        assert found.cpu().numpy().tolist() == [1] * len(ov) + [0, 0]
+        assert int(lab[-2]) == 123456789
+
+
+def test_capacity_sync_then_near_limit_fold_does_not_stall(gs, oracle_mod):
+    """after a synchronising capacity check, edges left unclaimed
+    by any report must not make later checks spin their 200 ms wait."""
+    import torch
+    n, B = 1 << 18, 1 << 12
+    s = torch.empty(n, dtype=torch.int64, device="cuda")
+    d = torch.empty(n, dtype=torch.int64, device="cuda")
+    gs.gen_er(s, d, 0, n, 17, 0x5EED00E5, True)
+    torch.cuda.synchronize()
+    with gs.Summary("cc", capacity_hint=16) as ds:
+        ds.set_pipelining(3)
+        for i in range(0, n, B):
+            ds.fold_device(s[i:], d[i:], n=B)
+        st = ds.capacity_stats()
+        assert st["syncs"] >= 1
+        # no wait may last the full 200 ms budget
+        assert st["wait_ms"] < 150 * max(1, st["waits"]), st
+        _assert_cc_equal(ds, oracle_mod, s.cpu().numpy(), d.cpu().numpy())
