@@ -49,13 +49,12 @@ def parse():
                    help="pipelined windows at N=1 (gs_set_pipelining depth; 1 = strictly in order)")
     p.add_argument("--exchange", action="store_true",
                    help="run the multi-GPU delta-exchange path even at one rank (overhead measurement)")
-    p.add_argument("--exchange-log-batch", type=int, default=20,
-                   help="per-rank micro-batch (log2 edges) between delta exchanges at N > 1 (or --exchange): "
-                        "SURVEY.md 8(d) config 3 = 2^20 per GPU, combine every global batch")
+    p.add_argument("--exchange-log-batch", type=int, default=22,
+                   help="combine cadence: edges per rank (log2) between delta exchanges at N > 1 (or --exchange). "
+                        "Every rank folds 2^20-edge micro-batches (SURVEY.md 8(d) config 3); the exchange runs every "
+                        "4 of them by default because each exchange has a fixed host cost (DESIGN.md section 5)")
     p.add_argument("--capacity-log2", type=int, default=0,
-                   help="relabel-table capacity hint of the CC summary (log2 vertices; 0: 2^scale, or "
-                        "2^(scale+1) on the exchange path: headroom for the host capacity bound while "
-                        "gathered rows are in flight, DESIGN.md section 5)")
+                   help="relabel-table capacity hint of the CC summary (log2 vertices; 0: 2^scale)")
     p.add_argument("--exchange-impl", choices=["native", "torch"], default="native",
                    help="native: RCCL inside libgs_summary (gs_group_*); torch: torch.distributed all-gather")
     return p.parse_args()
@@ -339,12 +338,13 @@ def main():
     from gelly_streaming_amd.distributed import DeltaExchangeFold
 
     E = (1 << args.scale) * args.edge_factor
-    B = 1 << (args.exchange_log_batch if (world > 1 or args.exchange) else args.log_batch)
+    grouped = world > 1 or args.exchange
+    B = 1 << (args.exchange_log_batch if grouped else args.log_batch)
     per = E // world
     start = rank * per
     nbatch = (per + B - 1) // B
 
-    xlog = args.scale + 1 if (world > 1 or args.exchange) else args.scale
+    xlog = args.scale
     summ = gs.Summary("cc", device=local, capacity_hint=1 << (args.capacity_log2 or xlog))
     st = summ.stream
     src = torch.empty(per, dtype=torch.int64, device=dev)
@@ -483,7 +483,10 @@ def main():
             "dtype": "int64",
             "data": "synthetic",
             "config": {"workload": "rmat%d-cc-stream" % args.scale, "scale": args.scale,
-                       "edges": E, "micro_batch": B, "ids": "sparse 64-bit (scrambled)",
+                       "edges": E, "micro_batch": 1 << args.log_batch if not grouped else 1 << 20,
+                       "combine_every_edges_per_gpu": 1 << args.exchange_log_batch,
+                       "combine": "delta exchange (native RCCL group)" if grouped else "none at 1 GPU (same cadence)",
+                       "ids": "sparse 64-bit (scrambled)",
                        "capacity_hint": 1 << (args.capacity_log2 or xlog),
                        "vertices_labelled": int(labelled),
                        "parallelism": ("edge-shard x%d, per-batch delta all-gather (%s)" % (world, args.exchange_impl))

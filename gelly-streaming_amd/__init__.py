@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "gs_group_destroy", "gs_group_tree_combine", "gs_combine_exported_device",
     "gs_group_fold_batches_device", "gs_export_labels_part_device",
     "gs_delta_capacity", "gs_find_labels_device", "gs_capacity_stats",
+    "gs_set_change_tracking", "gs_take_changes_device",
 )
 
 
@@ -107,6 +108,8 @@ def lib():
     L.gs_delta_capacity.argtypes = [_vp, ctypes.POINTER(_u64)]
     L.gs_find_labels_device.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.gs_capacity_stats.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double)]
+    L.gs_set_change_tracking.argtypes = [_vp, ctypes.c_int]
+    L.gs_take_changes_device.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.POINTER(_u64)]
     L.gs_get_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
     L.gs_set_profiling.argtypes = [_vp, ctypes.c_int]
     L.gs_set_pipelining.argtypes = [_vp, ctypes.c_int]
@@ -291,6 +294,29 @@ class Summary:
     # --- delta (multi-GPU exchange)
     def set_delta_tracking(self, on=True):
         _check(lib().gs_set_delta_tracking(self._h, 1 if on else 0))
+
+    # --- per-window change emission (sinks)
+    def set_change_tracking(self, on=True):
+        _check(lib().gs_set_change_tracking(self._h, 1 if on else 0))
+
+    def take_changes_device(self, v, label, parity=None):
+        """Rows (v, canonical label[, parity]) of every vertex inserted or relabelled
+        since the previous take into DEVICE arrays (capacity >= num_vertices());
+        returns the row count (gs_take_changes_device)."""
+        n = _u64()
+        cap = v.numel() if hasattr(v, "numel") else len(v)
+        _check(lib().gs_take_changes_device(self._h, _ptr(v), _ptr(label), _ptr(parity), int(cap), ctypes.byref(n)))
+        return n.value
+
+    def take_changes(self):
+        """take_changes_device into fresh device arrays; (v, label) numpy arrays."""
+        import torch
+        m = self.num_vertices() + 1
+        dev = torch.device("cuda", self.device)
+        v = torch.empty(m, dtype=torch.int64, device=dev)
+        lab = torch.empty(m, dtype=torch.int64, device=dev)
+        k = self.take_changes_device(v, lab)
+        return v[:k].cpu().numpy(), lab[:k].cpu().numpy()
 
     def delta_capacity(self):
         """Rows the delta list holds between two takes / stages (gs_delta_capacity)."""

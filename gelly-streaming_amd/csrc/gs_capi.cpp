@@ -207,7 +207,7 @@ int grow(gs_summary* h, uint64_t new_cap) {
   rc = alloc_table(h, new_cap, /*keep_delta=*/true);
   if (!rc && fail_flag && hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, h->stream) != hipSuccess)
     rc = fail(GS_ERR_HIP, "table rebuild: flag write failed");
-  if (!rc && h->changes) rc = change_tracking_reset(h, /*full=*/true);
+  if (!rc && h->changes) rc = change_tracking_reset(h, 2);
   if (!rc) {
     reset_capacity_tracking(h, got);
     rc = fold_device_impl(h, v, l, p, got, 1, 1, /*track=*/false, /*check_cap=*/false);
@@ -350,9 +350,10 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
   // overlap the previous fold. Union is associative and commutative, so the forest
   // after both is the same; readers join the lanes.
   const bool pipe = fs.allow_pipe && h->pipe_depth > 1 && !track && fs.rows == 0 && !h->profiling && !h->changes;
+  const bool on_lane = fs.lane >= 0 && !h->profiling;
   // remote rows of a group exchange: on the side stream, overlapping own folds
   const bool side = fs.on_side && side_ok(h) && !track;
-  if (!pipe && !side) {
+  if (!pipe && !side && !on_lane) {
     if (int rc = join_pipe_lanes(h)) return rc;  // the side stream is NOT joined: union commutes
   }
   const bool sign = h->kind == GS_KIND_SIGNED;
@@ -360,8 +361,8 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     const uint32_t c = (uint32_t)std::min<size_t>(kMaxChunk, n - off);
     const uint32_t blocks = (c + gs::kFoldBS - 1) / gs::kFoldBS;
     if (track) {
-      h->delta_fill_ub += per_shard_edges(c);
-      if (!h->drec || h->delta_fill_ub > h->delta_shard_cap)
+      h->delta_fill_ub[h->dset] += per_shard_edges(c);
+      if (!h->drec || h->delta_fill_ub[h->dset] > h->delta_shard_cap)
         return fail(GS_ERR_CAPACITY, "delta list full: stage or take the delta records after at most " +
                                          std::to_string(h->delta_edges) + " folded edges");
     }
@@ -372,6 +373,9 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       st = h->lane[h->lane_next];
       h->lane_next = (h->lane_next + 1) % h->pipe_depth;
       GS_HIP(hipStreamWaitEvent(st, h->main_ev, 0));
+      h->lanes_dirty = true;
+    } else if (on_lane) {  // the caller ordered the lane (a group's own fold)
+      st = h->lane[fs.lane];
       h->lanes_dirty = true;
     }
     gs::FoldLaunch f;
@@ -456,22 +460,23 @@ int ensure_delta_list(gs_summary* h, uint64_t edges) {
     (void)hipFree(h->drec);
     h->drec = nullptr;
   }
-  GS_HIP(hipMalloc(&h->drec, (size_t)gs::kShards * per * 24));
+  GS_HIP(hipMalloc(&h->drec, 2 * (size_t)gs::kShards * per * 24));
   h->delta_shard_cap = (uint32_t)per;
   h->delta_edges = edges;
   return GS_OK;
 }
 
 int stage_delta(gs_summary* h, int64_t* out, uint64_t cap, int width, unsigned long long* count_out, bool with_fail,
-                hipStream_t st) {
+                hipStream_t st, int set) {
   if (!h->drec) return fail(GS_ERR_INVALID, "delta tracking was never enabled");
   st = st ? st : h->stream;
+  if (set < 0) set = h->dset;
   {
     Prof p(h, KID_STAGE, st);
-    gs::launch_stage(h->table(), h->delta(), out, cap, width, count_out, with_fail, st);
+    gs::launch_stage(h->table(), h->delta(set), out, cap, width, count_out, with_fail, st);
   }
   GS_HIP(hipGetLastError());
-  h->delta_fill_ub = 0;
+  h->delta_fill_ub[set] = 0;
   return GS_OK;
 }
 
@@ -570,21 +575,21 @@ int gs_reset(gs_handle h) {
   if (int rc = check(h)) return rc;
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
+  const bool by_list = use_vertex_list(h, h->nv_ub);
   {
     Prof p(h, KID_INIT);
-    if (use_vertex_list(h, h->nv_ub)) {  // O(vertices): only the touched slots (no host sync)
+    if (by_list) {  // O(vertices): only the touched slots (no host sync)
       gs::launch_reset_list(h->table(), h->nxt, h->nv_ub, h->stream);
     } else {
       gs::launch_init(h->tab, h->cap + 1, h->stream);
     }
   }
   GS_HIP(hipGetLastError());
-  if (h->changes && !use_vertex_list(h, h->nv_ub))
-    if (int rc = change_tracking_reset(h, /*full=*/false)) return rc;
+  if (int rc = change_tracking_reset(h, by_list ? 0 : 1)) return rc;
   GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
   h->vlist_ok = true;
   reset_capacity_tracking(h, 0);
-  h->delta_fill_ub = 0;
+  h->delta_fill_ub[0] = h->delta_fill_ub[1] = 0;
   return GS_OK;
 }
 
@@ -898,8 +903,9 @@ int gs_set_delta_tracking(gs_handle h, int on) {
   if (int rc_ = join_lanes(h)) return rc_;
   if (on)
     if (int rc = ensure_delta_list(h, kMaxChunk)) return rc;
-  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, gs::kShards * gs::kCtrStride * 4, h->stream));
-  h->delta_fill_ub = 0;
+  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, 2 * gs::kShards * gs::kCtrStride * 4, h->stream));
+  h->delta_fill_ub[0] = h->delta_fill_ub[1] = 0;
+  h->dset = 0;
   h->track = on != 0;
   return GS_OK;
 }

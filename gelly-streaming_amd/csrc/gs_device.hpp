@@ -41,8 +41,8 @@ constexpr int kCtrStride = 32;     // u32 per counter line
 constexpr uint64_t kFailBit = 1ull << 62;  // exchange count word: the sender's verdict failed
 enum CounterBlock : int {
   CTR_NV = 0,                    // [kShards] new-vertex counts (= vertex-list fill per shard)
-  CTR_DELTA = kShards,           // [kShards] delta-record counts
-  CTR_FAIL = 2 * kShards,        // sticky bipartiteness failure
+  CTR_DELTA = kShards,           // [2][kShards] delta-record counts (two delta sets)
+  CTR_FAIL = 3 * kShards,        // sticky bipartiteness failure
   CTR_ERR,                       // device-side error (table overflow)
   CTR_EXPORT,                    // export append counter
   CTR_OVF,                       // delta list overflow
@@ -66,6 +66,7 @@ __host__ __device__ constexpr int ctr_index(int c) { return c * kCtrStride; }
 // aux bits of a slot
 constexpr uint32_t kAuxPresent = 1u;  // reserved slot only: INT64_MIN is a vertex
 constexpr uint32_t kAuxNew = 2u;      // change tracking: inserted since the last emission
+constexpr uint32_t kAuxBig = 4u;      // change emission: a root whose absorbed list is too long to walk
 
 struct alignas(16) Slot {
   int64_t key;
@@ -86,8 +87,9 @@ struct Table {
 };
 
 struct Delta {
-  int64_t* drec;       // records {a, b, parity} [kShards][shard_cap][3], or null (not tracking)
+  int64_t* drec;       // records {a, b, parity} of one delta set [kShards][shard_cap][3], or null
   uint32_t shard_cap;
+  uint32_t dctr;       // counter index of that set's shard 0 (CTR_DELTA + set * kShards)
 };
 
 __device__ __forceinline__ uint32_t hash_slot(int64_t key, int shift) {
@@ -325,7 +327,7 @@ __device__ __forceinline__ void combine_hooks(bool active, uint32_t& a, int64_t&
 // Append one delta record {a, b, w} to shard `shard` of the delta list.
 __device__ __forceinline__ void append_record(const Table& t, const Delta& D, int shard, int64_t a, int64_t b,
                                               int64_t w) {
-  const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_DELTA + shard)], 1u);
+  const uint32_t pos = atomicAdd(&t.ctr[ctr_index(D.dctr + shard)], 1u);
   if (pos < D.shard_cap) {
     int64_t* r = D.drec + ((size_t)shard * D.shard_cap + pos) * 3;
     r[0] = a;

@@ -82,16 +82,21 @@ struct gs_summary {
   uint64_t e_lost = 0;      // launched edges no report will ever claim (complete: dropped at a sync)
   uint64_t nv_exact = 0, e_exact = 0;  // an exact count and the edges complete when it was read
   // delta records (multi-GPU exchange, change emission)
+  // Two delta sets: a group's own fold b records into set b % 2 while the stage of
+  // exchange b - 1 reads the other set on the communication stream.
   bool track = false;
-  int64_t* drec = nullptr;  // [kShards][delta_shard_cap][3]
+  int64_t* drec = nullptr;  // [2][kShards][delta_shard_cap][3]
   uint32_t delta_shard_cap = 0;
-  uint64_t delta_edges = 0;  // fold edges the delta list holds between two stages
-  uint64_t delta_fill_ub = 0;  // worst-case per-shard fill since the last stage
+  uint64_t delta_edges = 0;  // fold edges one delta set holds between two stages
+  int dset = 0;              // the set tracked folds record into
+  uint64_t delta_fill_ub[2] = {0, 0};  // worst-case per-shard fill of each set since its last stage
   // change tracking (gs_changes.cpp)
   bool changes = false;
   uint32_t* nxt = nullptr;  // [cap + 1] circular member lists
-  unsigned long long* chg_scratch = nullptr;  // emission scratch: staged records, counters
+  uint64_t nxt_slots = 0;
+  unsigned long long* chg_scratch = nullptr;  // emission scratch: count, marks, big roots, staged records
   uint64_t chg_scratch_rows = 0;
+  bool chg_scan_all = false;  // the next emission emits every vertex (after a rebuild)
   // staging for host folds
   int64_t* d_stage = nullptr;  // [2][2][kStageChunk]
   uint8_t* d_wstage = nullptr; // [2][kStageChunk]
@@ -157,10 +162,12 @@ struct gs_summary {
     t.mark_new = changes ? 1 : 0;
     return t;
   }
-  gs::Delta delta() const {
+  gs::Delta delta(int set = -1) const {
+    if (set < 0) set = dset;
     gs::Delta D;
-    D.drec = drec;
+    D.drec = drec ? drec + (size_t)set * gs::kShards * delta_shard_cap * 3 : nullptr;
     D.shard_cap = delta_shard_cap;
+    D.dctr = (uint32_t)(gs::CTR_DELTA + set * gs::kShards);
     return D;
   }
 };
@@ -177,6 +184,7 @@ struct FoldSource {
   const uint32_t* fail_in = nullptr;           // device failure flag of a combined summary
   bool on_side = false;  // launch on h->side (a group's apply stream) instead of h->stream
   bool allow_pipe = false;
+  int lane = -1;         // >= 0: launch on this pipelining lane (a group's own tracked fold)
 };
 
 int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
@@ -191,9 +199,11 @@ int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t
 // stage every pending delta record into out (first cap rows, `width` int64 each) and
 // the count word into *count_out (device); the delta list is emptied
 int stage_delta(gs_summary* h, int64_t* out, uint64_t cap, int width, unsigned long long* count_out, bool with_fail,
-                hipStream_t st = nullptr);
+                hipStream_t st = nullptr, int set = -1);
 int ensure_delta_list(gs_summary* h, uint64_t edges);
 bool use_vertex_list(gs_summary* h, uint64_t nv_bound);
-int change_tracking_reset(gs_summary* h, bool full);  // gs_changes.cpp: after reset / rebuild
+// gs_changes.cpp, after a reset (mode 0: vertex-list reset, 1: full table init) or a
+// rebuild into a new table (mode 2)
+int change_tracking_reset(gs_summary* h, int mode);
 
 }  // namespace gsi

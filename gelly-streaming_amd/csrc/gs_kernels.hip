@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Delta D, int64_t* __rest
   __shared__ uint64_t off_sh, total_sh;
   __shared__ uint32_t last;
   const uint32_t s = blockIdx.x;
-  if (threadIdx.x < kShards) cnt[threadIdx.x] = min(t.ctr[ctr_index(CTR_DELTA + threadIdx.x)], D.shard_cap);
+  if (threadIdx.x < kShards) cnt[threadIdx.x] = min(t.ctr[ctr_index(D.dctr + threadIdx.x)], D.shard_cap);
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t off = 0, tot = 0;
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Delta D, int64_t* __rest
   if (threadIdx.x == 0) last = atomicAdd(&t.ctr[ctr_index(CTR_STAGE_DONE)], 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  if (threadIdx.x < kShards) t.ctr[ctr_index(CTR_DELTA + threadIdx.x)] = 0u;
+  if (threadIdx.x < kShards) t.ctr[ctr_index(D.dctr + threadIdx.x)] = 0u;
   if (threadIdx.x == 0) atomicExch(&t.ctr[ctr_index(CTR_STAGE_DONE)], 0u);
 }
 

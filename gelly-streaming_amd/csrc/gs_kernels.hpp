@@ -40,4 +40,15 @@ void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st);
 void launch_find_batch(const Table& t, const int64_t* v, uint64_t n, int64_t* label, uint8_t* found, uint8_t* parity,
                        hipStream_t st);
 
+// change emission (gs_changes_k.hip)
+void launch_iota(uint32_t* nxt, uint64_t n, hipStream_t st);
+void launch_relist(const Table& t, uint32_t* nxt, hipStream_t st);
+void launch_emit_records(const Table& t, uint32_t* nxt, const int64_t* rec, const unsigned long long* nrec,
+                         uint64_t nrec_bound, uint32_t walk_max, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap,
+                         uint32_t* big, hipStream_t st);
+void launch_emit_scan(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap, bool all, hipStream_t st);
+void launch_clear_big(const Table& t, const uint32_t* big, uint64_t n, hipStream_t st);
+void launch_emit_new(const Table& t, uint32_t* vmark, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap,
+                     uint64_t bound, bool emit, hipStream_t st);
+
 }  // namespace gs

@@ -201,6 +201,24 @@ int gs_fold_records_device(gs_handle h, const int64_t* rec, size_t n, int track)
 int gs_fold_exchange_device(gs_handle h, const int64_t* recv, const uint64_t* counts, size_t world, size_t rows,
                             int width, int skip_rank);
 
+/* ---- per-window change emission (sinks) ------------------------------------------
+ * The reference's Merger emits the whole cumulative summary every window
+ * (SummaryAggregation.java:107-119) and its sinks flatten it: FlattenSet emits
+ * (v, find(v)) for every vertex (ConnectedComponentsExample.java:143-156), keyed
+ * downstream; DisjointSet.toString groups every vertex (DisjointSet.java:134-150).
+ * With change tracking on, gs_take_changes_device emits only the rows a keyed sink
+ * needs to reach the same state: (v, canonical label[, parity]) for every vertex
+ * inserted or relabelled since the previous take, into DEVICE arrays; *n on the host
+ * (synchronises). Work is O(changes): members of each component whose old root was
+ * hooked this window are enumerated by walking a member list, not by a table scan;
+ * a relabelled component of more than 2^16 vertices is emitted by one parallel scan,
+ * which also re-emits the absorbing component's unchanged members (idempotent
+ * rows). The first take after a table rebuild emits every vertex. cap must be at
+ * least gs_num_vertices (each vertex is emitted at most once). Turns delta
+ * tracking on and consumes the delta records (not for a group's summary). */
+int gs_set_change_tracking(gs_handle h, int on);
+int gs_take_changes_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* parity, size_t cap, uint64_t* n);
+
 /* ---- introspection -----------------------------------------------------------
  * The HIP stream (hipStream_t) the handle enqueues on, and per-kernel timing:
  * when profiling is on, every launch is bracketed by HIP events on the stream it

@@ -31,11 +31,10 @@ import gsamd as gs  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=int, default=26)
-    ap.add_argument("--log-batch", type=int, default=20)
+    ap.add_argument("--log-batch", type=int, default=22, help="edges per rank between exchanges (log2)")
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--hint-log2", type=int, default=0, help="capacity hint of the rank replicas (0: 2^scale)")
-    ap.add_argument("--first-cap", type=int, default=0, help="rows of the first exchanges (0: the batch)")
     a = ap.parse_args()
     E, B = 16 << a.scale, 1 << a.log_batch
     src = torch.empty(E, dtype=torch.int64, device="cuda")
@@ -69,7 +68,7 @@ def main():
 
         def rank(r):
             try:
-                g = gs.Group(summ[r], uid, n, r, B, a.first_cap)
+                g = gs.Group(summ[r], uid, n, r, B)
                 for _ in range(a.reps + 1):
                     summ[r].reset()
                     summ[r].sync()
@@ -98,10 +97,12 @@ def main():
         for x in summ:
             x.close()
         tn = min(max(times[r][k] for r in range(n)) for k in range(1, a.reps + 1))
+        sent = sum(x["records_sent"] for x in recs)
         print("N=%d: %.2f ms for all ranks on one GPU, inflation %.2fx (efficiency bound %.2f); "
-              "exchanges/rank %d, records sent by rank 0 %d, final cap %d; vertices %s"
-              % (n, tn * 1e3, tn / t1, t1 / tn, recs[0]["exchanges"], recs[0]["records_sent"],
-                 recs[0]["cap"], sorted(set(nv))), flush=True)
+              "exchanges/rank %d, records sent by all ranks %d (per pass %d), rows received by rank 0 %d; "
+              "vertices %s"
+              % (n, tn * 1e3, tn / t1, t1 / tn, recs[0]["exchanges"], sent, sent // (a.reps + 1),
+                 recs[0]["rows_received"] // (a.reps + 1), sorted(set(nv))), flush=True)
     return 0
 
 
