@@ -29,20 +29,50 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-leve
 BYTES_PER_EDGE_SPARSE = 48   # 16 B edge + 2 x 12 B relabel probe + 2 x 4 B parent read
 
 
+def _lib_sha16():
+    import hashlib
+    path = os.path.join(ROOT, "gelly-streaming_amd", "lib", "libgs_summary.so")
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def _matching_pmc_profile(args, batch):
+    """roofline.traffic (HBM bytes per k_fold launch) from the committed rocprofv3 PMC
+    summary (profiles/pmc_fold_traffic.json, tools/rocprof_summary.py), used only when
+    it was taken of THIS library build, workload, micro-batch and pipeline depth;
+    otherwise null."""
+    path = os.path.join(ROOT, "profiles", "pmc_fold_traffic.json")
+    if not os.path.exists(path):
+        return None, {}
+    with open(path) as f:
+        pm = json.load(f)
+    want = {"workload": "rmat%d-cc-stream" % args.scale, "batch": batch, "pipeline": args.pipeline,
+            "lib_sha16": _lib_sha16()}
+    if any(pm.get(k) != v for k, v in want.items()):
+        return None, {"traffic_note": "no PMC profile of this build / configuration (profiles/pmc_fold_traffic.json "
+                                      "is of %s)" % pm.get("round")}
+    extra = {"traffic_source": pm.get("source"), "read_requests_per_edge": pm.get("read_requests_per_edge"),
+             "l2_hit_rate": pm.get("l2_hit_rate")}
+    return int(pm["hbm_bytes_per_launch"]), extra
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--workload", choices=["rmat-cc", "bip", "er-latency", "ingest"], default="rmat-cc",
+    p.add_argument("--workload", choices=["rmat-cc", "bip", "er-latency", "ingest", "dropin"], default="rmat-cc",
                    help="rmat-cc: BASELINE config 3 (the headline line); bip: config 4 (bipartiteness, "
                         "2x2^19 vertices, 2^24 edges); er-latency: config 5 (ER G(2^22, 2^26), 2^16-edge windows, "
-                        "per-window latency)")
+                        "per-window latency); dropin: config 2 through the unchanged operators (C++ host mirror, "
+                        "host edges, p = 1 and 8 partitions); ingest: text edge parsing")
     p.add_argument("--scale", type=int, default=26)
     p.add_argument("--edge-factor", type=int, default=16)
     p.add_argument("--log-batch", type=int, default=20)
     p.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED0026)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--bip-prefix-log2", type=int, default=15,
+                   help="bip: edges of the prefix the quirk-exact Candidates oracle folds (O(E x components))")
     p.add_argument("--cpu-sample-log2", type=int, default=24)
     p.add_argument("--no-profile-pass", action="store_true")
     p.add_argument("--pipeline", type=int, default=3,
@@ -173,12 +203,20 @@ def bench_bip(args):
         agree = True
     line = None
     if rank == 0:
-        import oracle  # checker only
+        import oracle  # checker and CPU baseline legs only
         fs = torch.empty(E, dtype=torch.int64, device=dev)
         fd = torch.empty(E, dtype=torch.int64, device=dev)
         gs.gen_bip(fs, fd, 0, E, logside, seed, inject, stream=summ.stream)
         summ.sync()
         first = oracle.bip_first_failure(fs.cpu().numpy(), fd.cpu().numpy())
+        # SURVEY.md 8(a) contract (ii): does the reference's Candidates diverge from the
+        # truth on this stream? Its merge is O(E x components): a capped prefix, one window
+        cap = 1 << args.bip_prefix_log2
+        ps, pd = fs[:cap].cpu().numpy(), fd[:cap].cpu().numpy()
+        div = oracle.bip_quirk_divergence(ps, pd)
+        c0 = time.perf_counter()
+        oracle.cpu_baseline_bip(ps, pd)
+        cpu_secs = time.perf_counter() - c0
         del fs, fd
         expect = None if first < 0 else first // B
         cfg = {"workload": "bip-config4", "side_vertices": 1 << logside, "edges": E, "micro_batch": B,
@@ -190,10 +228,20 @@ def bench_bip(args):
         else:
             cfg.update({"verdict_parity": agree and oks[0] and oks[1] == (first < 0),
                         "parallelism": "edge-shard x%d, per-batch signed delta all-gather (native group)" % world})
+        cfg["reference_quirk_check"] = {
+            "prefix_edges": cap, "diverges": div["diverges"],
+            "note": "quirk-exact Candidates restatement (oracle/gs_oracle.cpp) on the first %d edges of the odd-cycle "
+                    "stream in one window vs the truth; the generator's ids are not in first-appearance order, so "
+                    "the reference's colouring differs from the canonical one (Candidates.java:142-192) when "
+                    "diverges is true" % cap}
         line = {"metric": "edges/sec for streaming bipartiteness (config 4)", "value": round(E * args.steps / el, 1),
                 "unit": "edges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(el * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "strong",
-                "vs_baseline": None, "dtype": "int64", "data": "synthetic", "config": cfg}
+                "vs_baseline": None, "dtype": "int64", "data": "synthetic", "config": cfg,
+                "cpu_baseline": {"value": round(cap / cpu_secs, 1), "unit": "edges/s", "cores": 1, "kind": "port",
+                                 "sample": "first %d edges of the odd-cycle stream, Candidates.merge per edge "
+                                           "(quirk-exact restatement, O(E x components)), 1 thread, %.2f s"
+                                           % (cap, cpu_secs)}}
         print(json.dumps(line), flush=True)
     if group is not None:
         group.close()
@@ -311,8 +359,59 @@ def bench_ingest(args):
     print(json.dumps(line), flush=True)
 
 
+def bench_dropin(args):
+    """SURVEY.md 8(f) row 1 / VERDICT r1 item 3: BASELINE config 2 (RMAT-20, 2^24 edges,
+    2^20-edge windows) through the reference's UNCHANGED operators on the C++ host mirror
+    (gelly-streaming_amd/host/gelly_streaming.hpp): per edge UpdateCC.foldEdges ->
+    DisjointSet.union (buffered), per (partition, window) a fresh initial value (pooled
+    handle, gs_reset), per window CombineCC of the partials and the Merger -- the call
+    sequence Flink issues through the JNI glue. Edges in host memory
+    (PCIe-inclusive). p = 1 and 8 partitions; final labels checked against the oracle."""
+    import subprocess
+    import tempfile
+    import oracle  # checker and CPU baseline legs only
+    exe = os.path.join(ROOT, "gelly-streaming_amd", "host", "bin", "dropin_bench")
+    scale, logE, logW, seed = 20, 24, 20, 0x5EED0020
+    s, d = oracle.rmat_edges(seed, scale, 0, 1 << logE, True)
+    ov, olab = oracle.cc_labels(s, d)
+    runs = {}
+    for p in (1, 8):
+        best = None
+        for _ in range(max(1, args.steps)):
+            with tempfile.NamedTemporaryFile(suffix=".bin") as f:
+                r = subprocess.run([exe, str(scale), hex(seed), str(logE), str(logW), str(p), f.name],
+                                   capture_output=True, text=True, timeout=300)
+                if r.returncode != 0:
+                    raise SystemExit("dropin_bench failed: " + r.stderr[-2000:])
+                res = json.loads(r.stdout.strip().splitlines()[-1])
+                lab = np.fromfile(f.name, dtype=np.int64).reshape(-1, 2)
+            res["parity"] = bool(np.array_equal(lab[:, 0], ov) and np.array_equal(lab[:, 1], olab))
+            if best is None or res["seconds"] < best["seconds"]:
+                best = res
+        runs[p] = best
+    cpu = None
+    if not args.no_cpu_baseline:
+        secs1 = oracle.cpu_baseline_cc(s, d, 1 << logW, threads=1)
+        cpu = {"value": round((1 << logE) / secs1, 1), "unit": "edges/s", "cores": 1, "kind": "port",
+               "sample": "the same 2^%d edges, 2^%d-edge windows: DisjointSet.union per edge + CombineCC/Merger per "
+                         "window (oracle/gs_oracle.cpp), 1 thread, %.1f s" % (logE, logW, secs1)}
+    line = {"metric": "edges/sec through the drop-in operators (config 2, host edges)",
+            "value": round(runs[1]["edges_per_s"], 1), "unit": "edges/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": 0, "ms_per_step": round(runs[1]["seconds"] * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": "dropin-rmat20-config2", "edges": 1 << logE, "window": 1 << logW,
+                       "p1": runs[1], "p8": runs[8], "parity": runs[1]["parity"] and runs[8]["parity"],
+                       "path": "C++ host mirror: SummaryBulkAggregation.run -> ConnectedComponents (UpdateCC, "
+                               "CombineCC, Merger) over GPU DisjointSet summaries from a handle pool; wall time "
+                               "includes per-edge buffering and PCIe"},
+            "cpu_baseline": cpu}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.workload == "dropin":
+        return bench_dropin(args)
     if args.workload == "ingest":
         return bench_ingest(args)
     if args.workload == "bip":
@@ -413,41 +512,35 @@ def main():
         dist.all_reduce(c)
         labelled = int(c.item())
 
-    # Roofline of the dominant kernel (k_fold): HIP events around every launch on
-    # the summary's own stream, over one extra full step (same work as a timed step).
+    # Roofline of the dominant kernel (k_fold). Per launch: HIP events around every
+    # launch on the stream it runs on, over one extra full step (profiling serialises
+    # the folds, so each event pair brackets one kernel alone). Per step: the same
+    # algorithmic bytes over the timed wall clock (pipelined folds, exchange, label pass).
     roof = None
-    fold_avg_ms = None
     if not args.no_profile_pass:
         summ.set_profiling(True)
         one_step()
         summ.sync()
         nf, fold_ms = summ.kernel_stats("fold")
-        nh, hook_ms = summ.kernel_stats("stage")
+        ns, stage_ms = summ.kernel_stats("stage")
         ne, exp_ms = summ.kernel_stats("export")
         summ.set_profiling(False)
         fold_avg_ms = fold_ms / max(nf, 1)
-        edges_per_launch = per / max(nf, 1) if world == 1 else B  # own-shard launches dominate
+        edges_per_launch = per / max(nf, 1) if not grouped else 1 << 20  # own micro-batches dominate
         achieved = BYTES_PER_EDGE_SPARSE * edges_per_launch / (fold_avg_ms * 1e-3) / 1e9
-        traffic = None
-        traffic_gbs = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_fold_traffic.json")
-        if os.path.exists(pmc):  # PMC bytes per launch from the committed rocprofv3 passes
-            with open(pmc) as f:
-                pm = json.load(f)
-            if pm.get("workload") == "rmat%d-cc-stream" % args.scale and pm.get("batch") == B:
-                traffic = int(pm.get("hbm_bytes_per_launch"))
-                traffic_gbs = round(traffic / (fold_avg_ms * 1e-3) / 1e9, 1)
+        step_gbs = BYTES_PER_EDGE_SPARSE * per / (elapsed / args.steps) / 1e9
+        traffic, extra = _matching_pmc_profile(args, B)
         roof = {"kernel": "k_fold", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_gbs": traffic_gbs,
-                "traffic_frac": round(traffic_gbs / HBM_PEAK_GBS, 4) if traffic_gbs else None,
+                "achieved_step": round(step_gbs, 1), "frac_step": round(step_gbs / HBM_PEAK_GBS, 4),
                 "bytes_per_edge": BYTES_PER_EDGE_SPARSE, "edges_per_launch": int(edges_per_launch),
                 "fold_avg_us": round(fold_avg_ms * 1e3, 2), "fold_launches": int(nf),
-                "stage_avg_us": round(hook_ms * 1e3 / max(nh, 1), 2), "stage_launches": int(nh),
+                "stage_avg_us": round(stage_ms * 1e3 / max(ns, 1), 2), "stage_launches": int(ns),
                 "export_ms": round(exp_ms, 3)}
-        if xch is not None:
+        roof.update(extra)
+        if grouped:
             roof["note"] = ("exchange path: fold launches include the other ranks' gathered rows (side stream); "
-                            "achieved assumes %d own edges per launch" % int(edges_per_launch))
+                            "achieved assumes 2^20 own edges per launch")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

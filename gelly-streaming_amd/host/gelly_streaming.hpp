@@ -31,6 +31,7 @@
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -84,16 +85,64 @@ struct MapFunction {
 };
 
 // --------------------------------------------------------------------------
+// Handle pool. Flink copies the summary's initial value for every (partition,
+// window) fold (SummaryBulkAggregation.java:80, FoldingState) and drops the partial
+// after the all-window reduce; creating a GPU summary each time would cost a table
+// allocation and initialisation per window. Released handles are reset (O(touched
+// vertices) on the device, asynchronous) and handed to the next summary of the same
+// kind, device and capacity.
+// --------------------------------------------------------------------------
+class HandlePool {
+ public:
+  static HandlePool& instance() {
+    static HandlePool p;
+    return p;
+  }
+  gs_handle acquire(int kind, int device, uint64_t capacity_hint) {
+    auto& free = free_[{kind, device, capacity_hint}];
+    if (!free.empty()) {
+      gs_handle h = free.back();
+      free.pop_back();
+      ++reused_;
+      return h;
+    }
+    gs_handle h = nullptr;
+    gs_check(gs_create(&h, device, kind, capacity_hint));
+    ++created_;
+    return h;
+  }
+  void release(gs_handle h, int kind, int device, uint64_t capacity_hint) {
+    if (gs_reset(h) != GS_OK) {  // a broken handle is not pooled
+      gs_destroy(h);
+      return;
+    }
+    free_[{kind, device, capacity_hint}].push_back(h);
+  }
+  size_t created() const { return created_; }
+  size_t reused() const { return reused_; }
+  ~HandlePool() {
+    for (auto& kv : free_)
+      for (gs_handle h : kv.second) gs_destroy(h);
+  }
+
+ private:
+  std::map<std::tuple<int, int, uint64_t>, std::vector<gs_handle>> free_;
+  size_t created_ = 0, reused_ = 0;
+};
+
+// --------------------------------------------------------------------------
 // GPU-resident summaries
 // --------------------------------------------------------------------------
 class GpuSummary {
  public:
   GpuSummary(int kind, int device, uint64_t capacity_hint, size_t flush_edges)
-      : kind_(kind), device_(device), flush_edges_(flush_edges) {
-    gs_check(gs_create(&h_, device, kind, capacity_hint));
+      : kind_(kind), device_(device), hint_(capacity_hint), flush_edges_(flush_edges) {
+    h_ = HandlePool::instance().acquire(kind, device, capacity_hint);
+    src_.reserve(std::min<size_t>(flush_edges_, 1 << 16));
+    dst_.reserve(std::min<size_t>(flush_edges_, 1 << 16));
   }
   virtual ~GpuSummary() {
-    if (h_) gs_destroy(h_);
+    if (h_) HandlePool::instance().release(h_, kind_, device_, hint_);
   }
   GpuSummary(const GpuSummary&) = delete;
   GpuSummary& operator=(const GpuSummary&) = delete;
@@ -167,6 +216,7 @@ class GpuSummary {
  protected:
   int kind_;
   int device_;
+  uint64_t hint_;
   size_t flush_edges_;
   gs_handle h_ = nullptr;
   std::vector<int64_t> src_, dst_;
@@ -395,7 +445,10 @@ class SummaryBulkAggregation : public SummaryAggregation<K, EV, S, T> {
         const int part = (int)(k % (size_t)p);  // PartitionMapper.map (:103-105)
         if (!partial[part]) partial[part] = this->getInitialValue();
         const Edge<K, EV>& e = stream.edges[k];
-        partial[part] = this->updateFun_->foldEdges(partial[part], e.getSource(), e.getTarget(), e.getValue());
+        // the accumulator is handed over and returned (Java passes the reference):
+        // moved, so no reference-count traffic per edge
+        partial[part] =
+            this->updateFun_->foldEdges(std::move(partial[part]), e.getSource(), e.getTarget(), e.getValue());
       }
       S acc{};
       for (int q = 0; q < p; ++q) {  // timeWindowAll reduce, arrival order = partition order

@@ -198,6 +198,17 @@ def cpu_baseline_bip(src, dst):
     return lib().or_cpu_baseline_bip(src, dst, len(src))
 
 
+def bip_quirk_divergence(src, dst, win=None, part=None):
+    """SURVEY.md 8(a) contract (ii): does the reference's Candidates (quirk-exact
+    restatement, O(E x components)) diverge from the truth on this stream? Returns
+    {"quirk": its final emission, "truth": the canonical truth string, "diverges"}.
+    Candidates.merge's order / window bugs: Candidates.java:77-139,176."""
+    q = bip_dataflow(src, dst, win, part)
+    quirk = q[-1] if q else "(true,{})"
+    truth = canonical_candidates_string(*bip_truth(src, dst))
+    return {"quirk": quirk, "truth": truth, "diverges": quirk != truth}
+
+
 # ---------------- canonical formatting shared by tests ----------------
 def canonical_cc_string(v, lab):
     """'{min=[members ascending], ...}' -- DisjointSet.toString() shape."""

@@ -232,3 +232,25 @@ def _malformed(text, sep, i):
         if not re.fullmatch(rb"[+-]?[0-9]+", f) or not (-(1 << 63) <= int(f) < (1 << 63)):
             return True
     return False
+
+
+def test_bip_quirk_divergence_report(oracle_mod):
+    # the triangle fed as (2,3),(1,2),(1,3) in one window makes the
+    # reference's Candidates answer "bipartite" (Candidates.java:77-139,176); fed as
+    # (1,2),(2,3),(1,3) it answers (false,{}). The report flags the first only.
+    bad = oracle_mod.bip_quirk_divergence([2, 1, 1], [3, 2, 3])
+    assert bad["diverges"] and bad["truth"] == "(false,{})" and bad["quirk"].startswith("(true,")
+    good = oracle_mod.bip_quirk_divergence([1, 2, 1], [2, 3, 3])
+    assert not good["diverges"] and good["quirk"] == "(false,{})"
+    # the config-4 generator's ids are not in first-appearance order: the reference's
+    # colouring differs from the canonical one (min vertex = true) -- reported
+    s, d = oracle_mod.bip_edges(0x5EED0B1B, 8, 0, 2000)
+    assert oracle_mod.bip_quirk_divergence(s, d)["diverges"]
+    # relabelled in first-appearance order, one window (the exact regime): no divergence
+    ids = {}
+    for a, b in zip(s.tolist(), d.tolist()):
+        for x in (a, b):
+            ids.setdefault(x, len(ids) + 1)
+    rs = [ids[x] for x in s.tolist()]
+    rd = [ids[x] for x in d.tolist()]
+    assert not oracle_mod.bip_quirk_divergence(rs, rd)["diverges"]

@@ -1,14 +1,15 @@
 #!/bin/bash
-# Kernel-trace + PMC passes of one bench step (run on the GPU box from the repo root).
+# Kernel-trace + PMC passes of one bench step, at the bench's own default settings
+# (pipeline depth 3), run on the GPU box from the repo root. Each PMC group is its own
+# rocprofv3 run (counters are never combined with tracing domains).
 # Usage: bash tools/rocprof_round.sh <tag> [bench args...]
+# Then, in the container: python tools/rocprof_summary.py gpurun_out/rocprof_<tag> <tag> <pipeline>
 set -u
-TAG=${1:-r01}; shift || true
+TAG=${1:-r02}; shift || true
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/rocprof_$TAG
 mkdir -p $OUT
-# --pipeline 1: launches serialised, so the trace's per-launch k_fold duration is the one
-# bench.py's roofline measures (its profile pass also runs the folds one at a time)
-ARGS="--steps 1 --warmup 0 --no-cpu-baseline --no-profile-pass --pipeline 1 $*"
+ARGS="--steps 1 --warmup 0 --no-cpu-baseline --no-profile-pass $*"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- python3 $R/bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
 echo "trace ok"

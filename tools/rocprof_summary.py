@@ -5,7 +5,9 @@ every PMC counter collected in the separate --pmc passes. HBM traffic per k_fold
 launch is derived from FETCH_SIZE/WRITE_SIZE (KiB) with the gfx950 note of
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE tallies 128-B requests at 64 B, i.e.
 reads x2 for wide requests; TCC_EA0_RDREQ gives the request count directly.
-Usage: python tools/rocprof_summary.py gpurun_out/rocprof_r01 r01
+Also the k_fold busy time of the traced step: the union of its dispatch intervals
+(pipelined folds overlap), which must not exceed the bench's ms_per_step.
+Usage: python tools/rocprof_summary.py gpurun_out/rocprof_r02 r02 <pipeline depth> [batch]
 """
 import glob
 import json
@@ -15,8 +17,10 @@ import sys
 from collections import defaultdict
 
 d, tag = sys.argv[1], sys.argv[2]
+pipeline = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+batch = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 20
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-out = {"tag": tag, "kernels": {}}
+out = {"tag": tag, "pipeline": pipeline, "kernels": {}}
 
 
 def short(name):
@@ -37,6 +41,23 @@ db = sqlite3.connect(tr)
 for name, calls, tot, avg, pct in db.execute("select name,total_calls,total_duration,average,percentage from top_kernels"):
     out["kernels"].setdefault(short(name), {}).update(
         {"calls": calls, "total_us": round(tot, 1), "avg_us": round(avg, 3), "pct": round(pct, 2)})
+
+# busy time of the fold: union of its dispatch intervals in the traced step
+views = [r[0] for r in db.execute("select name from sqlite_master where type in ('view','table')")]
+src = "kernels" if "kernels" in views else [v for v in views if "kernel" in v.lower()][0]
+iv = sorted((s_, e_) for n_, s_, e_ in db.execute("select name, start, end from %s" % src) if "k_fold" in n_)
+busy, cur_s, cur_e = 0, None, None
+for s_, e_ in iv:
+    if cur_e is None or s_ > cur_e:
+        if cur_e is not None:
+            busy += cur_e - cur_s
+        cur_s, cur_e = s_, e_
+    else:
+        cur_e = max(cur_e, e_)
+if cur_e is not None:
+    busy += cur_e - cur_s
+out["k_fold_busy_ms_per_step"] = round(busy / 1e6, 3)
+out["k_fold_span_ms"] = round((iv[-1][1] - iv[0][0]) / 1e6, 3) if iv else None
 
 for pdir in sorted(glob.glob(os.path.join(d, "pmc_*"))):
     dbs = glob.glob(os.path.join(pdir, "*.db"))
@@ -70,17 +91,23 @@ os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
 with open(os.path.join(root, "profiles", "%s_rocprof_summary.json" % tag), "w") as f:
     json.dump(out, f, indent=1)
 # per-launch HBM traffic of the plain CC fold, read by bench.py for roofline.traffic
-plain = "k_fold<false, false, 1, false>"
+plain = "k_fold<false, false>"
 r = out["kernels"].get(plain, {})
 if "derived" in r and r["derived"].get("read_requests"):
+    import hashlib
+    with open(os.path.join(root, "gelly-streaming_amd", "lib", "libgs_summary.so"), "rb") as f:
+        lib_sha16 = hashlib.sha256(f.read()).hexdigest()[:16]
     dv = r["derived"]
     traffic = {
-        "round": tag, "workload": "rmat26-cc-stream", "batch": 1 << 20, "kernel": plain,
+        "round": tag, "workload": "rmat26-cc-stream", "batch": batch, "pipeline": pipeline, "lib_sha16": lib_sha16,
+        "kernel": plain, "read_requests_per_edge": round(dv["read_requests"] / batch, 3),
+        "k_fold_busy_ms_per_step": out["k_fold_busy_ms_per_step"],
         "avg_us_rocprof": r.get("avg_us"), "read_requests_per_launch": dv["read_requests"],
         "bytes_per_read_request": 128, "write_bytes_per_launch": dv["write_bytes"],
         "hbm_bytes_per_launch": dv["hbm_read_bytes"] + dv["write_bytes"],
         "fetch_size_kib_raw": r["pmc_FETCH_SIZE"], "l2_hit_rate": dv["l2_hit_rate"],
-        "method": "separate rocprofv3 --pmc passes (tools/rocprof_round.sh, --pipeline 1) over one bench step; "
+        "method": "separate rocprofv3 --pmc passes (tools/rocprof_round.sh, bench defaults: pipeline %d) over one "
+                  "bench step; " % pipeline +
                   "read bytes = TCC_EA0_RDREQ x 128 B: on gfx950 one L2->fabric read request moves 128 B both "
                   "for 16-B/lane streaming (256 MiB = 2.10 M requests) and for random 16-B loads (same request "
                   "ceiling), see profiles/r01_calib_random_pmc.json; FETCH_SIZE tallies 64 B per request "
