@@ -306,6 +306,8 @@ struct gs_group {
   // statistics
   uint64_t exchanges = 0, rows_received = 0, live_received = 0;
   bool hostprof = false;  // GS_GROUP_HOSTPROF=1: host seconds per phase, printed at destroy
+  bool no_lanes = false;  // GS_GROUP_LANES=0 (diagnostic): own folds on the handle stream
+  bool no_side = false;   // GS_GROUP_SIDE=0 (diagnostic): remote folds on the handle stream
   double hp[4] = {};      // own fold, stage + count collective, wait for counts, data collective + apply
   uint64_t hp_calls = 0;
 
@@ -360,7 +362,7 @@ int finish_data(gs_group* g, uint64_t e) {
   const int r = g->api->allGather(g->send[k], g->recv[k], rows * g->width, kNcclInt64, g->comm_d, g->xd);
   if (r != 0) return rccl_fail(g->api, "ncclAllGather(data)", r);
   GS_HIP(hipEventRecord(g->gathered[k], g->xd));
-  const bool use_side = side_ok(h);
+  const bool use_side = side_ok(h) && !g->no_side;
   hipStream_t s = use_side ? h->side : h->stream;
   if (g->nranks > 1 || g->self_apply) {
     GS_HIP(hipStreamWaitEvent(s, g->gathered[k], 0));
@@ -382,16 +384,15 @@ int finish_data(gs_group* g, uint64_t e) {
   return GS_OK;
 }
 
-// Communication streams at the device's highest priority: a stage or collective
-// kernel gets CUs as soon as fold workgroups retire instead of queueing behind the
-// next fold (measured: 2^22-edge exchanges at one rank 47.9 -> 44.7 ms/step together
-// with the lane pipeline below).
-hipError_t create_comm_stream(hipStream_t* st) {
-  int least = 0, greatest = 0;
-  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
-    return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
-  return hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest);
-}
+// Communication streams at NORMAL priority. Highest-priority comm streams overlapped
+// stages with folds slightly better (2^22-edge exchanges at one rank 47.9 -> 44.7
+// ms/step), but under real multi-queue concurrency (GPU_MAX_HW_QUEUES=32, 5-8
+// emulated ranks) they LOST work: in some own-fold launches every workgroup of one or
+// more XCDs (blocks b = c mod 8) left no trace -- no key CAS, no vertex-count add --
+// so every replica missed those edges' vertices (tools/emu_check.py; DESIGN.md
+// section 5). Normal-priority streams, or the remote folds serialised on the handle
+// stream, were exact in every run.
+hipError_t create_comm_stream(hipStream_t* st) { return hipStreamCreateWithFlags(st, hipStreamNonBlocking); }
 
 }  // namespace
 
@@ -427,6 +428,8 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   g->batch = batch_edges;
   if (const char* m = getenv("GS_GROUP_SELF_APPLY")) g->self_apply = atoi(m) != 0;
   if (const char* m = getenv("GS_GROUP_HOSTPROF")) g->hostprof = atoi(m) != 0;
+  if (const char* m = getenv("GS_GROUP_LANES")) g->no_lanes = atoi(m) == 0;
+  if (const char* m = getenv("GS_GROUP_SIDE")) g->no_side = atoi(m) == 0;
   auto bail = [&](int code) {
     gs_group_destroy(g);
     return code;
@@ -492,7 +495,7 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   // The own fold records into delta set d. The summary stream only waits for the
   // stage of exchange b - 2 (which emptied set d): stages, collectives and the
   // remote folds all run on other streams, so own folds go back to back.
-  const bool lanes = !h->profiling;  // (profiling serialises folds on the handle stream)
+  const bool lanes = !h->profiling && !g->no_lanes;  // (profiling serialises folds on the handle stream)
   if (lanes) {
     if (h->pipe_depth < 2) h->pipe_depth = 2;
     if (b == 0) {  // the lanes start behind the caller's earlier work (reset, previous folds)

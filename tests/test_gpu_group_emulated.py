@@ -182,3 +182,21 @@ def test_tree_combine_emulated_ranks(gs, oracle_mod, monkeypatch, kind, world):
         t = oracle_mod.bip_truth(hs, hd)
         assert ok == t[0] and ok
         assert np.array_equal(comp, t[1]) and np.array_equal(v, t[2]) and np.array_equal(sign, t[3])
+
+
+def test_eight_ranks_many_hw_queues_subprocess():
+    """8 emulated ranks with 32 hardware queues (real concurrency between the own
+    folds, the remote folds on the apply stream and the comm streams), 16 exchanges
+    per rank per pass, 2 passes with a reset between: every replica equals the oracle
+    after every pass. GPU_MAX_HW_QUEUES must be set before HIP starts, hence a child
+    process. Regression: with highest-priority comm streams one XCD's share of some
+    own-fold launches was lost here (gs_group.cpp create_comm_stream)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="32")
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "emu_check.py"), "--ranks", "8",
+                        "--log-batch", "17", "--passes", "2"], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0 and "all replicas equal the oracle" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
