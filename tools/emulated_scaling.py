@@ -99,7 +99,7 @@ def main():
         tn = min(max(times[r][k] for r in range(n)) for k in range(1, a.reps + 1))
         sent = sum(x["records_sent"] for x in recs)
         print("N=%d: %.2f ms for all ranks on one GPU, inflation %.2fx (efficiency bound %.2f); "
-              "exchanges/rank %d, records sent by all ranks %d (per pass %d), rows received by rank 0 %d; "
+              "exchanges/rank %d (all passes), records sent by all ranks in the last pass %d, rows received by rank 0 per pass %d; "
               "vertices %s"
               % (n, tn * 1e3, tn / t1, t1 / tn, recs[0]["exchanges"], sent, sent // (a.reps + 1),
                  recs[0]["rows_received"] // (a.reps + 1), sorted(set(nv))), flush=True)
