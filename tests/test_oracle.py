@@ -254,3 +254,29 @@ def test_bip_quirk_divergence_report(oracle_mod):
     rs = [ids[x] for x in s.tolist()]
     rd = [ids[x] for x in d.tolist()]
     assert not oracle_mod.bip_quirk_divergence(rs, rd)["diverges"]
+
+
+def test_oracle_under_address_and_undefined_sanitizers(tmp_path):
+    """the oracle built with -fsanitize=address,undefined (host code
+    only) and run over the pin vectors, windowed/partitioned dataflows, a growth
+    stream, the parity truth, the quirk Candidates and the text codec
+    (tests/cpp/oracle_sanitize.cpp). Any sanitizer report aborts the driver."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("g++ not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "oracle_san")
+    build = subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                            "-fno-sanitize-recover=all", "-fno-omit-frame-pointer",
+                            os.path.join(root, "oracle", "gs_oracle.cpp"),
+                            os.path.join(root, "tests", "cpp", "oracle_sanitize.cpp"), "-o", exe, "-pthread"],
+                           capture_output=True, text=True, timeout=300)
+    assert build.returncode == 0, build.stderr[-3000:]
+    # a preloaded library may precede the ASan runtime: do not treat that as an error
+    env = dict(os.environ, ASAN_OPTIONS="verify_asan_link_order=0:detect_leaks=1:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    run = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert run.returncode == 0, run.stdout[-2000:] + run.stderr[-4000:]
+    assert "all checks passed" in run.stdout
+    assert "runtime error" not in run.stderr and "AddressSanitizer" not in run.stderr, run.stderr[-4000:]
