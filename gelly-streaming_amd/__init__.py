@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "gs_group_destroy", "gs_group_tree_combine", "gs_combine_exported_device",
     "gs_group_fold_batches_device", "gs_export_labels_part_device",
     "gs_delta_capacity", "gs_find_labels_device", "gs_capacity_stats",
-    "gs_set_change_tracking", "gs_take_changes_device",
+    "gs_set_change_tracking", "gs_take_changes_device", "gs_take_changes",
 )
 
 
@@ -110,6 +110,7 @@ def lib():
     L.gs_capacity_stats.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double)]
     L.gs_set_change_tracking.argtypes = [_vp, ctypes.c_int]
     L.gs_take_changes_device.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.POINTER(_u64)]
+    L.gs_take_changes.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.POINTER(_u64)]
     L.gs_get_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
     L.gs_set_profiling.argtypes = [_vp, ctypes.c_int]
     L.gs_set_pipelining.argtypes = [_vp, ctypes.c_int]
@@ -317,6 +318,20 @@ class Summary:
         lab = torch.empty(m, dtype=torch.int64, device=dev)
         k = self.take_changes_device(v, lab)
         return v[:k].cpu().numpy(), lab[:k].cpu().numpy()
+
+    def take_changes_host(self, with_parity=False):
+        """gs_take_changes: the same rows into HOST arrays (what a JVM sink binds);
+        (v, label[, parity]) numpy arrays."""
+        import numpy as np
+        m = self.num_vertices() + 1
+        v = np.empty(m, dtype=np.int64)
+        lab = np.empty(m, dtype=np.int64)
+        par = np.empty(m, dtype=np.uint8) if with_parity else None
+        n = _u64()
+        _check(lib().gs_take_changes(self._h, v.ctypes.data, lab.ctypes.data,
+                                     par.ctypes.data if with_parity else None, int(m), ctypes.byref(n)))
+        k = n.value
+        return (v[:k], lab[:k], par[:k]) if with_parity else (v[:k], lab[:k])
 
     def delta_capacity(self):
         """Rows the delta list holds between two takes / stages (gs_delta_capacity)."""

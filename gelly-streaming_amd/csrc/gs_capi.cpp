@@ -562,7 +562,8 @@ int gs_destroy(gs_handle h) {
   if (h->h_stage) (void)hipHostFree(h->h_stage);
   if (h->h_wstage) (void)hipHostFree(h->h_wstage);
   for (void* p : {(void*)h->d_text, (void*)h->d_tsrc, (void*)h->d_tdst, h->d_tscratch, (void*)h->tab, (void*)h->ctr,
-                  (void*)h->vlist, (void*)h->drec, (void*)h->nxt, (void*)h->chg_scratch, (void*)h->d_stage,
+                  (void*)h->vlist, (void*)h->drec, (void*)h->nxt, (void*)h->chg_scratch, (void*)h->chg_ov,
+                  (void*)h->chg_ol, (void*)h->chg_op, (void*)h->d_stage,
                   (void*)h->d_wstage, (void*)h->d_scratch, (void*)h->x_v, (void*)h->x_l, (void*)h->x_p,
                   (void*)h->x_cnt})
     (void)hipFree(p);

@@ -170,4 +170,41 @@ int gs_take_changes_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* par
   return GS_OK;
 }
 
+// Host-array variant for JVM sinks: the rows are emitted into
+// grow-only device scratch of the handle, then copied out (synchronises).
+int gs_take_changes(gs_handle h, int64_t* v, int64_t* label, uint8_t* parity, size_t cap, uint64_t* n) {
+  if (!h) return fail(GS_ERR_INVALID, "null handle");
+  if (!n || (cap && (!v || !label))) return fail(GS_ERR_INVALID, "null argument");
+  if (!h->changes) return fail(GS_ERR_INVALID, "change tracking is off");
+  DeviceGuard g(h->device);
+  uint64_t nv = 0;
+  if (int rc = read_nv(h, &nv)) return rc;
+  *n = 0;
+  if (cap < nv) return fail(GS_ERR_INVALID, "cap below the vertex count: " + std::to_string(nv));
+  if (h->chg_ocap < nv + 1) {
+    (void)hipFree(h->chg_ov);
+    (void)hipFree(h->chg_ol);
+    (void)hipFree(h->chg_op);
+    h->chg_ov = h->chg_ol = nullptr;
+    h->chg_op = nullptr;
+    h->chg_ocap = 0;
+    const uint64_t rows = std::max<uint64_t>(nv + 1, 1024) * 5 / 4;  // headroom: fewer reallocations
+    GS_HIP(hipMalloc(&h->chg_ov, rows * 8));
+    GS_HIP(hipMalloc(&h->chg_ol, rows * 8));
+    GS_HIP(hipMalloc(&h->chg_op, rows));
+    h->chg_ocap = rows;
+  }
+  uint64_t k = 0;
+  if (int rc = gs_take_changes_device(h, h->chg_ov, h->chg_ol, parity ? h->chg_op : nullptr, h->chg_ocap, &k))
+    return rc;
+  if (k) {
+    GS_HIP(hipMemcpyAsync(v, h->chg_ov, k * 8, hipMemcpyDeviceToHost, h->stream));
+    GS_HIP(hipMemcpyAsync(label, h->chg_ol, k * 8, hipMemcpyDeviceToHost, h->stream));
+    if (parity) GS_HIP(hipMemcpyAsync(parity, h->chg_op, k, hipMemcpyDeviceToHost, h->stream));
+    GS_HIP(hipStreamSynchronize(h->stream));
+  }
+  *n = k;
+  return GS_OK;
+}
+
 }  // extern "C"

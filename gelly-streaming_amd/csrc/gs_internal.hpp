@@ -96,6 +96,10 @@ struct gs_summary {
   uint64_t nxt_slots = 0;
   unsigned long long* chg_scratch = nullptr;  // emission scratch: count, marks, big roots, staged records
   uint64_t chg_scratch_rows = 0;
+  int64_t* chg_ov = nullptr;  // gs_take_changes (host arrays): device rows before the copy
+  int64_t* chg_ol = nullptr;
+  uint8_t* chg_op = nullptr;
+  uint64_t chg_ocap = 0;
   bool chg_scan_all = false;  // the next emission emits every vertex (after a rebuild)
   // staging for host folds
   int64_t* d_stage = nullptr;  // [2][2][kStageChunk]

@@ -218,6 +218,9 @@ int gs_fold_exchange_device(gs_handle h, const int64_t* recv, const uint64_t* co
  * tracking on and consumes the delta records (not for a group's summary). */
 int gs_set_change_tracking(gs_handle h, int on);
 int gs_take_changes_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* parity, size_t cap, uint64_t* n);
+/* The same rows into HOST arrays (a JVM sink; parity may be
+ * NULL); device scratch is kept in the handle. */
+int gs_take_changes(gs_handle h, int64_t* v, int64_t* label, uint8_t* parity, size_t cap, uint64_t* n);
 
 /* ---- introspection -----------------------------------------------------------
  * The HIP stream (hipStream_t) the handle enqueues on, and per-kernel timing:

@@ -113,3 +113,21 @@ def test_changes_enabled_mid_stream(gs, oracle_mod):
         v, lab = x.take_changes()
         sink.update(zip(v.tolist(), lab.tolist()))
         assert sink == _oracle_state(oracle_mod, s, d)
+
+
+def test_changes_host_arrays_equal_device_take(gs, oracle_mod):
+    """gs_take_changes (host arrays, the JVM sink's entry point) emits exactly the rows
+    gs_take_changes_device does, window by window, on two identical summaries; parity
+    rows for the signed kind too."""
+    s, d = oracle_mod.rmat_edges(0x5EED0018, 13, 0, 1 << 15, True)
+    for kind in ("cc", "signed"):
+        with gs.Summary(kind, capacity_hint=1 << 14) as a, gs.Summary(kind, capacity_hint=1 << 14) as b:
+            a.set_change_tracking(True)
+            b.set_change_tracking(True)
+            for lo in range(0, len(s), 1 << 12):
+                a.fold(s[lo:lo + (1 << 12)], d[lo:lo + (1 << 12)])
+                b.fold(s[lo:lo + (1 << 12)], d[lo:lo + (1 << 12)])
+                va, la = a.take_changes()
+                vb, lb = b.take_changes_host()
+                ia, ib = np.argsort(va), np.argsort(vb)
+                assert np.array_equal(va[ia], vb[ib]) and np.array_equal(la[ia], lb[ib])
