@@ -83,6 +83,10 @@ def parse():
                    help="combine cadence: edges per rank (log2) between delta exchanges at N > 1 (or --exchange). "
                         "Every rank folds 2^20-edge micro-batches (SURVEY.md 8(d) config 3); the exchange runs every "
                         "4 of them by default because each exchange has a fixed host cost (DESIGN.md section 5)")
+    p.add_argument("--ramp-log2", type=int, default=22,
+                   help="the first 2^k edges per rank are exchanged every 2^ramp-log-batch edges (gs_group_set_ramp; "
+                        "0: no ramp): fewer duplicate hook records (DESIGN.md section 5)")
+    p.add_argument("--ramp-log-batch", type=int, default=20)
     p.add_argument("--capacity-log2", type=int, default=0,
                    help="relabel-table capacity hint of the CC summary (log2 vertices; 0: 2^scale)")
     p.add_argument("--exchange-impl", choices=["native", "torch"], default="native",
@@ -460,6 +464,7 @@ def main():
             uid = [gs.group_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             xch = NativeExchange(gs.Group(summ, uid[0], world, rank, B))
+            xch.g.set_ramp(1 << args.ramp_log2 if args.ramp_log2 else 0, 1 << args.ramp_log_batch)
         else:
             xch = DeltaExchangeFold(summ, B, dev)
 
@@ -578,6 +583,8 @@ def main():
             "config": {"workload": "rmat%d-cc-stream" % args.scale, "scale": args.scale,
                        "edges": E, "micro_batch": 1 << args.log_batch if not grouped else 1 << 20,
                        "combine_every_edges_per_gpu": 1 << args.exchange_log_batch,
+                       "combine_ramp": {"first_edges_per_gpu": 1 << args.ramp_log2 if args.ramp_log2 else 0,
+                                        "every": 1 << args.ramp_log_batch},
                        "combine": "delta exchange (native RCCL group)" if grouped else "none at 1 GPU (same cadence)",
                        "ids": "sparse 64-bit (scrambled)",
                        "capacity_hint": 1 << (args.capacity_log2 or xlog),

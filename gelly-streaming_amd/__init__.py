@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
     "gs_parse_edges_device", "gs_fold_text",
     "gs_group_unique_id", "gs_group_create", "gs_group_fold_device", "gs_group_finish", "gs_group_stats",
     "gs_group_destroy", "gs_group_tree_combine", "gs_combine_exported_device",
-    "gs_group_fold_batches_device", "gs_export_labels_part_device",
+    "gs_group_fold_batches_device", "gs_group_set_ramp", "gs_export_labels_part_device",
     "gs_delta_capacity", "gs_find_labels_device", "gs_capacity_stats",
     "gs_set_change_tracking", "gs_take_changes_device", "gs_take_changes",
 )
@@ -131,6 +131,7 @@ def lib():
     L.gs_group_destroy.argtypes = [_vp]
     L.gs_group_tree_combine.argtypes = [_vp]
     L.gs_group_fold_batches_device.argtypes = [_vp, _vp, _vp, _sz, _sz]
+    L.gs_group_set_ramp.argtypes = [_vp, _sz, _sz]
     L.gs_export_labels_part_device.argtypes = [_vp, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _sz,
                                                ctypes.POINTER(_sz)]
     L.gs_combine_exported_device.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.c_int]
@@ -443,6 +444,11 @@ class Group:
     def fold_batches(self, src, dst, n, batch):
         """ceil(n / batch) micro-batches of fold_device, looped in native code."""
         _check(lib().gs_group_fold_batches_device(self._g, _ptr(src), _ptr(dst), int(n), int(batch)))
+
+    def set_ramp(self, edges, batch=1 << 20):
+        """fold_batches exchanges the first `edges` own edges after create / finish every
+        `batch` edges (gs_group_set_ramp; 0 disables). Same on every rank."""
+        _check(lib().gs_group_set_ramp(self._g, int(edges), int(batch)))
 
     def finish(self):
         _check(lib().gs_group_finish(self._g))

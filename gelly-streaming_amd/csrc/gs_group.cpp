@@ -302,6 +302,8 @@ struct gs_group {
   uint64_t chunks = 0;                                  // own micro-batches launched (lane = chunks % 2)
   hipEvent_t counted[kLag] = {}, gathered[kLag] = {}, applied[kLag] = {};  // per buffer set
   uint64_t b = 0;       // exchanges since create / finish
+  uint64_t own_edges = 0;  // own edges folded since create / finish (the ramp's position)
+  uint64_t ramp_edges = 1ull << 22, ramp_batch = 1ull << 20;  // gs_group_set_ramp
   uint64_t done = 0;    // exchanges whose data half has been issued
   // statistics
   uint64_t exchanges = 0, rows_received = 0, live_received = 0;
@@ -487,6 +489,7 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   const uint64_t b = g->b;
   const int d = (int)(b & 1u), k = (int)(b % kLag);  // delta set, buffer set
   g->hp_calls++;
+  g->own_edges += n;
   // the data half of exchange b - kLag (its counts landed long ago): issued first, so
   // buffer set k is released (events recorded) before this exchange reuses it
   if (b >= (uint64_t)kLag)
@@ -557,8 +560,22 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
 int gs_group_fold_batches_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n, size_t batch) {
   if (!g) return fail(GS_ERR_INVALID, "null group");
   if (batch == 0) return fail(GS_ERR_INVALID, "batch is 0");
-  for (size_t off = 0; off < n; off += batch)
-    if (int rc = gs_group_fold_device(g, src + off, dst + off, std::min(batch, n - off))) return rc;
+  for (size_t off = 0; off < n;) {
+    size_t m = batch;
+    if (g->own_edges < g->ramp_edges && g->ramp_batch < m) m = g->ramp_batch;  // the ramp
+    m = std::min(m, n - off);
+    if (int rc = gs_group_fold_device(g, src + off, dst + off, m)) return rc;
+    off += m;
+  }
+  return GS_OK;
+}
+
+int gs_group_set_ramp(gs_group_t g, size_t ramp_edges, size_t ramp_batch) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  if (ramp_edges && (ramp_batch == 0 || ramp_batch > g->batch))
+    return fail(GS_ERR_INVALID, "ramp_batch must be in (0, batch_edges]");
+  g->ramp_edges = ramp_edges;
+  g->ramp_batch = ramp_edges ? ramp_batch : g->batch;
   return GS_OK;
 }
 
@@ -573,6 +590,7 @@ int gs_group_finish(gs_group_t g) {
   if (g->xd) GS_HIP(hipStreamSynchronize(g->xd));
   g->b = g->done = 0;
   g->chunks = 0;
+  g->own_edges = 0;
   if (g->hdr_host)
     for (int k = 0; k < kLag; ++k) __atomic_store_n(&g->hdr(k)[g->nranks], (long long)-1, __ATOMIC_RELEASE);
   return GS_OK;

@@ -134,3 +134,38 @@ def test_tree_only_group_single_rank(gs, oracle_mod):
         g.close()
     ov, olab = oracle_mod.cc_labels(s, d)
     assert np.array_equal(v, ov) and np.array_equal(lab, olab)
+
+
+def test_group_ramp_exchange_cadence(gs, oracle_mod, monkeypatch):
+    """gs_group_set_ramp: the first `ramp` edges after create / finish are exchanged
+    every `ramp_batch` edges, the rest every `batch` (a self-applying rank folds its
+    own rows back, so every exchange's rows are parsed); the ramp restarts after
+    finish, bad arguments are refused."""
+    import torch
+    monkeypatch.setenv("GS_GROUP_SELF_APPLY", "1")
+    n, B = 1 << 17, 1 << 14
+    src = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int64, device="cuda")
+    gs.gen_rmat(src, dst, 0, n, 15, 0x5EED0026, True)
+    torch.cuda.synchronize()
+    ov, olab = oracle_mod.cc_labels(src.cpu().numpy(), dst.cpu().numpy())
+    with gs.Summary("cc", capacity_hint=1 << 15) as s:
+        g = gs.Group(s, gs.group_unique_id(), 1, 0, B)
+        with pytest.raises(gs.GSError):
+            g.set_ramp(1 << 15, B * 2)  # ramp batch above batch_edges
+        g.set_ramp(1 << 15, 1 << 12)
+        for p in range(2):  # the ramp restarts after finish
+            s.reset()
+            g.fold_batches(src, dst, n, B)
+            g.finish()
+            st = g.stats()
+            # 2^15 edges in 2^12 exchanges (8), then 2^17 - 2^15 in 2^14 exchanges (6)
+            assert st["exchanges"] == (p + 1) * (8 + 6)
+            v, lab = s.labels()
+            assert np.array_equal(v, ov) and np.array_equal(lab, olab)
+        g.set_ramp(0)  # off: 2^17 / 2^14 exchanges
+        s.reset()
+        g.fold_batches(src, dst, n, B)
+        g.finish()
+        assert g.stats()["exchanges"] == 2 * 14 + 8
+        g.close()

@@ -35,6 +35,10 @@ def main():
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--hint-log2", type=int, default=0, help="capacity hint of the rank replicas (0: 2^scale)")
+    ap.add_argument("--ramp-log2", type=int, default=22,
+                    help="first 2^ramp-log2 edges per rank exchanged every --ramp-log-batch edges "
+                         "(gs_group_set_ramp; 0: no ramp)")
+    ap.add_argument("--ramp-log-batch", type=int, default=20)
     a = ap.parse_args()
     E, B = 16 << a.scale, 1 << a.log_batch
     src = torch.empty(E, dtype=torch.int64, device="cuda")
@@ -69,6 +73,7 @@ def main():
         def rank(r):
             try:
                 g = gs.Group(summ[r], uid, n, r, B)
+                g.set_ramp(1 << a.ramp_log2 if a.ramp_log2 else 0, 1 << a.ramp_log_batch)
                 for _ in range(a.reps + 1):
                     summ[r].reset()
                     summ[r].sync()
@@ -101,7 +106,7 @@ def main():
         print("N=%d: %.2f ms for all ranks on one GPU, inflation %.2fx (efficiency bound %.2f); "
               "exchanges/rank %d (all passes), records sent by all ranks in the last pass %d, rows received by rank 0 per pass %d; "
               "vertices %s"
-              % (n, tn * 1e3, tn / t1, t1 / tn, recs[0]["exchanges"], sent, sent // (a.reps + 1),
+              % (n, tn * 1e3, tn / t1, t1 / tn, recs[0]["exchanges"], sent,
                  recs[0]["rows_received"] // (a.reps + 1), sorted(set(nv))), flush=True)
     return 0
 
