@@ -297,6 +297,19 @@ int check(gs_handle h) {
 
 bool side_ok(const gs_summary* h) { return h->side && !h->profiling; }
 
+// Pipelining lanes are created on first use, only as many as used: every stream of a
+// process maps onto one of GPU_MAX_HW_QUEUES hardware queues (default 4), and two
+// streams on one queue run in submission order -- a kernel waiting on another
+// stream's event then blocks everything queued behind it on that queue.
+int ensure_lanes(gs_summary* h, int n) {
+  for (int i = 0; i < n && i < gs_summary::kLanes; ++i) {
+    if (h->lane[i]) continue;
+    GS_HIP(hipStreamCreateWithFlags(&h->lane[i], hipStreamNonBlocking));
+    GS_HIP(hipEventCreateWithFlags(&h->lane_ev[i], hipEventDisableTiming));
+  }
+  return GS_OK;
+}
+
 int join_lanes(gs_summary* h) {
   if (int rc = join_pipe_lanes(h)) return rc;
   if (h->side_dirty) {
@@ -460,7 +473,7 @@ int ensure_delta_list(gs_summary* h, uint64_t edges) {
     (void)hipFree(h->drec);
     h->drec = nullptr;
   }
-  GS_HIP(hipMalloc(&h->drec, 2 * (size_t)gs::kShards * per * 24));
+  GS_HIP(hipMalloc(&h->drec, (size_t)gs::kDeltaSets * gs::kShards * per * 24));
   h->delta_shard_cap = (uint32_t)per;
   h->delta_edges = edges;
   return GS_OK;
@@ -521,10 +534,6 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   for (int i = 0; i < 2; ++i)
     if (hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming) != hipSuccess)
       return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
-  for (int i = 0; i < gs_summary::kLanes; ++i)
-    if (hipStreamCreateWithFlags(&h->lane[i], hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&h->lane_ev[i], hipEventDisableTiming) != hipSuccess)
-      return bail(fail(GS_ERR_HIP, "lane stream creation failed"));
   if (hipEventCreateWithFlags(&h->main_ev, hipEventDisableTiming) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
   if (hipHostMalloc(&h->rep, gs_summary::kRepRing * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -590,7 +599,7 @@ int gs_reset(gs_handle h) {
   GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
   h->vlist_ok = true;
   reset_capacity_tracking(h, 0);
-  h->delta_fill_ub[0] = h->delta_fill_ub[1] = 0;
+  for (uint64_t& f : h->delta_fill_ub) f = 0;
   return GS_OK;
 }
 
@@ -904,8 +913,9 @@ int gs_set_delta_tracking(gs_handle h, int on) {
   if (int rc_ = join_lanes(h)) return rc_;
   if (on)
     if (int rc = ensure_delta_list(h, kMaxChunk)) return rc;
-  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, 2 * gs::kShards * gs::kCtrStride * 4, h->stream));
-  h->delta_fill_ub[0] = h->delta_fill_ub[1] = 0;
+  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0,
+                        (size_t)gs::kDeltaSets * gs::kShards * gs::kCtrStride * 4, h->stream));
+  for (uint64_t& f : h->delta_fill_ub) f = 0;
   h->dset = 0;
   h->track = on != 0;
   return GS_OK;
@@ -1117,6 +1127,7 @@ int gs_set_pipelining(gs_handle h, int depth) {
   if (depth < 1 || depth > gs_summary::kLanes) return fail(GS_ERR_INVALID, "pipelining depth must be 1..4");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
+  if (int rc_ = ensure_lanes(h, depth)) return rc_;
   h->pipe_depth = depth;
   h->lane_next = 0;
   return GS_OK;

@@ -39,10 +39,16 @@ constexpr uint32_t kFoldBS = 256;  // k_fold threads per block (one edge per thr
 constexpr int kShards = 64;        // sharded append counters (one 128-B line each)
 constexpr int kCtrStride = 32;     // u32 per counter line
 constexpr uint64_t kFailBit = 1ull << 62;  // exchange count word: the sender's verdict failed
+// Delta sets: tracked folds of a group's exchange b record into set b mod kDeltaSets, so
+// they wait only for the stage of exchange b - kDeltaSets (which emptied that set).
+#ifndef GS_DELTA_SETS
+#define GS_DELTA_SETS 4
+#endif
+constexpr int kDeltaSets = GS_DELTA_SETS;
 enum CounterBlock : int {
   CTR_NV = 0,                    // [kShards] new-vertex counts (= vertex-list fill per shard)
-  CTR_DELTA = kShards,           // [2][kShards] delta-record counts (two delta sets)
-  CTR_FAIL = 3 * kShards,        // sticky bipartiteness failure
+  CTR_DELTA = kShards,           // [kDeltaSets][kShards] delta-record counts
+  CTR_FAIL = (1 + kDeltaSets) * kShards,  // sticky bipartiteness failure
   CTR_ERR,                       // device-side error (table overflow)
   CTR_EXPORT,                    // export append counter
   CTR_OVF,                       // delta list overflow

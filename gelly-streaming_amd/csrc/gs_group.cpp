@@ -46,11 +46,18 @@ constexpr uint64_t kMaxGroupBatch = 1ull << 26;
 // counts have long landed (a stage waits ~20 us for its fold's event on another
 // queue, then the count collective and k_headers), so the host never blocks and its
 // per-exchange launch work overlaps the folds. kLag buffer sets rotate.
-constexpr int kLag = 3;
+#ifndef GS_GROUP_LAG
+#define GS_GROUP_LAG 3
+#endif
+constexpr int kLag = GS_GROUP_LAG;
 // Own folds are launched in micro-batches of 2^20 edges,
 // alternating over two pipelining lanes of the summary so that each launch's tail
 // overlaps the next one; every micro-batch of exchange b records into delta set b % 2.
 constexpr uint64_t kMicro = 1ull << 20;
+#ifndef GS_GROUP_LANES_N
+#define GS_GROUP_LANES_N 3
+#endif
+constexpr int kGroupLanes = GS_GROUP_LANES_N;  // own-fold lanes (chunk c runs on lane c mod kGroupLanes)
 
 struct RcclApi {
   void* lib = nullptr;
@@ -290,7 +297,7 @@ struct gs_group {
   bool exchange = false;         // false: tree-combine-only group
   bool self_apply = false;       // test knob (GS_GROUP_SELF_APPLY=1): also fold this rank's own rows back
   uint64_t batch = 0, rows_cap = 0;
-  // exchange b uses buffer set b % kLag (send, counts, headers, receive) and delta set b % 2
+  // exchange b uses buffer set b % kLag (send, counts, headers, receive) and delta set b % kDeltaSets
   int64_t* send[kLag] = {};                             // [rows_cap * width]
   int64_t* recv[kLag] = {};                             // [nranks * rows_cap * width]
   unsigned long long* cnt = nullptr;                    // device: [kLag] send counts, then [kLag][nranks] gathered
@@ -298,7 +305,7 @@ struct gs_group {
   long long* hdr_dev = nullptr;
   hipStream_t xc = nullptr, xd = nullptr, as = nullptr;  // counts, data, apply (the summary's side stream)
   hipEvent_t as_ev = nullptr;
-  hipEvent_t folded[2][2] = {}, staged[2] = {};         // per delta set (folded: per lane)
+  hipEvent_t folded[gs::kDeltaSets][kGroupLanes] = {}, staged[gs::kDeltaSets] = {};  // per delta set (folded: per lane)
   uint64_t chunks = 0;                                  // own micro-batches launched (lane = chunks % 2)
   hipEvent_t counted[kLag] = {}, gathered[kLag] = {}, applied[kLag] = {};  // per buffer set
   uint64_t b = 0;       // exchanges since create / finish
@@ -439,6 +446,7 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   if (g->exchange) {
     if (h->side) return bail(fail(GS_ERR_INVALID, "the summary already belongs to an exchange group"));
     if (int rc = join_lanes(h)) return bail(rc);
+    if (int rc = ensure_lanes(h, kGroupLanes)) return bail(rc);  // own folds rotate over the lanes
     if (int rc = ensure_delta_list(h, batch_edges)) return bail(rc);
     if (int rc = gs_set_delta_tracking(h, 1)) return bail(rc);
     g->rows_cap = (uint64_t)gs::kShards * h->delta_shard_cap;
@@ -449,10 +457,11 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
               create_comm_stream(&g->xc) == hipSuccess && create_comm_stream(&g->xd) == hipSuccess &&
               hipStreamCreateWithFlags(&g->as, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&g->as_ev, hipEventDisableTiming) == hipSuccess;
-    for (int k = 0; k < 2 && ok; ++k)
-      ok = hipEventCreateWithFlags(&g->folded[k][0], hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&g->folded[k][1], hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&g->staged[k], hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; k < gs::kDeltaSets && ok; ++k) {
+      for (int i = 0; i < kGroupLanes && ok; ++i)
+        ok = hipEventCreateWithFlags(&g->folded[k][i], hipEventDisableTiming) == hipSuccess;
+      ok = ok && hipEventCreateWithFlags(&g->staged[k], hipEventDisableTiming) == hipSuccess;
+    }
     for (int k = 0; k < kLag && ok; ++k)
       ok = hipMalloc(&g->send[k], g->rows_cap * g->width * 8) == hipSuccess &&
            hipMalloc(&g->recv[k], (size_t)nranks * g->rows_cap * g->width * 8) == hipSuccess &&
@@ -487,7 +496,7 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
   if (n > g->batch) return fail(GS_ERR_INVALID, "n above the group's batch_edges");
   const uint64_t b = g->b;
-  const int d = (int)(b & 1u), k = (int)(b % kLag);  // delta set, buffer set
+  const int d = (int)(b % gs::kDeltaSets), k = (int)(b % kLag);  // delta set, buffer set
   g->hp_calls++;
   g->own_edges += n;
   // the data half of exchange b - kLag (its counts landed long ago): issued first, so
@@ -496,27 +505,27 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
     if (int rc = finish_data(g, b - kLag)) return rc;
   HostTimer ht(g->hostprof ? &g->hp[0] : nullptr);
   // The own fold records into delta set d. The summary stream only waits for the
-  // stage of exchange b - 2 (which emptied set d): stages, collectives and the
+  // stage of exchange b - kDeltaSets (which emptied set d): stages, collectives and the
   // remote folds all run on other streams, so own folds go back to back.
   const bool lanes = !h->profiling && !g->no_lanes;  // (profiling serialises folds on the handle stream)
   if (lanes) {
-    if (h->pipe_depth < 2) h->pipe_depth = 2;
+    if (h->pipe_depth < kGroupLanes) h->pipe_depth = kGroupLanes;
     if (b == 0) {  // the lanes start behind the caller's earlier work (reset, previous folds)
       GS_HIP(hipEventRecord(h->main_ev, h->stream));
-      for (int i = 0; i < 2; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], h->main_ev, 0));
+      for (int i = 0; i < kGroupLanes; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], h->main_ev, 0));
     }
-    if (b >= 2)
-      for (int i = 0; i < 2; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], g->staged[d], 0));
-  } else if (b >= 2) {
+    if (b >= (uint64_t)gs::kDeltaSets)
+      for (int i = 0; i < kGroupLanes; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], g->staged[d], 0));
+  } else if (b >= (uint64_t)gs::kDeltaSets) {
     GS_HIP(hipStreamWaitEvent(h->stream, g->staged[d], 0));
   }
   h->dset = d;
   int frc = GS_OK;
-  bool used_lane[2] = {false, false};
+  bool used_lane[kGroupLanes] = {};
   for (size_t off = 0; off < n && !frc; off += kMicro) {
     FoldSource fs;
     if (lanes) {
-      fs.lane = (int)(g->chunks++ & 1u);
+      fs.lane = (int)(g->chunks++ % kGroupLanes);
       used_lane[fs.lane] = true;
     }
     frc = fold_device_impl(h, src + off, dst + off, nullptr, std::min<uint64_t>(kMicro, n - off), 1, 1,
@@ -526,12 +535,12 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   if (frc) return frc;
   // the stage waits for every micro-batch of this exchange (one event per lane used)
   int nev = 0;
-  hipEvent_t evs[2];
+  hipEvent_t evs[kGroupLanes];
   if (!lanes) {
     GS_HIP(hipEventRecord(g->folded[d][0], h->stream));
     evs[nev++] = g->folded[d][0];
   } else {
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < kGroupLanes; ++i)
       if (used_lane[i]) {
         GS_HIP(hipEventRecord(g->folded[d][i], h->lane[i]));
         evs[nev++] = g->folded[d][i];
@@ -750,9 +759,11 @@ int gs_group_destroy(gs_group_t g) {
     (void)hipStreamDestroy(g->as);
   }
   if (g->as_ev) (void)hipEventDestroy(g->as_ev);
-  for (int k = 0; k < 2; ++k)
-    for (hipEvent_t e : {g->folded[k][0], g->folded[k][1], g->staged[k]})
+  for (int k = 0; k < gs::kDeltaSets; ++k) {
+    for (hipEvent_t e : g->folded[k])
       if (e) (void)hipEventDestroy(e);
+    if (g->staged[k]) (void)hipEventDestroy(g->staged[k]);
+  }
   for (int k = 0; k < kLag; ++k) {
     for (hipEvent_t e : {g->counted[k], g->gathered[k], g->applied[k]})
       if (e) (void)hipEventDestroy(e);

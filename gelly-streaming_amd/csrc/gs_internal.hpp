@@ -85,11 +85,11 @@ struct gs_summary {
   // Two delta sets: a group's own fold b records into set b % 2 while the stage of
   // exchange b - 1 reads the other set on the communication stream.
   bool track = false;
-  int64_t* drec = nullptr;  // [2][kShards][delta_shard_cap][3]
+  int64_t* drec = nullptr;  // [kDeltaSets][kShards][delta_shard_cap][3]
   uint32_t delta_shard_cap = 0;
   uint64_t delta_edges = 0;  // fold edges one delta set holds between two stages
   int dset = 0;              // the set tracked folds record into
-  uint64_t delta_fill_ub[2] = {0, 0};  // worst-case per-shard fill of each set since its last stage
+  uint64_t delta_fill_ub[gs::kDeltaSets] = {};  // worst-case per-shard fill of each set since its last stage
   // change tracking (gs_changes.cpp)
   bool changes = false;
   uint32_t* nxt = nullptr;  // [cap + 1] circular member lists
@@ -196,6 +196,7 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
                      const FoldSource& fs = FoldSource());
 int join_lanes(gs_summary* h);
 bool side_ok(const gs_summary* h);
+int ensure_lanes(gs_summary* h, int n);  // create lane streams 0..n-1 on first use
 int read_nv(gs_summary* h, uint64_t* nv);
 int check_device_flags(gs_summary* h);
 int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n, int part = 0,
