@@ -323,14 +323,17 @@ int join_lanes(gs_summary* h) {
 // Error flags, read with ONE host synchronisation. Also refreshes whether the
 // vertex list is complete.
 int check_device_flags(gs_summary* h) {
+  // CTR_ERR .. CTR_VOVF are consecutive counter lines: one copy (each copy is a
+  // host round trip of its own: 3 copies cost ~10 us of a 2^16-edge window)
+  static_assert(gs::CTR_OVF == gs::CTR_ERR + 2 && gs::CTR_VOVF == gs::CTR_ERR + 3, "flag counters moved");
   uint32_t* f = h->h_flags;
-  GS_HIP(hipMemcpyAsync(&f[0], h->ctr + gs::ctr_index(gs::CTR_ERR), 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipMemcpyAsync(&f[1], h->ctr + gs::ctr_index(gs::CTR_OVF), 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipMemcpyAsync(&f[2], h->ctr + gs::ctr_index(gs::CTR_VOVF), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipMemcpyAsync(f, h->ctr + gs::ctr_index(gs::CTR_ERR), (3 * gs::kCtrStride + 1) * 4, hipMemcpyDeviceToHost,
+                        h->stream));
   GS_HIP(hipStreamSynchronize(h->stream));
-  if (f[2]) h->vlist_ok = false;
-  if (f[0]) return fail(GS_ERR_CAPACITY, "vertex table overflow (device probe limit)");
-  if (f[1]) return fail(GS_ERR_CAPACITY, "delta list overflow: stage or take the delta records after each fold");
+  const uint32_t err = f[0], ovf = f[2 * gs::kCtrStride], vovf = f[3 * gs::kCtrStride];
+  if (vovf) h->vlist_ok = false;
+  if (err) return fail(GS_ERR_CAPACITY, "vertex table overflow (device probe limit)");
+  if (ovf) return fail(GS_ERR_CAPACITY, "delta list overflow: stage or take the delta records after each fold");
   return GS_OK;
 }
 
@@ -356,6 +359,13 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
   // exchange buffer the caller's count of live rows it will fold. The valid rows may
   // sit in any chunk, so an exchange fold claims all its units with its last chunk.
   const uint64_t units = fs.rows ? fs.units : n;
+  if (track) {  // refuse before any capacity accounting: edges charged there must be folded
+    uint64_t fill = h->delta_fill_ub[h->dset];
+    for (size_t off = 0; off < n; off += kMaxChunk) fill += per_shard_edges(std::min<size_t>(kMaxChunk, n - off));
+    if (!h->drec || fill > h->delta_shard_cap)
+      return fail(GS_ERR_CAPACITY, "delta list full: stage or take the delta records after at most " +
+                                       std::to_string(h->delta_edges) + " folded edges");
+  }
   if (check_cap && units) {
     if (int rc = ensure_capacity(h, units)) return rc;
   }
@@ -373,12 +383,7 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
   for (size_t off = 0; off < n; off += kMaxChunk) {
     const uint32_t c = (uint32_t)std::min<size_t>(kMaxChunk, n - off);
     const uint32_t blocks = (c + gs::kFoldBS - 1) / gs::kFoldBS;
-    if (track) {
-      h->delta_fill_ub[h->dset] += per_shard_edges(c);
-      if (!h->drec || h->delta_fill_ub[h->dset] > h->delta_shard_cap)
-        return fail(GS_ERR_CAPACITY, "delta list full: stage or take the delta records after at most " +
-                                         std::to_string(h->delta_edges) + " folded edges");
-    }
+    if (track) h->delta_fill_ub[h->dset] += per_shard_edges(c);
     hipStream_t st = side ? h->side : h->stream;
     if (side) h->side_dirty = true;
     if (pipe) {  // the lane waits for the caller's work on the handle stream, not for the other lane
@@ -529,7 +534,7 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
     return bail(fail(GS_ERR_HIP, "hipMalloc(staging) failed"));
   if (hipHostMalloc(&h->h_stage, sizeof(int64_t) * 4 * kStageChunk, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&h->h_wstage, 2 * kStageChunk, hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&h->h_flags, 16, hipHostMallocDefault) != hipSuccess)
+      hipHostMalloc(&h->h_flags, (3 * gs::kCtrStride + 1) * 4, hipHostMallocDefault) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipHostMalloc(staging) failed"));
   for (int i = 0; i < 2; ++i)
     if (hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming) != hipSuccess)

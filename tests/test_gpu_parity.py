@@ -575,3 +575,40 @@ def test_capacity_sync_then_near_limit_fold_does_not_stall(gs, oracle_mod):
         # no wait may last the full 200 ms budget
         assert st["wait_ms"] < 150 * max(1, st["waits"]), st
         _assert_cc_equal(ds, oracle_mod, s.cpu().numpy(), d.cpu().numpy())
+
+
+def test_delta_list_full_error_leaves_capacity_tracking_intact(gs, oracle_mod):
+    """A tracked fold refused for a full delta list must not charge its edges to the
+    capacity bound (they are never folded, so no report would ever claim them and
+    every later capacity check would wait out its 200 ms timeout). Fold until the
+    list refuses, take, go on: no fold + sync may take anywhere near 200 ms, and the
+    labels equal the oracle."""
+    import time
+    import torch
+    n, B = 1 << 23, 1 << 18  # the delta list holds >= 2^22 folded edges (kMaxChunk)
+    src = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int64, device="cuda")
+    gs.gen_er(src, dst, 0, n, 17, 0x5EED00E5, True)
+    torch.cuda.synchronize()
+    with gs.Summary("cc", capacity_hint=1 << 17) as s:
+        s.set_delta_tracking(True)
+        cap = s.delta_capacity()
+        rec = torch.empty((cap, 3), dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        refused, worst, o = 0, 0.0, 0
+        while o < n:
+            t0 = time.perf_counter()
+            try:
+                s.fold_device(src[o:], dst[o:], n=B)
+                s.sync()
+                o += B
+            except gs.GSError:
+                refused += 1
+                s.take_delta_records(rec, cap, cnt)
+                s.sync()
+            worst = max(worst, time.perf_counter() - t0)
+        assert refused > 0, "the delta list never filled: the test does not exercise the refusal"
+        assert worst < 0.1, "a fold + sync took %.3f s (capacity wait)" % worst
+        v, lab = s.labels()
+    ov, olab = oracle_mod.cc_labels(src.cpu().numpy(), dst.cpu().numpy())
+    assert np.array_equal(v, ov) and np.array_equal(lab, olab)
