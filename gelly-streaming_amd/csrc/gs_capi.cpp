@@ -154,6 +154,7 @@ int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
   while ((1ull << h->logcap) < cap) ++h->logcap;
   GS_HIP(hipMalloc(&h->tab, (cap + 1) * sizeof(gs::Slot)));
   if (int rc = alloc_vlist(h)) return rc;
+  memset(h->h_flags, 0, 16);  // the device flags are cleared below (no kernel of the old table runs)
   if (keep_delta) {
     GS_HIP(hipMemsetAsync(h->ctr, 0, gs::ctr_index(gs::CTR_DELTA) * 4, h->stream));
     GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 0,
@@ -323,14 +324,14 @@ int join_lanes(gs_summary* h) {
 // Error flags, read with ONE host synchronisation. Also refreshes whether the
 // vertex list is complete.
 int check_device_flags(gs_summary* h) {
-  // CTR_ERR .. CTR_VOVF are consecutive counter lines: one copy (each copy is a
-  // host round trip of its own: 3 copies cost ~10 us of a 2^16-edge window)
-  static_assert(gs::CTR_OVF == gs::CTR_ERR + 2 && gs::CTR_VOVF == gs::CTR_ERR + 3, "flag counters moved");
-  uint32_t* f = h->h_flags;
-  GS_HIP(hipMemcpyAsync(f, h->ctr + gs::ctr_index(gs::CTR_ERR), (3 * gs::kCtrStride + 1) * 4, hipMemcpyDeviceToHost,
-                        h->stream));
+  // kernels mirror the rare flags into host-mapped memory (raise_flag): after the
+  // stream sync they are read with no device-to-host copy (each copy is a launch and
+  // a round trip of its own: the three per-flag copies cost ~10 us of a 2^16-edge
+  // window, config 5)
   GS_HIP(hipStreamSynchronize(h->stream));
-  const uint32_t err = f[0], ovf = f[2 * gs::kCtrStride], vovf = f[3 * gs::kCtrStride];
+  const uint32_t err = __atomic_load_n(&h->h_flags[0], __ATOMIC_ACQUIRE);
+  const uint32_t ovf = __atomic_load_n(&h->h_flags[1], __ATOMIC_ACQUIRE);
+  const uint32_t vovf = __atomic_load_n(&h->h_flags[2], __ATOMIC_ACQUIRE);
   if (vovf) h->vlist_ok = false;
   if (err) return fail(GS_ERR_CAPACITY, "vertex table overflow (device probe limit)");
   if (ovf) return fail(GS_ERR_CAPACITY, "delta list overflow: stage or take the delta records after each fold");
@@ -534,13 +535,15 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
     return bail(fail(GS_ERR_HIP, "hipMalloc(staging) failed"));
   if (hipHostMalloc(&h->h_stage, sizeof(int64_t) * 4 * kStageChunk, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&h->h_wstage, 2 * kStageChunk, hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&h->h_flags, (3 * gs::kCtrStride + 1) * 4, hipHostMallocDefault) != hipSuccess)
+      hipHostMalloc(&h->h_flags, 16, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hflags_dev), h->h_flags, 0) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipHostMalloc(staging) failed"));
   for (int i = 0; i < 2; ++i)
     if (hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming) != hipSuccess)
       return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
   if (hipEventCreateWithFlags(&h->main_ev, hipEventDisableTiming) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
+  memset(h->h_flags, 0, 16);
   if (hipHostMalloc(&h->rep, gs_summary::kRepRing * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&h->rep_dev), h->rep, 0) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "capacity report buffer allocation failed"));
@@ -602,6 +605,9 @@ int gs_reset(gs_handle h) {
   GS_HIP(hipGetLastError());
   if (int rc = change_tracking_reset(h, by_list ? 0 : 1)) return rc;
   GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
+  // host mirror: a flag a fold queued before this reset raises later is an error of
+  // that fold's epoch and surfaces at the next check
+  memset(h->h_flags, 0, 16);
   h->vlist_ok = true;
   reset_capacity_tracking(h, 0);
   for (uint64_t& f : h->delta_fill_ub) f = 0;

@@ -90,7 +90,16 @@ struct Table {
   uint32_t* vlist;     // vertex list [kShards][vshard_cap] (dense ids), or null
   uint32_t vshard_cap;
   int mark_new;        // change tracking: fresh inserts set kAuxNew
+  uint32_t* hflags;    // host-mapped mirror of the rare flags: [0] CTR_ERR, [1] CTR_OVF, [2] CTR_VOVF
 };
+
+// Raise a rare flag: the device counter (read by later kernels) and its host-mapped
+// mirror, so the host checks flags after a stream sync without a device-to-host copy.
+__device__ __forceinline__ void raise_flag(const Table& t, int ctr_id, int mirror) {
+  atomicOr(&t.ctr[ctr_index(ctr_id)], 1u);
+  // a flag only goes 0 -> 1: a system-scope store (as k_report's), no PCIe atomic needed
+  if (t.hflags) __hip_atomic_store(t.hflags + mirror, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 struct Delta {
   int64_t* drec;       // records {a, b, parity} of one delta set [kShards][shard_cap][3], or null
@@ -166,7 +175,7 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
     h = (h + 1) & t.mask;
     load_slot(t.tab + h, k, l);
   }
-  atomicOr(&t.ctr[ctr_index(CTR_ERR)], 1u);
+  raise_flag(t, CTR_ERR, 0);
   return kNoSlot;
 }
 
@@ -206,7 +215,7 @@ __device__ __forceinline__ void note_new_vertices(const Table& t, int shard, boo
   const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], k);
   if (!t.vlist) return;
   if (pos + k > t.vshard_cap) {
-    atomicOr(&t.ctr[ctr_index(CTR_VOVF)], 1u);
+    raise_flag(t, CTR_VOVF, 2);
     return;
   }
   uint32_t* vl = t.vlist + (size_t)shard * t.vshard_cap + pos;
@@ -340,7 +349,7 @@ __device__ __forceinline__ void append_record(const Table& t, const Delta& D, in
     r[1] = b;
     r[2] = w;
   } else {
-    atomicOr(&t.ctr[ctr_index(CTR_OVF)], 1u);
+    raise_flag(t, CTR_OVF, 1);
   }
 }
 

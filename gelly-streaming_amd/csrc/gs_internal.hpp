@@ -62,7 +62,8 @@ struct gs_summary {
   uint32_t vshard_cap = 0;
   uint32_t shard0 = 0;        // first shard of the next fold launch (rotates)
   bool vlist_ok = true;       // false once a shard of the vertex list overflowed (until reset)
-  uint32_t* h_flags = nullptr;  // pinned: error / overflow flags
+  uint32_t* h_flags = nullptr;     // host-mapped mirror of CTR_ERR / CTR_OVF / CTR_VOVF (raise_flag)
+  uint32_t* hflags_dev = nullptr;  // its device address
   // capacity tracking: a host upper bound of the vertex count, refreshed without
   // host synchronisation from k_report words (ring in host-coherent memory)
   uint64_t nv_ub = 0;
@@ -164,6 +165,7 @@ struct gs_summary {
     t.vlist = vlist;
     t.vshard_cap = vshard_cap;
     t.mark_new = changes ? 1 : 0;
+    t.hflags = hflags_dev;
     return t;
   }
   gs::Delta delta(int set = -1) const {
