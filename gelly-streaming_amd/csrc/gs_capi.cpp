@@ -250,21 +250,31 @@ int ensure_capacity(gs_summary* h, size_t n) {
     h->e_launched += n;
     return GS_OK;
   }
-  // wait for reports of the folds in flight (the GPU keeps working: no drain)
-  h->cap_waits++;
-  const auto t0 = std::chrono::steady_clock::now();
-  while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200)) {
-    b = capacity_bound(h, &all);
-    if ((double)(b + 2 * (uint64_t)n) <= limit) {
-      h->cap_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      h->nv_ub = b + 2 * (uint64_t)n;
-      h->e_launched += n;
-      return GS_OK;
+  // A table (below kSlackGrowMaxCap) too small to hold even the pipeline's slack --
+  // pipe_depth + 1 folds of n edges in flight on top of the vertices known exactly --
+  // goes straight to the synchronous path and is sized for that slack once. Waiting
+  // for reports below is then only back-pressure with enough folds queued to keep the
+  // GPU busy, instead of a drain before every fold (RMAT-20, config 2: 1.07 -> 0.72
+  // ms/step).
+  const uint64_t slack = 2ull * n * (uint64_t)(std::max(1, h->pipe_depth) + 1);
+  const bool slack_grow = h->cap < kSlackGrowMaxCap && (double)(h->nv_exact + slack) > limit;
+  if (!slack_grow) {
+    // wait for reports of the folds in flight (the GPU keeps working: no drain)
+    h->cap_waits++;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200)) {
+      b = capacity_bound(h, &all);
+      if ((double)(b + 2 * (uint64_t)n) <= limit) {
+        h->cap_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        h->nv_ub = b + 2 * (uint64_t)n;
+        h->e_launched += n;
+        return GS_OK;
+      }
+      if (all) break;
+      std::this_thread::yield();
     }
-    if (all) break;
-    std::this_thread::yield();
+    h->cap_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
-  h->cap_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   uint64_t nv = 0;
   h->cap_syncs++;
   int rc = read_nv(h, &nv);  // exact (joins every stream: every issued report has landed)
@@ -278,12 +288,17 @@ int ensure_capacity(gs_summary* h, size_t n) {
   for (int i = 0; i < gs_summary::kRepStreams; ++i) h->rep_skip[i] = 0, h->rep_pending[i] = 0;
   memset(h->rep, 0, gs_summary::kRepRing * 8);  // every report of this epoch has landed
   h->nv_ub = nv + 2 * (uint64_t)n;
-  if ((double)h->nv_ub > limit) {
+  uint64_t need = h->nv_ub;
+  if (slack_grow) need = std::max<uint64_t>(need, nv + slack);
+  if ((double)need > limit) {
     uint64_t nc = h->cap;
-    while (kMaxLoad * (double)nc < (double)h->nv_ub) nc <<= 1;
-    rc = grow(h, nc);  // resets the tracking to the rebuilt table's exact count
-    if (rc) return rc;
-    h->nv_ub = h->nv_exact + 2 * (uint64_t)n;
+    while (kMaxLoad * (double)nc < (double)h->nv_ub) nc <<= 1;  // what this fold needs
+    while (slack_grow && kMaxLoad * (double)nc < (double)need && nc < kSlackGrowMaxCap) nc <<= 1;  // + slack
+    if (nc > h->cap) {
+      rc = grow(h, nc);  // resets the tracking to the rebuilt table's exact count
+      if (rc) return rc;
+      h->nv_ub = h->nv_exact + 2 * (uint64_t)n;
+    }
   }
   h->e_launched += n;
   return GS_OK;

@@ -26,6 +26,11 @@ constexpr uint32_t kMaxChunk = 1u << 22;     // edges per k_fold launch
 constexpr uint32_t kStageChunk = 1u << 20;   // edges per pinned staging buffer
 constexpr double kMaxLoad = 0.70;            // grow the table past this load factor
 constexpr uint64_t kMaxCap = 1ull << 30;     // link holds slot << 1 in 32 bits
+// A table whose load limit is crossed by pipeline slack alone (the capacity bound
+// charges 2 new vertices per in-flight edge) grows once instead of waiting for
+// capacity reports on every fold -- up to this many slots (1 GiB); tables keep
+// their capacity across resets.
+constexpr uint64_t kSlackGrowMaxCap = 1ull << 26;
 
 enum { KID_FOLD = 0, KID_STAGE = 1, KID_EXPORT = 2, KID_INIT = 3, KID_N = 4 };
 
