@@ -550,6 +550,10 @@ def main():
                 "stage_avg_us": round(stage_ms * 1e3 / max(ns, 1), 2), "stage_launches": int(ns),
                 "export_ms": round(exp_ms, 3)}
         roof.update(extra)
+        if traffic and not grouped:  # measured HBM bytes (PMC, per launch) over the pipelined step
+            tgbs = traffic * nf / (elapsed / args.steps) / 1e9
+            roof["traffic_gbs_step"] = round(tgbs, 1)
+            roof["traffic_frac_step"] = round(tgbs / HBM_PEAK_GBS, 4)
         if grouped:
             roof["note"] = ("exchange path: fold launches include the other ranks' gathered rows (side stream); "
                             "achieved assumes 2^20 own edges per launch")

@@ -125,8 +125,10 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
   }
   const uint32_t wi = (valid && a.w) ? a.w[(size_t)i * a.w_stride] : 1u;
   if (wi & 0x80u) valid = false;
-  const int64_t ks = valid ? a.src[(size_t)i * a.stride] : 0;
-  const int64_t kd = valid ? a.dst[(size_t)i * a.stride] : 0;
+  // the edge stream is read once: non-temporal loads leave the L2 to table lines
+  // (RMAT-26: 40.37 -> 40.10 ms/step, 1.945 -> 1.941 fabric requests per edge)
+  const int64_t ks = valid ? __builtin_nontemporal_load(a.src + (size_t)i * a.stride) : 0;
+  const int64_t kd = valid ? __builtin_nontemporal_load(a.dst + (size_t)i * a.stride) : 0;
   uint32_t need = SIGNED ? (wi & 1u) : 0u;
   // both first relabel probes in flight together
   const uint32_t hu = hash_slot(ks, t.shift), hv = hash_slot(kd, t.shift);
@@ -260,7 +262,7 @@ __device__ __forceinline__ void export_one(const Table& t, uint32_t s, int64_t* 
   const int64_t v = settle_key(t, s, k);
   int64_t kx = v;
   find_ro(t, s, l, kx, acc);
-  if (pos < cap_out) {
+  if (pos < cap_out) {  // (non-temporal stores here measured no different: 0.82 ms either way)
     ov[pos] = v;
     ol[pos] = kx;
     if (op) op[pos] = (uint8_t)acc;
