@@ -72,8 +72,8 @@ int main(int argc, char** argv) {
     std::fclose(f);
   }
   std::printf("{\"edges\": %llu, \"seconds\": %.6f, \"edges_per_s\": %.1f, \"windows\": %zu, \"partitions\": %d, "
-              "\"vertices\": %llu, \"handles_created\": %zu, \"handles_reused\": %zu}\n",
+              "\"vertices\": %llu, \"handles_created\": %zu, \"handles_reused\": %zu, \"flush_seconds\": %.6f, \"fold_loop_seconds\": %.6f, \"combine_merger_seconds\": %.6f}\n",
               (unsigned long long)E, secs, (double)E / secs, windows, p, (unsigned long long)nv,
-              HandlePool::instance().created(), HandlePool::instance().reused());
+              HandlePool::instance().created(), HandlePool::instance().reused(), GpuSummary::flush_seconds(), cc.run_seconds()[0], cc.run_seconds()[1]);
   return 0;
 }

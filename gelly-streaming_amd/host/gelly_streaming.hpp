@@ -23,9 +23,11 @@
 #pragma once
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 #include <functional>
+#include <limits>
 #include <map>
 #include <memory>
 #include <optional>
@@ -138,8 +140,6 @@ class GpuSummary {
   GpuSummary(int kind, int device, uint64_t capacity_hint, size_t flush_edges)
       : kind_(kind), device_(device), hint_(capacity_hint), flush_edges_(flush_edges) {
     h_ = HandlePool::instance().acquire(kind, device, capacity_hint);
-    src_.reserve(std::min<size_t>(flush_edges_, 1 << 16));
-    dst_.reserve(std::min<size_t>(flush_edges_, 1 << 16));
   }
   virtual ~GpuSummary() {
     if (h_) HandlePool::instance().release(h_, kind_, device_, hint_);
@@ -147,17 +147,28 @@ class GpuSummary {
   GpuSummary(const GpuSummary&) = delete;
   GpuSummary& operator=(const GpuSummary&) = delete;
 
-  // push one buffered edge (flushes a full micro-batch)
+  // push one buffered edge (flushes a full micro-batch); the buffers are sized for
+  // a whole micro-batch on first use, so the per-edge path is two stores and a compare
   void push(int64_t u, int64_t v) {
-    src_.push_back(u);
-    dst_.push_back(v);
-    if (src_.size() >= flush_edges_) flush();
+    if (!src_) {
+      src_.reset(new int64_t[flush_edges_]);
+      dst_.reset(new int64_t[flush_edges_]);
+    }
+    src_[n_] = u;
+    dst_[n_] = v;
+    if (++n_ == flush_edges_) flush();
   }
   void flush() {
-    if (src_.empty()) return;
-    gs_check(gs_fold(h_, src_.data(), dst_.data(), src_.size()));
-    src_.clear();
-    dst_.clear();
+    if (n_ == 0) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    gs_check(gs_fold(h_, src_.get(), dst_.get(), n_));
+    flush_seconds() += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    n_ = 0;
+  }
+  // host seconds spent in gs_fold (micro-batch flushes), process-wide (dropin_bench)
+  static double& flush_seconds() {
+    static double s = 0;
+    return s;
   }
   gs_handle handle() {
     flush();
@@ -169,8 +180,7 @@ class GpuSummary {
     return (size_t)n;
   }
   void reset() {
-    src_.clear();
-    dst_.clear();
+    n_ = 0;
     gs_check(gs_reset(h_));
   }
   // all (vertex, canonical label, parity) rows, sorted by vertex
@@ -207,8 +217,7 @@ class GpuSummary {
     return buf;
   }
   void deserialize(const std::vector<uint8_t>& buf) {
-    src_.clear();
-    dst_.clear();
+    n_ = 0;
     gs_check(gs_deserialize(h_, buf.data(), buf.size()));
   }
   int device() const { return device_; }
@@ -219,7 +228,8 @@ class GpuSummary {
   uint64_t hint_;
   size_t flush_edges_;
   gs_handle h_ = nullptr;
-  std::vector<int64_t> src_, dst_;
+  std::unique_ptr<int64_t[]> src_, dst_;  // [flush_edges_] each, allocated on first push
+  size_t n_ = 0;                          // buffered edges
 };
 
 // DisjointSet<Long> (DisjointSet.java:25-151) over the GPU forest. find() returns
@@ -439,10 +449,19 @@ class SummaryBulkAggregation : public SummaryAggregation<K, EV, S, T> {
     while (i < n) {
       const int64_t w = window_of(stream, i);
       size_t j = i;
-      while (j < n && window_of(stream, j) == w) ++j;
+      if (stream.timestamps.empty() || timeMillis_ <= 0) {
+        j = n;  // one window
+      } else {  // the edges with ts / timeMillis_ == w: compared against the window's
+                // bounds, not divided one by one (a 64-bit division per edge was ~5 ns)
+        int64_t lo, hi;
+        window_bounds(w, &lo, &hi);
+        const int64_t* ts = stream.timestamps.data();
+        while (j < n && ts[j] >= lo && ts[j] <= hi) ++j;
+      }
       std::vector<S> partial(p);  // per-(partition, window) fold state
-      for (size_t k = i; k < j; ++k) {
-        const int part = (int)(k % (size_t)p);  // PartitionMapper.map (:103-105)
+      const auto tf = std::chrono::steady_clock::now();
+      int part = (int)(i % (size_t)p);  // PartitionMapper.map (:103-105): edge k -> k mod p
+      for (size_t k = i; k < j; ++k, part = (part + 1 == p) ? 0 : part + 1) {
         if (!partial[part]) partial[part] = this->getInitialValue();
         const Edge<K, EV>& e = stream.edges[k];
         // the accumulator is handed over and returned (Java passes the reference):
@@ -450,6 +469,7 @@ class SummaryBulkAggregation : public SummaryAggregation<K, EV, S, T> {
         partial[part] =
             this->updateFun_->foldEdges(std::move(partial[part]), e.getSource(), e.getTarget(), e.getValue());
       }
+      const auto tc = std::chrono::steady_clock::now();
       S acc{};
       for (int q = 0; q < p; ++q) {  // timeWindowAll reduce, arrival order = partition order
         if (!partial[q]) continue;
@@ -457,8 +477,15 @@ class SummaryBulkAggregation : public SummaryAggregation<K, EV, S, T> {
       }
       S emitted = merger.flatMap(acc);
       sink(emit(emitted));
+      run_seconds()[0] += std::chrono::duration<double>(tc - tf).count();
+      run_seconds()[1] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tc).count();
       i = j;
     }
+  }
+  // host seconds in run(): [0] per-edge folds (incl. flushes), [1] reduce + Merger + sink
+  static double* run_seconds() {
+    static double t[2] = {0, 0};
+    return t;
   }
   // Convenience: collect the emissions (references to live summaries; read them
   // before the next window mutates the running summary, or use the sink form).
@@ -472,6 +499,22 @@ class SummaryBulkAggregation : public SummaryAggregation<K, EV, S, T> {
   int64_t window_of(const EdgeStream<K, EV>& s, size_t i) const {
     const int64_t ts = s.timestamps.empty() ? 0 : s.timestamps[i];
     return timeMillis_ > 0 ? ts / timeMillis_ : 0;
+  }
+  // [lo, hi]: every ts with ts / timeMillis_ == w (C++ truncating division), saturated
+  void window_bounds(int64_t w, int64_t* lo, int64_t* hi) const {
+    const int64_t tm = timeMillis_;
+    const int64_t base = w * tm;  // |base| <= |ts| of an existing edge: no overflow
+    const int64_t kMax = std::numeric_limits<int64_t>::max(), kMin = std::numeric_limits<int64_t>::min();
+    if (w > 0) {
+      *lo = base;
+      *hi = base > kMax - (tm - 1) ? kMax : base + (tm - 1);
+    } else if (w < 0) {
+      *lo = base < kMin + (tm - 1) ? kMin : base - (tm - 1);
+      *hi = base;
+    } else {
+      *lo = -(tm - 1);
+      *hi = tm - 1;
+    }
   }
   T emit(S s) {
     if constexpr (std::is_same<S, T>::value) {
