@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <set>
+#include <limits>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -71,6 +72,22 @@ static void connected_components_test_parallel_windows() {
   CHECK("ConnectedComponentsTest.parallel", parser(values) == std::vector<std::string>({"1, 2, 3, 5", "6, 7", "8, 9"}),
         values.back());
   std::printf("PASS ConnectedComponentsTest.parallel\n");
+}
+
+static void windows_with_negative_and_extreme_timestamps() {
+  // window = ts / timeMillis (truncating, as window_of): -5,-4 -> -2; -3 -> -1;
+  // -1,0,1 -> 0; 2 -> 1; 4 -> 2; 2^63-2, 2^63-1 -> 2^62-1: six windows, six emissions
+  auto s = stream_of({{1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {6, 7}, {7, 8}, {8, 9}, {9, 10}, {10, 11}});
+  const int64_t mx = std::numeric_limits<int64_t>::max();
+  s.timestamps = {-5, -4, -3, -1, 0, 1, 2, 4, mx - 1, mx};
+  SimpleEdgeStream<int64_t, NullValue> graph(s);
+  ConnectedComponents<NullValue> cc(2);
+  std::vector<std::string> values;
+  graph.aggregate(cc, [&](const DisjointSetRef& ds) { values.push_back(ds->toString()); });
+  CHECK("windows.negative_extreme", values.size() == 6, std::to_string(values.size()));
+  CHECK("windows.negative_extreme", parser(values) == std::vector<std::string>({"1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11"}),
+        values.back());
+  std::printf("PASS windows.negative_extreme\n");
 }
 
 static void bipartite_test() {
@@ -137,6 +154,7 @@ static void merger_checkpoint_test() {
 int main() {
   connected_components_test();
   connected_components_test_parallel_windows();
+  windows_with_negative_and_extreme_timestamps();
   bipartite_test();
   non_bipartite_test();
   disjoint_set_tests();
