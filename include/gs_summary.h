@@ -74,7 +74,9 @@ int gs_reset(gs_handle h);
  * candidates.merge(edgeToCandidate(u, v)) (BipartitenessCheck.java:54-61,93-95),
  * called once per buffered micro-batch instead of once per edge.
  * New endpoints are added (DisjointSet.makeSet :53-56); a self-loop adds its vertex
- * and never fails the bipartiteness verdict (BipartitenessCheck.java:58-59). */
+ * and never fails the bipartiteness verdict (BipartitenessCheck.java:58-59).
+ * src/dst may be pageable or pinned; the fold itself is asynchronous, but the edges
+ * have been copied to the device when the call returns, so the caller may reuse them. */
 int gs_fold(gs_handle h, const int64_t* src, const int64_t* dst, size_t n);
 
 /* Same, from DEVICE memory already resident on the handle's device. Element i is
