@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "gs_last_error", "gs_version", "gs_create", "gs_destroy", "gs_reset", "gs_fold", "gs_fold_device",
     "gs_combine", "gs_sync", "gs_num_vertices", "gs_find", "gs_export_labels", "gs_export_labels_device",
     "gs_bip_status", "gs_export_colouring", "gs_serialize", "gs_deserialize", "gs_set_delta_tracking",
-    "gs_take_delta_records", "gs_delta_stage", "gs_fold_records_device", "gs_fold_exchange_device",
+    "gs_take_delta_records", "gs_fold_take_device", "gs_delta_stage", "gs_fold_records_device", "gs_fold_exchange_device",
     "gs_get_stream", "gs_set_pipelining", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity", "gs_counters",
     "gs_gen_rmat", "gs_gen_er", "gs_gen_bip",
     "gs_parse_edges_device", "gs_fold_text",
@@ -102,6 +102,7 @@ def lib():
     L.gs_deserialize.argtypes = [_vp, _vp, _sz]
     L.gs_set_delta_tracking.argtypes = [_vp, ctypes.c_int]
     L.gs_take_delta_records.argtypes = [_vp, _vp, _sz, _vp]
+    L.gs_fold_take_device.argtypes = [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp]
     L.gs_fold_records_device.argtypes = [_vp, _vp, _sz, ctypes.c_int]
     L.gs_delta_stage.argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
     L.gs_fold_exchange_device.argtypes = [_vp, _vp, _vp, _sz, _sz, ctypes.c_int, ctypes.c_int]
@@ -344,6 +345,16 @@ class Summary:
         """Pack the delta since the last take into `rec` (device int64 [cap, 3]) and
         its record count into `count` (device int64 [1]); asynchronous on self.stream."""
         _check(lib().gs_take_delta_records(self._h, _ptr(rec), int(cap), _ptr(count)))
+
+    def fold_take(self, src, dst, n, rec, cap, count):
+        """One latency-path window (gs_fold_take_device): fold n device edges (tracked),
+        take the records since the previous take into `rec` (device int64 [cap, 3]) and
+        their count into `count` (device int64 [1]); returns the count once the window
+        is complete."""
+        c = _u64()
+        _check(lib().gs_fold_take_device(self._h, _ptr(src), _ptr(dst), int(n), _ptr(rec), int(cap), _ptr(count),
+                                         ctypes.byref(c)))
+        return c.value
 
     def delta_stage(self, send, cap, count, width=3):
         """Stage every pending record into `send` (device int64 [cap, width]) and the

@@ -241,6 +241,20 @@ uint64_t capacity_bound(gs_summary* h, bool* all_reported) {
   return best;
 }
 
+// An exact vertex count read after every stream was joined and every queued fold
+// (and report) completed.
+void note_exact_count(gs_summary* h, uint64_t nv) {
+  h->nv_exact = nv;
+  h->e_exact = h->e_launched;
+  // edges queued since their stream's last report are complete and counted in nv, but
+  // no report will claim them: keep them out of later reports' "behind" (ADVICE r1)
+  h->e_lost += h->rep_pending_edges;
+  h->rep_pending_edges = 0;
+  for (int i = 0; i < gs_summary::kRepStreams; ++i) h->rep_skip[i] = 0, h->rep_pending[i] = 0;
+  memset(h->rep, 0, gs_summary::kRepRing * 8);  // every report of this epoch has landed
+  h->nv_ub = nv;
+}
+
 int ensure_capacity(gs_summary* h, size_t n) {
   const double limit = kMaxLoad * (double)h->cap;
   bool all = false;
@@ -279,14 +293,7 @@ int ensure_capacity(gs_summary* h, size_t n) {
   h->cap_syncs++;
   int rc = read_nv(h, &nv);  // exact (joins every stream: every issued report has landed)
   if (rc) return rc;
-  h->nv_exact = nv;
-  h->e_exact = h->e_launched;
-  // edges queued since their stream's last report are complete and counted in nv, but
-  // no report will claim them: keep them out of later reports' "behind" (ADVICE r1)
-  h->e_lost += h->rep_pending_edges;
-  h->rep_pending_edges = 0;
-  for (int i = 0; i < gs_summary::kRepStreams; ++i) h->rep_skip[i] = 0, h->rep_pending[i] = 0;
-  memset(h->rep, 0, gs_summary::kRepRing * 8);  // every report of this epoch has landed
+  note_exact_count(h, nv);
   h->nv_ub = nv + 2 * (uint64_t)n;
   uint64_t need = h->nv_ub;
   if (slack_grow) need = std::max<uint64_t>(need, nv + slack);
@@ -336,14 +343,47 @@ int join_lanes(gs_summary* h) {
   return GS_OK;
 }
 
+// Host wait for h->stream: k_signal queued behind everything, then a spin on its
+// host-mapped word (6.5 vs 12.2 us for hipStreamSynchronize after a short kernel,
+// tools/calib_launch.hip). A wait that outlasts kSpinWait (a long fold queue) hands
+// over to hipStreamSynchronize, which also surfaces asynchronous HIP errors.
+int wait_stream(gs_summary* h, const uint32_t* vals, uint64_t* value, int nvals, int stride) {
+  if (!vals && hipStreamQuery(h->stream) == hipSuccess) return GS_OK;  // already idle (0.6 us, no launch)
+  const unsigned long long seq = ++h->done_seq;
+  gs::launch_signal(h->done_dev, seq, vals, nvals, stride, h->stream);
+  GS_HIP(hipGetLastError());
+  if (int rc = wait_done(h, seq)) return rc;
+  if (value) *value = __atomic_load_n(h->h_done + 1, __ATOMIC_ACQUIRE);
+  return GS_OK;
+}
+
+// Spin until the completion word reaches seq (its writer is queued on h->stream).
+int wait_done(gs_summary* h, unsigned long long seq) {
+  constexpr auto kSpinWait = std::chrono::milliseconds(20);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1;; ++i) {
+    if (__atomic_load_n(h->h_done, __ATOMIC_ACQUIRE) >= seq) return GS_OK;
+    if ((i & 255u) == 0 && std::chrono::steady_clock::now() - t0 > kSpinWait) break;
+    __builtin_ia32_pause();
+  }
+  GS_HIP(hipStreamSynchronize(h->stream));
+  if (__atomic_load_n(h->h_done, __ATOMIC_ACQUIRE) < seq) return fail(GS_ERR_HIP, "completion word not written");
+  return GS_OK;
+}
+
 // Error flags, read with ONE host synchronisation. Also refreshes whether the
 // vertex list is complete.
 int check_device_flags(gs_summary* h) {
   // kernels mirror the rare flags into host-mapped memory (raise_flag): after the
-  // stream sync they are read with no device-to-host copy (each copy is a launch and
+  // stream wait they are read with no device-to-host copy (each copy is a launch and
   // a round trip of its own: the three per-flag copies cost ~10 us of a 2^16-edge
   // window, config 5)
-  GS_HIP(hipStreamSynchronize(h->stream));
+  if (int rc = wait_stream(h)) return rc;
+  return check_flags_now(h);
+}
+
+// The host-mapped flags as they stand (the caller has waited for the stream).
+int check_flags_now(gs_summary* h) {
   const uint32_t err = __atomic_load_n(&h->h_flags[0], __ATOMIC_ACQUIRE);
   const uint32_t ovf = __atomic_load_n(&h->h_flags[1], __ATOMIC_ACQUIRE);
   const uint32_t vovf = __atomic_load_n(&h->h_flags[2], __ATOMIC_ACQUIRE);
@@ -355,13 +395,9 @@ int check_device_flags(gs_summary* h) {
 
 int read_nv(gs_summary* h, uint64_t* nv) {
   if (int rc = join_lanes(h)) return rc;
-  std::vector<uint32_t> c(gs::CTR_COUNT * gs::kCtrStride);
-  GS_HIP(hipMemcpyAsync(c.data(), h->ctr, c.size() * 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
-  uint64_t s = 0;
-  for (int i = 0; i < gs::kShards; ++i) s += c[gs::ctr_index(gs::CTR_NV + i)];
-  if (c[gs::ctr_index(gs::CTR_VOVF)]) h->vlist_ok = false;
-  *nv = s;
+  // the 64 shard counts summed on the device and handed over with the wait
+  if (int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_NV), nv, gs::kShards, gs::kCtrStride)) return rc;
+  if (__atomic_load_n(&h->h_flags[2], __ATOMIC_ACQUIRE)) h->vlist_ok = false;  // CTR_VOVF's mirror
   return GS_OK;
 }
 
@@ -375,7 +411,7 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
   // exchange buffer the caller's count of live rows it will fold. The valid rows may
   // sit in any chunk, so an exchange fold claims all its units with its last chunk.
   const uint64_t units = fs.rows ? fs.units : n;
-  if (track) {  // refuse before any capacity accounting: edges charged there must be folded
+  if (track && !fs.take_out) {  // refuse before any capacity accounting: edges charged there must be folded
     uint64_t fill = h->delta_fill_ub[h->dset];
     for (size_t off = 0; off < n; off += kMaxChunk) fill += per_shard_edges(std::min<size_t>(kMaxChunk, n - off));
     if (!h->drec || fill > h->delta_shard_cap)
@@ -399,7 +435,7 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
   for (size_t off = 0; off < n; off += kMaxChunk) {
     const uint32_t c = (uint32_t)std::min<size_t>(kMaxChunk, n - off);
     const uint32_t blocks = (c + gs::kFoldBS - 1) / gs::kFoldBS;
-    if (track) h->delta_fill_ub[h->dset] += per_shard_edges(c);
+    if (track && !fs.take_out) h->delta_fill_ub[h->dset] += per_shard_edges(c);  // (a fused take bypasses the set)
     hipStream_t st = side ? h->side : h->stream;
     if (side) h->side_dirty = true;
     if (pipe) {  // the lane waits for the caller's work on the handle stream, not for the other lane
@@ -426,6 +462,15 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     f.n_dev = fs.n_dev;
     f.fail_in = off == 0 ? fs.fail_in : nullptr;
     f.shard0 = h->shard0;
+    if (fs.take_out) {
+      f.take_out = fs.take_out;
+      f.take_cap = fs.take_cap;
+      f.take_count = fs.take_count;
+      f.done = h->done_dev;
+      // drawn here, after the capacity check: a table rebuild there waits on the same
+      // completion word with sequence numbers of its own
+      f.seq = *fs.take_seq = ++h->done_seq;
+    }
     h->shard0 = (h->shard0 + blocks) & (gs::kShards - 1);
     {
       Prof p(h, KID_FOLD, st);
@@ -448,7 +493,8 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       // off the handle stream a report is not a gap between folds: report every chunk
       // while the bound is near the load limit (small tables), so no fold has to wait
       const bool tight = rs != 0 && (double)(h->nv_ub + 4ull * gs_summary::kRepEvery * c) > kMaxLoad * (double)h->cap;
-      if (++h->rep_skip[rs] >= gs_summary::kRepEvery || tight) {
+      // (a fused take is waited for: its caller takes the exact count instead)
+      if (!fs.take_out && (++h->rep_skip[rs] >= gs_summary::kRepEvery || tight)) {
         const uint64_t claim = h->rep_pending[rs];
         gs::launch_report(h->ctr, claim, h->rep_dev + (h->rep_seq++ % gs_summary::kRepRing),
                           (unsigned)(h->rep_epoch & 7u), st);
@@ -475,9 +521,8 @@ int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t
       gs::launch_export(h->table(), v, l, p, cap, h->stream, part, nparts);
   }
   GS_HIP(hipGetLastError());
-  uint32_t cnt = 0;
-  GS_HIP(hipMemcpyAsync(&cnt, h->ctr + gs::ctr_index(gs::CTR_EXPORT), 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
+  uint64_t cnt = 0;
+  if (int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_EXPORT), &cnt)) return rc;
   *n = cnt;
   if (cnt > cap) return fail(GS_ERR_TRUNCATED, "output capacity " + std::to_string(cap) + " < " + std::to_string(cnt));
   return GS_OK;
@@ -548,9 +593,12 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   if (hipMalloc(&h->d_stage, sizeof(int64_t) * 4 * kStageChunk) != hipSuccess ||
       hipMalloc(&h->d_wstage, 2 * kStageChunk) != hipSuccess || hipMalloc(&h->d_scratch, 64) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipMalloc(staging) failed"));
-  if (hipHostMalloc(&h->h_flags, 16, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+  if (hipHostMalloc(&h->h_flags, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hflags_dev), h->h_flags, 0) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipHostMalloc(flags) failed"));
+  memset(h->h_flags, 0, 64);
+  h->h_done = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h->h_flags) + 32);
+  h->done_dev = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h->hflags_dev) + 32);
   for (int i = 0; i < 2; ++i)
     if (hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming) != hipSuccess)
       return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
@@ -960,6 +1008,38 @@ int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
   return stage_delta(h, rec, cap, 3, reinterpret_cast<unsigned long long*>(count), false);
+}
+
+int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, size_t n, int64_t* rec, size_t cap,
+                        uint64_t* count_dev, uint64_t* count) {
+  if (int rc = check(h)) return rc;
+  if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
+  if (!count_dev || !count || (cap && !rec)) return fail(GS_ERR_INVALID, "null argument");
+  if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
+  DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
+  auto* cd = reinterpret_cast<unsigned long long*>(count_dev);
+  // One launch when the window fits one k_fold launch and nothing else is pending in
+  // the delta set (earlier tracked folds' records belong to this take too), and no
+  // change emission consumes the records.
+  const bool fused = n > 0 && n <= kMaxChunk && h->delta_fill_ub[h->dset] == 0 && !h->changes && !h->profiling;
+  if (!fused) {
+    if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, true)) return rc;
+    if (int rc = stage_delta(h, rec, cap, 3, cd, false)) return rc;
+    if (int rc = wait_stream(h, reinterpret_cast<const uint32_t*>(cd), count)) return rc;  // rows < 2^32
+    return check_flags_now(h);
+  }
+  FoldSource fs;
+  fs.take_out = rec;
+  fs.take_cap = cap;
+  fs.take_count = cd;
+  unsigned long long seq = 0;
+  fs.take_seq = &seq;
+  if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, true, true, fs)) return rc;
+  if (int rc = wait_done(h, seq)) return rc;
+  note_exact_count(h, __atomic_load_n(h->h_done + 1, __ATOMIC_ACQUIRE));
+  *count = __atomic_load_n(h->h_done + 2, __ATOMIC_ACQUIRE);
+  return check_flags_now(h);
 }
 
 int gs_delta_stage(gs_handle h, int64_t* send, size_t cap, int width, uint64_t* count) {

@@ -129,7 +129,7 @@ int gs_take_changes_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* par
   if (int rc = read_nv(h, &nv)) return rc;  // joins every stream
   *n = 0;
   if (cap < nv) return fail(GS_ERR_INVALID, "cap below the vertex count: " + std::to_string(nv));
-  if (int rc = check_device_flags(h)) return rc;
+  if (int rc = check_flags_now(h)) return rc;  // read_nv waited
   if (int rc = ensure_scratch(h)) return rc;
   const ChgScratch c = scratch(h);
   const gs::Table t = h->table();
@@ -146,15 +146,13 @@ int gs_take_changes_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* par
     GS_HIP(hipGetLastError());
     h->chg_scan_all = false;
   } else {
-    uint64_t nrec = 0;
-    GS_HIP(hipMemcpyAsync(&nrec, c.nrec, 8, hipMemcpyDeviceToHost, h->stream));
-    GS_HIP(hipStreamSynchronize(h->stream));
+    uint64_t nrec = 0;  // (< 2^32: at most the delta capacity)
+    if (int rc = wait_stream(h, reinterpret_cast<const uint32_t*>(c.nrec), &nrec)) return rc;
     // phase 0 flags roots too large to walk, phase 1 walks the rest and splices
     if (nrec) gs::launch_emit_records(t, h->nxt, c.rec, c.nrec, nrec, walk_max(), v, label, parity, cap, c.big, h->stream);
     GS_HIP(hipGetLastError());
-    uint32_t nbig = 0;
-    GS_HIP(hipMemcpyAsync(&nbig, h->ctr + gs::ctr_index(gs::CTR_BIG), 4, hipMemcpyDeviceToHost, h->stream));
-    GS_HIP(hipStreamSynchronize(h->stream));
+    uint64_t nbig = 0;
+    if (int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_BIG), &nbig)) return rc;
     if (nbig) {  // before k_emit_new clears the new bits the scan tests
       gs::launch_emit_scan(t, v, label, parity, cap, false, h->stream);
       gs::launch_clear_big(t, c.big, nbig, h->stream);
@@ -162,9 +160,8 @@ int gs_take_changes_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* par
     gs::launch_emit_new(t, c.vmark, v, label, parity, cap, nv, true, h->stream);
     GS_HIP(hipGetLastError());
   }
-  uint64_t emitted = 0;
-  GS_HIP(hipMemcpyAsync(&emitted, h->ctr + gs::ctr_index(gs::CTR_EMIT), 8, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
+  uint64_t emitted = 0;  // (low word of the u64 counter: rows < 2^32)
+  if (int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_EMIT), &emitted)) return rc;
   *n = emitted;
   if (emitted > cap) return fail(GS_ERR_TRUNCATED, "emission rows above cap");
   return GS_OK;

@@ -62,6 +62,9 @@ enum CounterBlock : int {
   CTR_EMIT_HI,
   CTR_BIG,                       // change emission: hooked roots too large to walk
   CTR_SCAN_ALL,                  // change emission: emit every vertex (after a table rebuild)
+  CTR_TAKE,                      // fused window take (k_fold TAKE): output rows reserved (u64)
+  CTR_TAKE_HI,
+  CTR_TAKE_DONE,                 //   block ticket
   CTR_DBG_HOOKS,                 // debug build (-DGS_DEBUG_COUNTERS): hook calls,
   CTR_DBG_ITERS,                 //   hook-loop iterations,
   CTR_DBG_CASFAIL,               //   failed hook CASes
@@ -105,6 +108,9 @@ struct Delta {
   int64_t* drec;       // records {a, b, parity} of one delta set [kShards][shard_cap][3], or null
   uint32_t shard_cap;
   uint32_t dctr;       // counter index of that set's shard 0 (CTR_DELTA + set * kShards)
+  // fused window take (k_fold TAKE): the block's records go to an LDS buffer instead
+  int64_t* lrec = nullptr;   // [kFoldBS][3] (LDS)
+  uint32_t* lcnt = nullptr;  // its fill (LDS)
 };
 
 __device__ __forceinline__ uint32_t hash_slot(int64_t key, int shift) {
@@ -339,9 +345,21 @@ __device__ __forceinline__ void combine_hooks(bool active, uint32_t& a, int64_t&
   }
 }
 
-// Append one delta record {a, b, w} to shard `shard` of the delta list.
+// Append one delta record {a, b, w} to shard `shard` of the delta list, or (TAKE) to
+// the block's LDS buffer: a lane appends at most one record per edge it folds (a
+// self-loop's new vertex or one successful hook), so kFoldBS rows always suffice.
+template <bool TAKE = false>
 __device__ __forceinline__ void append_record(const Table& t, const Delta& D, int shard, int64_t a, int64_t b,
                                               int64_t w) {
+  if (TAKE) {
+    const uint32_t p = atomicAdd(D.lcnt, 1u);
+    if (p < kFoldBS) {
+      D.lrec[p * 3] = a;
+      D.lrec[p * 3 + 1] = b;
+      D.lrec[p * 3 + 2] = w;
+    }
+    return;
+  }
   const uint32_t pos = atomicAdd(&t.ctr[ctr_index(D.dctr + shard)], 1u);
   if (pos < D.shard_cap) {
     int64_t* r = D.drec + ((size_t)shard * D.shard_cap + pos) * 3;
@@ -359,7 +377,7 @@ __device__ __forceinline__ void append_record(const Table& t, const Delta& D, in
 // agent-scope loads; before its CAS the loop re-reads the target root's link
 // (test-and-test-and-set): a root a concurrent hook already moved -- the hub root
 // while a giant component forms -- is followed without queueing a CAS on its address.
-template <bool SIGNED, bool TRACK>
+template <bool SIGNED, bool TRACK, bool TAKE = false>
 __device__ __forceinline__ void hook(const Table& t, const Delta& D, int shard, uint32_t a, uint32_t la, int64_t ka,
                                      uint32_t b, uint32_t lb, int64_t kb, uint32_t need) {
   GS_DBG(CTR_DBG_HOOKS);
@@ -382,7 +400,7 @@ __device__ __forceinline__ void hook(const Table& t, const Delta& D, int shard, 
     const uint32_t seen = load_link_fresh(t.tab + hi);
     const uint32_t old = seen == expect ? atomicCAS(&t.tab[hi].link, expect, desired) : seen;
     if (old == expect) {
-      if (TRACK) append_record(t, D, shard, a_lo ? kb : ka, a_lo ? ka : kb, (int64_t)(SIGNED ? (need & 1u) : 0u));
+      if (TRACK) append_record<TAKE>(t, D, shard, a_lo ? kb : ka, a_lo ? ka : kb, (int64_t)(SIGNED ? (need & 1u) : 0u));
       return;
     }
     // hi was hooked meanwhile: continue that side from its live link

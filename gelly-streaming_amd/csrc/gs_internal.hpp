@@ -69,6 +69,11 @@ struct gs_summary {
   bool vlist_ok = true;       // false once a shard of the vertex list overflowed (until reset)
   uint32_t* h_flags = nullptr;     // host-mapped mirror of CTR_ERR / CTR_OVF / CTR_VOVF (raise_flag)
   uint32_t* hflags_dev = nullptr;  // its device address
+  // host waits (wait_stream): completion word {seq, value} in the same host-mapped
+  // allocation (bytes 32..47), written by k_signal
+  unsigned long long* h_done = nullptr;
+  unsigned long long* done_dev = nullptr;
+  unsigned long long done_seq = 0;
   // capacity tracking: a host upper bound of the vertex count, refreshed without
   // host synchronisation from k_report words (ring in host-coherent memory)
   uint64_t nv_ub = 0;
@@ -194,6 +199,12 @@ struct FoldSource {
   bool on_side = false;  // launch on h->side (a group's apply stream) instead of h->stream
   bool allow_pipe = false;
   int lane = -1;         // >= 0: launch on this pipelining lane (a group's own tracked fold)
+  // fused window take (gs_fold_take_device): one tracked launch that also writes the
+  // rows, the count and the completion word {seq, vertices, rows}
+  int64_t* take_out = nullptr;
+  uint64_t take_cap = 0;
+  unsigned long long* take_count = nullptr;
+  unsigned long long* take_seq = nullptr;  // out: the completion sequence number, drawn at launch
 };
 
 int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
@@ -203,7 +214,14 @@ int join_lanes(gs_summary* h);
 bool side_ok(const gs_summary* h);
 int ensure_lanes(gs_summary* h, int n);  // create lane streams 0..n-1 on first use
 int read_nv(gs_summary* h, uint64_t* nv);
+// wait until every operation queued on h->stream so far has completed; *value
+// (optional) = the sum of nvals device u32 counters vals[i * stride], read in the same
+// round trip
+int wait_stream(gs_summary* h, const uint32_t* vals = nullptr, uint64_t* value = nullptr, int nvals = 1,
+                int stride = 0);
 int check_device_flags(gs_summary* h);
+int check_flags_now(gs_summary* h);
+int wait_done(gs_summary* h, unsigned long long seq);  // spin on the completion word (h->stream)  // after a wait: the host-mapped flags only
 int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n, int part = 0,
                        int nparts = 1);
 // stage every pending delta record into out (first cap rows, `width` int64 each) and

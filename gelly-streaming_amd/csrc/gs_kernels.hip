@@ -104,18 +104,86 @@ struct FoldArgs {
   const unsigned long long* n_dev;   // optional: device element count (valid: base + i < *n_dev)
   const uint32_t* fail_in;           // optional: failure flag of a combined summary (SIGNED)
   uint32_t shard0;    // first shard of this launch (rotates per launch: balanced shard fill)
+  // fused window take (TAKE): rows -> take_out[take_cap][3], count -> *take_count; the
+  // last block writes {seq, vertices, rows} to the host-mapped completion word `done`
+  int64_t* take_out;
+  unsigned long long take_cap;
+  unsigned long long* take_count;
+  unsigned long long* done;
+  unsigned long long seq;
 };
 
 constexpr int kCombineRounds = 2;  // wave-level hook combining (combine_hooks)
 
-template <bool SIGNED, bool TRACK>
+// Tail of a fused window take (config 5's per-window fold + delta export + completion
+// in ONE launch instead of fold, stage and completion kernels, each a kernel boundary of
+// ~3 us). Each block reserves its rows in the output with one atomic and writes them
+// from LDS with write-through (agent-scope) stores, so that they are in memory -- not
+// in this XCD's L2 -- once the block's stores are acknowledged; the block then takes a
+// ticket. The last block publishes the count, resets the take counters and stores the
+// completion word (system scope) that the host spins on. The table writes need no
+// fence: the next kernel of the stream starts after this one's end-of-kernel release,
+// and only the rows and the count are read before that (by the host or other streams).
+__device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, const int64_t* lrec, uint32_t lcnt) {
+  __shared__ unsigned long long base_sh;
+  __shared__ uint32_t last_sh;
+  const uint32_t nb = min(lcnt, kFoldBS);
+  if (threadIdx.x == 0)
+    base_sh = nb ? atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE)),
+                             (unsigned long long)nb)
+                 : 0ull;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nb; j += kFoldBS) {
+    const unsigned long long pos = base_sh + j;
+    if (pos < a.take_cap) {
+      int64_t* r = a.take_out + pos * 3;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        __hip_atomic_store(r + c, lrec[j * 3 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // every wave waits for its stores' acknowledgements before the barrier (the barrier
+  // alone does not wait for global stores); no L2 writeback needed for write-through rows
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) last_sh = atomicAdd(t.ctr + ctr_index(CTR_TAKE_DONE), 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last_sh || threadIdx.x >= 64) return;
+  unsigned long long nv = __hip_atomic_load(t.ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) nv += __shfl_xor(nv, o, 64);
+  if (threadIdx.x != 0) return;
+  unsigned long long* take = reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE));
+  const unsigned long long total = __hip_atomic_load(take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  *a.take_count = total;
+  atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_SENT)), total < a.take_cap ? total : a.take_cap);
+  __hip_atomic_store(take, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(t.ctr + ctr_index(CTR_TAKE_DONE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __threadfence_system();
+  __hip_atomic_store(a.done + 1, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(a.done + 2, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(a.done, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <bool SIGNED, bool TRACK, bool TAKE>
 __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) {
+  __shared__ int64_t lrec[TAKE ? kFoldBS * 3 : 1];
+  __shared__ uint32_t lcnt;
+  if (TAKE) {
+    D.lrec = lrec;
+    D.lcnt = &lcnt;
+    if (threadIdx.x == 0) lcnt = 0;
+    __syncthreads();
+  }
   if (SIGNED && a.fail_in && blockIdx.x == 0 && threadIdx.x == 0 && *a.fail_in)
     atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);  // the verdict is the AND (Candidates.java:79-81)
-  if (SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0) return;
+  // a failed verdict is final: no more work (a TAKE block still reaches its ticket)
+  const bool failed = SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0;
+  if (failed && !TAKE) return;
   const int shard = (int)((blockIdx.x + a.shard0) & (kShards - 1));
   const uint32_t i = blockIdx.x * kFoldBS + threadIdx.x;
-  bool valid = i < a.n;
+  bool valid = i < a.n && !failed;
   if (valid && a.n_dev) valid = (unsigned long long)(a.base + i) < *a.n_dev;
   if (valid && a.rows) {  // exchange layout: the block's count word gives its live rows
     const uint32_t ig = a.base + i, r = ig / a.rows, j = ig - r * a.rows;
@@ -150,7 +218,7 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
     // record (as the hooked root or as the new parent: its singleton tree can only
     // change through a CAS on it or onto it), so only a new vertex seen through a
     // self-loop needs a record of its own.
-    if (TRACK && nu && su == sv) append_record(t, D, shard, ks, ks, 0);
+    if (TRACK && nu && su == sv) append_record<TAKE>(t, D, shard, ks, ks, 0);
     ru = su;
     rv = sv;
     if (su != kNoSlot && sv != kNoSlot && su != sv) {  // a self-loop adds its vertex, never a conflict
@@ -175,7 +243,11 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
     }
   }
   if (__popcll(__ballot(act)) >= 2) combine_hooks(act, ru, kru, rv, krv, need, kCombineRounds);  // wave-uniform
-  if (act) hook<SIGNED, TRACK>(t, D, shard, ru, ru << 1, kru, rv, rv << 1, krv, need);
+  if (act) hook<SIGNED, TRACK, TAKE>(t, D, shard, ru, ru << 1, kru, rv, rv << 1, krv, need);
+  if (TAKE) {
+    __syncthreads();
+    take_tail(t, a, lrec, lcnt);
+  }
 }
 
 // Export (vertex, label, parity) of every occupied slot of [s_begin, s_end). Each
@@ -377,6 +449,25 @@ __global__ __launch_bounds__(64) void k_headers(const unsigned long long* __rest
   }
 }
 
+// Completion word of a host wait (gs_sync and every other host synchronisation of a
+// handle). Queued last on the handle stream, it starts only after all earlier work of
+// the stream has completed -- end-of-kernel releases included -- so its system-scope
+// store tells the host that everything before it is done and visible. The host spins
+// on host-mapped memory instead of waiting for the stream's completion signal: a
+// one-wave kernel + hipStreamSynchronize costs 12.2 us, a kernel whose store the
+// host polls 6.5 us (tools/calib_launch.hip). `vals` (optional): the sum of nvals
+// device counters (stride apart, <= 64) handed to the host in the same round trip
+// (row counts, the sharded vertex count) instead of a copy and a second wait.
+__global__ __launch_bounds__(64) void k_signal(unsigned long long* out, unsigned long long seq, const uint32_t* vals,
+                                               int nvals, int stride) {
+  unsigned long long v = (vals && (int)threadIdx.x < nvals) ? vals[(size_t)threadIdx.x * stride] : 0ull;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (threadIdx.x != 0) return;
+  if (vals) __hip_atomic_store(out + 1, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(out, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Single-vertex lookup (gs_find): presence and label.
 __global__ void k_find_one(Table t, int64_t key, int64_t* out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -427,13 +518,19 @@ void launch_reset_list(const Table& t, uint32_t* nxt, uint64_t bound, hipStream_
 }
 
 void launch_fold(bool sign, bool track, const Table& t, const Delta& D, const FoldLaunch& f, hipStream_t st) {
-  FoldArgs a{f.src,  f.dst,    f.w,      f.n,     f.stride,  f.w_stride, f.rows,
-             f.skip_rank, f.counts, f.base, f.n_dev, f.fail_in, f.shard0};
+  FoldArgs a{f.src,       f.dst,    f.w,      f.n,       f.stride,   f.w_stride,  f.rows,
+             f.skip_rank, f.counts, f.base,   f.n_dev,   f.fail_in,  f.shard0,    f.take_out,
+             f.take_cap,  f.take_count, f.done, f.seq};
   const dim3 g((f.n + kFoldBS - 1) / kFoldBS), b(kFoldBS);
-  if (!sign && !track) hipLaunchKernelGGL((k_fold<false, false>), g, b, 0, st, t, D, a);
-  if (!sign && track) hipLaunchKernelGGL((k_fold<false, true>), g, b, 0, st, t, D, a);
-  if (sign && !track) hipLaunchKernelGGL((k_fold<true, false>), g, b, 0, st, t, D, a);
-  if (sign && track) hipLaunchKernelGGL((k_fold<true, true>), g, b, 0, st, t, D, a);
+  if (f.take_out) {  // fused window take (always tracked)
+    if (sign) hipLaunchKernelGGL((k_fold<true, true, true>), g, b, 0, st, t, D, a);
+    else hipLaunchKernelGGL((k_fold<false, true, true>), g, b, 0, st, t, D, a);
+    return;
+  }
+  if (!sign && !track) hipLaunchKernelGGL((k_fold<false, false, false>), g, b, 0, st, t, D, a);
+  if (!sign && track) hipLaunchKernelGGL((k_fold<false, true, false>), g, b, 0, st, t, D, a);
+  if (sign && !track) hipLaunchKernelGGL((k_fold<true, false, false>), g, b, 0, st, t, D, a);
+  if (sign && track) hipLaunchKernelGGL((k_fold<true, true, false>), g, b, 0, st, t, D, a);
 }
 
 void launch_export(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, hipStream_t st, int part,
@@ -463,6 +560,11 @@ void launch_report(uint32_t* ctr, uint64_t n, unsigned long long* out, unsigned 
 
 void launch_headers(const unsigned long long* counts, int nranks, long long* out, long long seq, hipStream_t st) {
   hipLaunchKernelGGL(k_headers, dim3(1), dim3(64), 0, st, counts, nranks, out, seq);
+}
+
+void launch_signal(unsigned long long* out, unsigned long long seq, const uint32_t* vals, int nvals, int stride,
+                   hipStream_t st) {
+  hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, out, seq, vals, nvals, stride);
 }
 
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st) {

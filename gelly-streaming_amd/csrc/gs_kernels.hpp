@@ -23,6 +23,12 @@ struct FoldLaunch {
   const unsigned long long* n_dev = nullptr;
   const uint32_t* fail_in = nullptr;
   uint32_t shard0 = 0;
+  // fused window take (k_fold TAKE, one launch): rows, device count, completion word
+  int64_t* take_out = nullptr;
+  unsigned long long take_cap = 0;
+  unsigned long long* take_count = nullptr;
+  unsigned long long* done = nullptr;
+  unsigned long long seq = 0;
 };
 
 void launch_init(Slot* tab, uint64_t nslots, hipStream_t st);
@@ -36,6 +42,10 @@ void launch_stage(const Table& t, const Delta& D, int64_t* out, uint64_t cap, in
                   unsigned long long* count_out, bool with_fail, hipStream_t st);
 void launch_report(uint32_t* ctr, uint64_t n, unsigned long long* out, unsigned epoch, hipStream_t st);
 void launch_headers(const unsigned long long* counts, int nranks, long long* out, long long seq, hipStream_t st);
+// completion word for host waits: out[1] = sum of nvals (<= 64) counters vals[i * stride]
+// (if vals), then out[0] = seq (release, system scope)
+void launch_signal(unsigned long long* out, unsigned long long seq, const uint32_t* vals, int nvals, int stride,
+                   hipStream_t st);
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st);
 void launch_find_batch(const Table& t, const int64_t* v, uint64_t n, int64_t* label, uint8_t* found, uint8_t* parity,
                        hipStream_t st);

@@ -187,6 +187,16 @@ int gs_deserialize(gs_handle h, const void* buf, size_t len);
  * folds such records (track = 0: apply another replica's delta without
  * re-recording it).
  *
+ * gs_fold_take_device is one small window of the latency path (BASELINE config 5:
+ * per window fold + delta export + completion; PartialAgg.fold then CombineCC /
+ * Merger, S/SummaryBulkAggregation.java:109-130, S/SummaryAggregation.java:107-119):
+ * fold n device edges with tracking on, take the records since the previous take
+ * as gs_take_delta_records does (rec, cap, DEVICE *count_dev), and return when the
+ * window is complete with the record total in the HOST word *count. A window of at
+ * most 2^22 edges with nothing else pending runs as ONE launch whose last workgroup
+ * publishes the rows and signals the host through mapped memory. Tracking must be
+ * on; change tracking (which consumes the records itself) takes the general path.
+ *
  * gs_delta_stage is the exchange form: every pending record into `send` as rows of
  * `width` int64 ({a, b} for CC, {a, b, w} for the signed kind; cap must be at least
  * gs_delta_capacity), and the DEVICE count word *count = rows | 2^62 when the
@@ -198,6 +208,8 @@ int gs_deserialize(gs_handle h, const void* buf, size_t len);
 int gs_set_delta_tracking(gs_handle h, int on);
 int gs_delta_capacity(gs_handle h, uint64_t* rows);
 int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count);
+int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, size_t n, int64_t* rec, size_t cap,
+                        uint64_t* count_dev, uint64_t* count);
 int gs_delta_stage(gs_handle h, int64_t* send, size_t cap, int width, uint64_t* count);
 int gs_fold_records_device(gs_handle h, const int64_t* rec, size_t n, int track);
 int gs_fold_exchange_device(gs_handle h, const int64_t* recv, const uint64_t* counts, size_t world, size_t rows,

@@ -1,0 +1,144 @@
+"""The latency path's fused window (gs_fold_take_device: fold + delta take + completion in
+one launch, BASELINE config 5) against the oracle and against the separate
+fold / take / sync sequence. Reference: per-window PartialAgg.fold then CombineCC and
+the Merger (S/SummaryBulkAggregation.java:109-130, S/SummaryAggregation.java:107-119)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _labels_equal(a, b):
+    v1, l1 = a.labels()
+    v2, l2 = b.labels()
+    return np.array_equal(v1, v2) and np.array_equal(l1, l2)
+
+
+@pytest.mark.parametrize("logn,logb", [(14, 10), (17, 12)])
+def test_fused_window_take_matches_oracle_and_replays(gs, oracle_mod, logn, logb):
+    """ER windows through fold_take: labels oracle-exact after every checkpoint; the
+    taken records alone rebuild the summary; host count == device count <= window."""
+    import torch
+    E, B = 1 << (logn + 3), 1 << logb
+    src = torch.empty(E, dtype=torch.int64, device="cuda")
+    dst = torch.empty(E, dtype=torch.int64, device="cuda")
+    gs.gen_er(src, dst, 0, E, logn, 0x5EED00E5, True)
+    torch.cuda.synchronize()
+    rec = torch.empty((B, 3), dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    hs, hd = src.cpu().numpy(), dst.cpu().numpy()
+    ps, pd = src.data_ptr(), dst.data_ptr()
+    with gs.Summary("cc", capacity_hint=1 << logn) as s, gs.Summary("cc", capacity_hint=1 << logn) as rep:
+        s.set_delta_tracking(True)
+        total = 0
+        for w in range(E // B):
+            o = w * B
+            k = s.fold_take(ps + 8 * o, pd + 8 * o, B, rec, B, cnt)
+            assert k == int(cnt.item()) and 0 <= k <= B
+            total += k
+            rep.fold_records(rec, k)
+            if w + 1 in (1, 2, 7, E // B):
+                ov, olab = oracle_mod.cc_labels(hs[:o + B], hd[:o + B])
+                v, lab = s.labels()
+                assert np.array_equal(v, ov) and np.array_equal(lab, olab), "oracle differs at window %d" % (w + 1)
+                assert _labels_equal(s, rep), "replay differs at window %d" % (w + 1)
+        # records >= component merges + vertices (every vertex is named by some record)
+        assert total >= len(np.unique(np.concatenate([hs, hd]))) - len(set(olab.tolist()))
+
+
+def test_fused_window_take_self_loops_and_growth(gs, oracle_mod):
+    """A 1-vertex capacity hint (the table grows inside the fused path's capacity check),
+    self-loops and duplicate edges: still oracle-exact and replayable."""
+    import torch
+    rng = np.random.default_rng(7)
+    n, B = 1 << 14, 1 << 10
+    hs = rng.integers(-(1 << 40), 1 << 40, n, dtype=np.int64)
+    hd = hs.copy()
+    m = rng.random(n) < 0.7
+    hd[m] = rng.choice(hs, int(m.sum()))  # 30 % self-loops, repeated ids
+    src = torch.from_numpy(hs).cuda()
+    dst = torch.from_numpy(hd).cuda()
+    rec = torch.empty((B, 3), dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    with gs.Summary("cc", capacity_hint=1) as s, gs.Summary("cc", capacity_hint=1) as rep:
+        s.set_delta_tracking(True)
+        for o in range(0, n, B):
+            k = s.fold_take(src[o:], dst[o:], B, rec, B, cnt)
+            rep.fold_records(rec, k)
+        ov, olab = oracle_mod.cc_labels(hs, hd)
+        v, lab = s.labels()
+        assert np.array_equal(v, ov) and np.array_equal(lab, olab)
+        assert _labels_equal(s, rep)
+
+
+def test_fused_window_take_signed_verdict(gs, oracle_mod):
+    """Signed kind: the parity rides in the records (w), the verdict flips in the truth's
+    window, and after failure the fused launch still completes (every block reaches its
+    ticket) with no records."""
+    import torch
+    logside, E, B = 12, 1 << 15, 1 << 11
+    inject = [E // 4, E // 2]
+    src = torch.empty(E, dtype=torch.int64, device="cuda")
+    dst = torch.empty(E, dtype=torch.int64, device="cuda")
+    gs.gen_bip(src, dst, 0, E, logside, 0x5EED0B1B, inject)
+    torch.cuda.synchronize()
+    first = oracle_mod.bip_first_failure(src.cpu().numpy(), dst.cpu().numpy())
+    assert first >= 0
+    rec = torch.empty((B, 3), dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    with gs.Summary("signed", capacity_hint=1 << 13) as c, gs.Summary("signed", capacity_hint=1 << 13) as rep:
+        c.set_delta_tracking(True)
+        for o in range(0, E, B):
+            k = c.fold_take(src[o:], dst[o:], B, rec, B, cnt)
+            if o >= first + B:
+                assert k == 0  # a failed verdict is final: nothing folds, nothing recorded
+            if first >= o + B:
+                rep.fold_records(rec, k)
+                assert rep.ok()
+            assert c.ok() == (first >= o + B), (o, first)
+
+
+def test_fused_window_take_truncates_and_counts(gs):
+    """cap below the window's records: only cap rows written, the count says how many."""
+    import torch
+    n = 1 << 12
+    hs = np.arange(0, 2 * n, 2, dtype=np.int64)
+    hd = hs + 1  # n disjoint edges: n hook records
+    src = torch.from_numpy(hs).cuda()
+    dst = torch.from_numpy(hd).cuda()
+    cap = 100
+    rec = torch.full((cap + 8, 3), -7, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    with gs.Summary("cc", capacity_hint=1 << 14) as s:
+        s.set_delta_tracking(True)
+        k = s.fold_take(src, dst, n, rec, cap, cnt)
+        assert k == n and int(cnt.item()) == n
+        r = rec.cpu().numpy()
+        assert (r[cap:] == -7).all()  # nothing past cap
+        got = {(int(a), int(b)) for a, b, _ in r[:cap]}
+        assert len(got) == cap and all(b == a - 1 or a == b - 1 for a, b in got)
+
+
+def test_fused_window_take_includes_pending_records(gs, oracle_mod):
+    """Records of an earlier tracked fold that nobody took belong to the next take
+    (general path); the following window is fused again."""
+    import torch
+    rng = np.random.default_rng(3)
+    hs = rng.integers(0, 1 << 12, 3 << 10, dtype=np.int64)
+    hd = rng.integers(0, 1 << 12, 3 << 10, dtype=np.int64)
+    src = torch.from_numpy(hs).cuda()
+    dst = torch.from_numpy(hd).cuda()
+    B = 1 << 10
+    rec = torch.empty((2 * B, 3), dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    with gs.Summary("cc", capacity_hint=1 << 13) as s, gs.Summary("cc", capacity_hint=1 << 13) as rep:
+        s.set_delta_tracking(True)
+        s.fold_device(src[:B], dst[:B], n=B)  # tracked, not taken
+        k = s.fold_take(src[B:], dst[B:], B, rec, 2 * B, cnt)
+        rep.fold_records(rec, k)
+        k = s.fold_take(src[2 * B:], dst[2 * B:], B, rec, 2 * B, cnt)
+        rep.fold_records(rec, k)
+        ov, olab = oracle_mod.cc_labels(hs, hd)
+        v, lab = rep.labels()
+        assert np.array_equal(v, ov) and np.array_equal(lab, olab)
+        assert _labels_equal(s, rep)

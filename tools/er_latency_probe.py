@@ -1,8 +1,9 @@
 """Where the config-5 per-window latency goes (diagnostic). ER G(2^22, 2^26), 2^16-edge
 windows, delta tracking on; p50 / p99 microseconds per window for:
-  bench      bench.py's loop (torch slices, fold_device, take_delta_records, sync)
+  separate   torch slices, fold_device, take_delta_records, gs_sync (three launches)
   rawptr     the same with precomputed integer device pointers (no torch slicing)
   fold_sync  rawptr without the delta take
+  fused      gs_fold_take_device (one launch: fold + take + completion word)
   sync_only  an empty gs_sync per window (host <-> device round trip)
     python tools/er_latency_probe.py
 """
@@ -44,9 +45,13 @@ def main():
         lat = []
         for o in range(0, E, B):
             t0 = time.perf_counter()
-            if kind == "bench":
+            if kind == "separate":
                 s.fold_device(src[o:], dst[o:], n=B)
                 s.take_delta_records(rec, cap, cnt)
+            elif kind == "fused":
+                s.fold_take(ps + 8 * o, pd + 8 * o, B, rec, cap, cnt)
+                lat.append(time.perf_counter() - t0)
+                continue
             elif kind in ("rawptr", "fold_sync"):
                 check(L.gs_fold_device(x._h, ps + 8 * o, pd + 8 * o, None, B, 1))
                 if kind == "rawptr":
@@ -56,7 +61,7 @@ def main():
         lat = np.array(lat[8:]) * 1e6
         return np.percentile(lat, 50), np.percentile(lat, 99)
 
-    for kind in ("bench", "rawptr", "fold_sync", "sync_only", "bench", "rawptr"):
+    for kind in ("separate", "rawptr", "fold_sync", "fused", "sync_only", "separate", "fused"):
         p50, p99 = run(kind)
         print("%-10s p50 %6.2f us  p99 %6.2f us" % (kind, p50, p99), flush=True)
     s.close()
