@@ -635,6 +635,8 @@ int gs_destroy(gs_handle h) {
   if (h->x_used) (void)hipEventDestroy(h->x_used);
   if (h->rep) (void)hipHostFree(h->rep);
   if (h->h_flags) (void)hipHostFree(h->h_flags);
+  if (h->h_stage) (void)hipHostFree(h->h_stage);
+  if (h->h_wstage) (void)hipHostFree(h->h_wstage);
   if (h->h_text) (void)hipHostFree(h->h_text);
   if (h->h_tres) (void)hipHostFree(h->h_tres);
   for (void* p : {(void*)h->d_text, (void*)h->d_tsrc, (void*)h->d_tdst, h->d_tscratch, (void*)h->tab, (void*)h->ctr,
@@ -673,31 +675,63 @@ int gs_reset(gs_handle h) {
   return GS_OK;
 }
 
-// Host edges: each 2^20-edge chunk is copied by HIP straight from the caller's buffer
-// into a device staging buffer (pageable memory through HIP's own DMA staging, pinned
-// memory by DMA), then folded. No host-side staging memcpy: RMAT-26 edges from
-// pageable memory 2.06 -> 2.63 G edges/s, from pinned memory 1.38 -> 2.68 G edges/s
-// (tools/host_fold_rate.py). gs_fold's contract -- the caller may reuse its buffers
-// when the call returns -- is kept by waiting, at the end, for the last chunk's copies
-// (pageable copies have consumed their source on return already).
+// Host edges, in chunks of up to 2^20 edges into a device staging buffer (two,
+// alternating), then folded:
+//  * a chunk of at most kDirectCopyEdges is copied by HIP straight from the caller's
+//    buffer (no host-side memcpy): `--workload dropin` p = 8 (2^17-edge flushes)
+//    59-62 (pinned staging) -> 78-81 M edges/s;
+//  * a larger chunk is memcpy'd into pinned staging and copied by DMA. HIP's own
+//    pageable path blocked the caller for 8-28 ms per 2^20-edge flush of the drop-in
+//    operators (instrumented: all of it inside hipMemcpyAsync): p = 1 34-44 M edges/s
+//    with direct copies of every size, 70-73 with this split (same box, tools/dropin_ab.sh).
+//    Isolated 2^20-edge calls into an otherwise idle handle (tools/host_fold_rate.py) do
+//    better with direct copies (2.63 vs 1.85-1.96 G edges/s); the operators' pattern wins.
+// gs_fold's contract -- the caller may reuse its buffers when the call returns -- holds
+// either way: the pinned path has copied them, and the direct path waits at the end for
+// the last chunk's copies (pageable copies have consumed their source on return).
+constexpr size_t kDirectCopyEdges = 1u << 18;
+
+static int ensure_host_stage(gs_summary* h) {
+  if (h->h_stage) return GS_OK;
+  GS_HIP(hipHostMalloc(&h->h_stage, sizeof(int64_t) * 4 * kStageChunk, hipHostMallocDefault));
+  GS_HIP(hipHostMalloc(&h->h_wstage, 2 * kStageChunk, hipHostMallocDefault));
+  return GS_OK;
+}
+
 static int fold_host_impl(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n) {
+  bool direct_pending = false;
   for (size_t off = 0; off < n; off += kStageChunk) {
     const size_t c = std::min<size_t>(kStageChunk, n - off);
     const int b = h->stage_next;
     h->stage_next ^= 1;
     int64_t* ds = h->d_stage + (size_t)b * 2 * kStageChunk;
-    GS_HIP(hipMemcpyAsync(ds, src + off, c * 8, hipMemcpyHostToDevice, h->stream));
-    GS_HIP(hipMemcpyAsync(ds + kStageChunk, dst + off, c * 8, hipMemcpyHostToDevice, h->stream));
-    uint8_t* dwp = nullptr;
-    if (w) {
-      dwp = h->d_wstage + (size_t)b * kStageChunk;
-      GS_HIP(hipMemcpyAsync(dwp, w + off, c, hipMemcpyHostToDevice, h->stream));
+    uint8_t* dwp = w ? h->d_wstage + (size_t)b * kStageChunk : nullptr;
+    if (c <= kDirectCopyEdges) {
+      GS_HIP(hipMemcpyAsync(ds, src + off, c * 8, hipMemcpyHostToDevice, h->stream));
+      GS_HIP(hipMemcpyAsync(ds + kStageChunk, dst + off, c * 8, hipMemcpyHostToDevice, h->stream));
+      if (w) GS_HIP(hipMemcpyAsync(dwp, w + off, c, hipMemcpyHostToDevice, h->stream));
+      direct_pending = true;
+    } else {
+      if (int rc = ensure_host_stage(h)) return rc;
+      GS_HIP(hipEventSynchronize(h->stage_ev[b]));  // the pinned buffer's previous copy is done
+      int64_t* hs = h->h_stage + (size_t)b * 2 * kStageChunk;
+      memcpy(hs, src + off, c * 8);
+      memcpy(hs + kStageChunk, dst + off, c * 8);
+      GS_HIP(hipMemcpyAsync(ds, hs, c * 8, hipMemcpyHostToDevice, h->stream));
+      GS_HIP(hipMemcpyAsync(ds + kStageChunk, hs + kStageChunk, c * 8, hipMemcpyHostToDevice, h->stream));
+      if (w) {
+        uint8_t* hw = h->h_wstage + (size_t)b * kStageChunk;
+        memcpy(hw, w + off, c);
+        GS_HIP(hipMemcpyAsync(dwp, hw, c, hipMemcpyHostToDevice, h->stream));
+      }
+      direct_pending = false;
     }
     GS_HIP(hipEventRecord(h->stage_ev[b], h->stream));  // this chunk's copies
     int rc = fold_device_impl(h, ds, ds + kStageChunk, dwp, c, 1, 1, h->track);
     if (rc) return rc;
   }
-  if (n) GS_HIP(hipEventSynchronize(h->stage_ev[h->stage_next ^ 1]));  // the last chunk's copies
+  // a direct last chunk still reads the caller's buffer until its copies are done
+  if (direct_pending) GS_HIP(hipEventSynchronize(h->stage_ev[h->stage_next ^ 1]));
   return GS_OK;
 }
 

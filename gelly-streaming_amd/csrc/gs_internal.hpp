@@ -115,6 +115,8 @@ struct gs_summary {
   // staging for host folds
   int64_t* d_stage = nullptr;  // [2][2][kStageChunk]
   uint8_t* d_wstage = nullptr; // [2][kStageChunk]
+  int64_t* h_stage = nullptr;  // pinned, same shape: large host folds (allocated on first use)
+  uint8_t* h_wstage = nullptr;
   hipEvent_t stage_ev[2] = {nullptr, nullptr};  // after each buffer's copies
   int stage_next = 0;
   int64_t* d_scratch = nullptr;  // small scratch (find_one)

@@ -11,11 +11,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <vector>
 #include "gs_gen.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
-constexpr int kShift = 64 - 27;
+__constant__ int kShift;     // 64 - log2(table slots) (argv[1], default 27)
+__constant__ int kRegionShift;  // log2(slots) - 3: the top 3 slot bits pick the region
 __device__ __forceinline__ uint32_t slot_of(int64_t k) { return (uint32_t)(((uint64_t)k * 0x9E3779B97F4A7C15ull) >> kShift); }
 __device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 15u; }
 
@@ -32,7 +34,7 @@ __global__ void k_bucket(const int64_t* src, const int64_t* dst, uint32_t n, int
   if (i >= n) return;
   const int64_t k[2] = {src[i], dst[i]};
   for (int j = 0; j < 2; ++j) {
-    const uint32_t r = slot_of(k[j]) >> 24;
+    const uint32_t r = slot_of(k[j]) >> kRegionShift;
     const uint32_t p = atomicAdd(&bn[r], 1u);
     if (p < bcap) bk[(size_t)r * bcap + p] = k[j];
   }
@@ -77,9 +79,14 @@ __global__ void k_static(const uint4* tab, const int64_t* bk, uint32_t bcap, con
   if (threadIdx.x == 0) xcc_of_block[blockIdx.x] = xcc_id();
 }
 
-int main() {
+int main(int argc, char** argv) {
   setvbuf(stdout, nullptr, _IONBF, 0);
-  const uint64_t slots = 1ull << 27;
+  const int logs = argc > 1 ? atoi(argv[1]) : 27, scale = argc > 2 ? atoi(argv[2]) : 26;
+  const uint64_t slots = 1ull << logs;
+  const int sh = 64 - logs, rsh = logs - 3;
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(kShift), &sh, sizeof(int)));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(kRegionShift), &rsh, sizeof(int)));
+  printf("table 2^%d slots (%llu MiB), RMAT-%d micro-batches\n", logs, (unsigned long long)(slots * 16 >> 20), scale);
   const uint32_t B = 1u << 20, NB = 16, first = 500;
   uint4* tab;
   int64_t *src, *dst, *bk;
@@ -93,7 +100,9 @@ int main() {
   CK(hipMalloc(&bn, NB * 8 * 4));
   CK(hipMalloc(&cur, NB * 8 * 4));
   CK(hipMalloc(&sink, 64));
-  if (gs_gen_rmat(nullptr, src, dst, (uint64_t)first * B, (uint64_t)NB * B, 26, 0x5EED0026ull, 1)) return 1;
+  if (gs_gen_rmat(nullptr, src, dst, (uint64_t)(scale >= 24 ? first : 0) * B, (uint64_t)NB * B, scale,
+                  scale == 26 ? 0x5EED0026ull : 0x5EED0020ull, 1))
+    return 1;
   CK(hipMemset(bn, 0, NB * 8 * 4));
   for (uint32_t b = 0; b < NB; ++b)
     k_bucket<<<B / 256, 256>>>(src + (size_t)b * B, dst + (size_t)b * B, B, bk + (size_t)b * 8 * bcap, bcap, bn + b * 8);

@@ -91,7 +91,7 @@ os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
 with open(os.path.join(root, "profiles", "%s_rocprof_summary.json" % tag), "w") as f:
     json.dump(out, f, indent=1)
 # per-launch HBM traffic of the plain CC fold, read by bench.py for roofline.traffic
-plain = "k_fold<false, false>"
+plain = "k_fold<false, false, false>"  # <SIGNED, TRACK, TAKE>
 r = out["kernels"].get(plain, {})
 if "derived" in r and r["derived"].get("read_requests"):
     import hashlib
