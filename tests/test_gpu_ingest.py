@@ -104,3 +104,44 @@ def test_fold_text_rmat_chunks_and_malformed(gs, oracle_mod):
         ref.fold(b0, b1)
         ca, cb = c.colouring(), ref.colouring()
         assert ca[0] == cb[0] and all(np.array_equal(x, y) for x, y in zip(ca[1:], cb[1:]))
+
+
+@pytest.mark.parametrize("sep", [0, 1])
+def test_parse_window_boundaries_and_junk(gs, oracle_mod, sep):
+    """Lines around the fast parser's 48-byte register window (padded with leading
+    zeros and trailing fields to every length 1..80), signs, '\\r' placements and random
+    byte junk, each against the oracle's split + Long.parseLong restatement."""
+    rng = np.random.default_rng(11 + sep)
+    s = b"\t" if sep == 1 else b" "
+    lines = []
+    for L in range(1, 81):
+        for form in range(6):
+            a = b"-9223372036854775808" if form == 0 else b"%d" % int(rng.integers(-(10 ** 9), 10 ** 9))
+            b = b"9223372036854775807" if form == 1 else b"+%d" % int(rng.integers(0, 10 ** 12))
+            core = a + s + b
+            if form == 2:  # leading zeros up to the length
+                ln = b"0" * max(0, L - len(core)) + core
+            elif form == 3:  # ignored third field up to the length
+                ln = core + s + b"z" * max(0, L - len(core) - 1)
+            elif form == 4:  # '\r' before the end, or inside
+                ln = core + b"\r" if L % 2 else a + b"\r" + b
+            else:  # digits of field 1 up to the length (overflow past 19 digits)
+                ln = a + s + b"1" * max(1, L - len(a) - 1)
+            lines.append(ln)
+    junk = b"0123456789 \t\r+-x"
+    for _ in range(3000):
+        n = int(rng.integers(0, 60))
+        lines.append(bytes(junk[int(i)] for i in rng.integers(0, len(junk), n)))
+    rng.shuffle(lines)
+    for tail in (b"", b"\n"):
+        text = b"\n".join(lines) + tail
+        es, ed, en, eb = oracle_mod.parse_edges(text, sep)
+        got = _gpu_parse(gs, text, sep)
+        assert (got[2], got[3]) == (en, eb)
+        assert np.array_equal(got[0], es) and np.array_equal(got[1], ed)
+    # every line on its own (first-malformed index = 0 or none), incl. the text's end
+    for ln in lines[:400]:
+        es, ed, en, eb = oracle_mod.parse_edges(ln, sep)
+        got = _gpu_parse(gs, ln, sep)
+        assert (got[2], got[3]) == (en, eb), ln
+        assert np.array_equal(got[0], es) and np.array_equal(got[1], ed), ln
