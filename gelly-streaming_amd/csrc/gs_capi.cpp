@@ -775,7 +775,7 @@ int gs_num_vertices(gs_handle h, uint64_t* n) {
   DeviceGuard g(h->device);
   int rc = read_nv(h, n);
   if (rc) return rc;
-  return check_device_flags(h);
+  return check_flags_now(h);  // read_nv waited for the stream
 }
 
 int gs_find(gs_handle h, int64_t v, int64_t* label, int* found) {

@@ -9,12 +9,15 @@
 //   exclusive scan of the tile counts (hipcub) -> '\n' before each tile
 //   k_parse       : per tile, the tile (+ 512 B of the next) is staged in LDS; every
 //                   thread owns 32 bytes, finds the line starts in them (byte after a
-//                   '\n'), numbers each line from the tile prefix + a block scan, and
-//                   parses it with the Java split/parseLong rules: SWAR from LDS words
-//                   (parse_line_swar), or one byte per step for the tile's last line
-//                   and over-long fields; malformed lines -> atomicMin(bad).
-// RMAT-26 text (684 MB, 2^24 lines): k_count_lines 124 us (5.5 TB/s), k_parse 592 us
-// (771 us with the per-character parse; 197 us of it staging + line starts).
+//                   '\n') and their ends ('\n' masks of its and the next two segments
+//                   in LDS), numbers the lines from the tile prefix + a block scan, and
+//                   parses them with the Java split/parseLong rules: SWAR from LDS words
+//                   (parse_line_swar), or one byte per step for long lines / fields;
+//                   malformed lines -> atomicMin(bad).
+// RMAT-26 text (684 MB, 2^24 lines): k_count_lines 126 us (5.4 TB/s); k_parse 771 us with
+// a per-character parse of compacted line starts, 592 us with the SWAR parse, 370 us
+// with lines parsed by the thread whose segment they start in (no start list: 9.8 KB
+// instead of 25 KB of LDS, 42 instead of 73 VGPRs, 8 instead of 6 blocks per CU).
 #include <hipcub/hipcub.hpp>
 
 #include "gs_ingest.h"
@@ -188,13 +191,31 @@ __device__ __forceinline__ int parse_line_swar(const uint8_t* L, int s, int e, i
   return 1;
 }
 
+// '\n' mask (bit j: byte 32 q + j) of the 32-byte LDS segment q of the tile, with every
+// byte at or past the text's end `vend` (tile-relative, when the tile holds it) counted
+// as the end of the last line: bit vend set, bits above it cleared
+__device__ __forceinline__ uint32_t seg_nl_mask(const uint8_t* L, uint32_t q, uint64_t vend) {
+  const uint4 w0 = *reinterpret_cast<const uint4*>(L + 32 * q);
+  const uint4 w1 = *reinterpret_cast<const uint4*>(L + 32 * q + 16);
+  const uint32_t ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+  uint32_t nl = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) nl |= (((ww[k] >> (8 * bb)) & 0xFFu) == '\n' ? 1u : 0u) << (4 * k + bb);
+  const uint64_t b0 = 32ull * q;
+  if (vend < b0 + 32) nl = vend <= b0 ? (vend == b0 ? 1u : 0u) : ((nl & ((1u << (vend - b0)) - 1u)) | (1u << (vend - b0)));
+  return nl;
+}
+
 __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                                const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                                int64_t* __restrict__ dst, uint64_t cap,
                                                unsigned long long* __restrict__ bad, bool aligned) {
   constexpr uint32_t kSeg = kTile / 256;  // bytes per thread in the line-start scan
+  constexpr uint32_t kExtra = 2;          // '\n' masks past the tile: lines that cross its end
   __shared__ __align__(16) uint8_t lds[kLds0 + kTile + kOver];
-  __shared__ uint16_t starts[kTile];
+  __shared__ uint32_t nlm[256 + kExtra];
   __shared__ uint32_t wsum[4];
   const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
   const uint64_t staged_end = min(len, t0 + kTile + kOver);
@@ -223,21 +244,18 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
   put(f1, i1, v1);
   put(f2, i2, v2);
   __syncthreads();
-  // (1) line starts of the tile (byte p - 1 is '\n', or p == 0), compacted into LDS
-  //     in order with a block scan, so that lane i then parses line i in lockstep.
-  //     Each thread tests its 32-byte segment in registers (two ds_read_b128).
+  // (1) each thread's 32-byte segment: its '\n' mask (to LDS: a line's end may lie in a
+  //     later segment) and its line starts (byte p - 1 is '\n', or p == 0); a block
+  //     scan of the start counts numbers the lines.
   static_assert(kSeg == 32, "one 32-bit mask per thread");
+  const uint8_t* L = lds + kLds0;
   const uint32_t seg = threadIdx.x * kSeg;
   const uint64_t tile_end = min(len, t0 + kTile);
-  const uint4 w0 = *reinterpret_cast<const uint4*>(lds + kLds0 + seg);
-  const uint4 w1 = *reinterpret_cast<const uint4*>(lds + kLds0 + seg + 16);
-  const uint32_t ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-  uint32_t nl = 0;  // bit j: byte seg + j is '\n'
-#pragma unroll
-  for (int k = 0; k < 8; ++k)
-#pragma unroll
-    for (int bb = 0; bb < 4; ++bb) nl |= (((ww[k] >> (8 * bb)) & 0xFFu) == '\n' ? 1u : 0u) << (4 * k + bb);
-  uint32_t mine = (nl << 1) | (lds[kLds0 - 1 + seg] == '\n' ? 1u : 0u);  // bit j: a line starts at seg + j
+  const uint64_t vend = staged_end == len ? len - t0 : ~0ull;  // the text ends inside the staged bytes
+  const uint32_t nl = seg_nl_mask(L, threadIdx.x, vend);
+  nlm[threadIdx.x] = nl;
+  if (threadIdx.x < kExtra) nlm[256 + threadIdx.x] = seg_nl_mask(L, 256 + threadIdx.x, vend);
+  uint32_t mine = (nl << 1) | (L[(int)seg - 1] == '\n' ? 1u : 0u);  // bit j: a line starts at seg + j
   const uint64_t valid = t0 + seg >= tile_end ? 0 : min<uint64_t>(kSeg, tile_end - (t0 + seg));
   if (valid < 32) mine &= (1u << valid) - 1u;
   const uint32_t c = __popc(mine);
@@ -250,35 +268,40 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
   }
   if (lane == 63) wsum[wid] = x;
   __syncthreads();
-  uint32_t wbase = 0, total = 0;
-  for (int q = 0; q < 4; ++q) {
+  uint32_t wbase = 0;
+  for (int q = 0; q < 4; ++q)
     if (q < wid) wbase += wsum[q];
-    total += wsum[q];
-  }
-  uint32_t k = wbase + (x - c);
+  // (2) each thread parses the lines that start in its segment (usually one); the k-th
+  //     start of the tile follows k '\n' of the tile if a line starts at t0, else k + 1
+  uint64_t line = tile_pre[blockIdx.x] + (L[-1] == '\n' ? 0u : 1u) + wbase + (x - c);
+  const LineBuf b{lds, text, t0, len, staged_end};
   while (mine) {
     const uint32_t j = __ffs(mine) - 1;
     mine &= mine - 1;
-    starts[k++] = (uint16_t)(seg + j);
-  }
-  __syncthreads();
-  // (2) the k-th start follows k '\n' of the tile if a line starts at t0, else k + 1
-  const uint64_t line0 = tile_pre[blockIdx.x] + (lds[kLds0 - 1] == '\n' ? 0u : 1u);
-  const LineBuf b{lds, text, t0, len, staged_end};
-  for (uint32_t i = threadIdx.x; i < total; i += 256u) {
-    const uint64_t line = line0 + i;
-    const uint32_t so = starts[i];
-    uint64_t q = t0 + so;
-    int64_t a = 0, d = 0;
-    // the '\n' of every line but the tile's last is the byte before the next start
-    int r = -1;
-    if (i + 1 < total) {
-      const int e = (int)starts[i + 1] - 1;
-      r = sep == GS_SEP_TAB ? parse_line_swar<GS_SEP_TAB>(lds + kLds0, (int)so, e, a, d)
-                            : parse_line_swar<GS_SEP_WHITESPACE>(lds + kLds0, (int)so, e, a, d);
+    const int so = (int)(seg + j);
+    // the line's '\n': the first one at or after its start, within this segment or
+    // the next two (longer lines take the per-character path)
+    int e = -1;
+    const uint32_t own = nl & (0xFFFFFFFFu << j);
+    if (own) {
+      e = (int)seg + __builtin_ctz(own);
+    } else {
+      const uint32_t n1 = nlm[threadIdx.x + 1];
+      if (n1) {
+        e = (int)seg + 32 + __builtin_ctz(n1);
+      } else {
+        const uint32_t n2 = nlm[threadIdx.x + 2];
+        if (n2) e = (int)seg + 64 + __builtin_ctz(n2);
+      }
     }
+    uint64_t q = t0 + (uint64_t)so;
+    int64_t a = 0, d = 0;
+    int r = -1;
+    if (e >= 0)
+      r = sep == GS_SEP_TAB ? parse_line_swar<GS_SEP_TAB>(L, so, e, a, d)
+                            : parse_line_swar<GS_SEP_WHITESPACE>(L, so, e, a, d);
     bool ok = r == 1;
-    if (r < 0) {  // the tile's last line, or a field of more than 23 bytes: one byte per step
+    if (r < 0) {  // a long line or field: one byte per step
       // two fields: the first must end at a separator (else fields[1] does not exist)
       ok = parse_long(b, q, sep, a) == kFieldSep;
       if (ok) {
@@ -292,6 +315,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
       src[line] = a;
       dst[line] = d;
     }
+    ++line;
   }
 }
 
