@@ -345,8 +345,9 @@ int join_lanes(gs_summary* h) {
 
 // Host wait for h->stream: k_signal queued behind everything, then a spin on its
 // host-mapped word (6.5 vs 12.2 us for hipStreamSynchronize after a short kernel,
-// tools/calib_launch.hip). A wait that outlasts kSpinWait (a long fold queue) hands
-// over to hipStreamSynchronize, which also surfaces asynchronous HIP errors.
+// tools/calib_launch.hip). A wait that outlasts kSpinWait (a fold queue, not a small
+// window) hands over to hipStreamSynchronize, which also surfaces asynchronous HIP
+// errors and leaves the core to other threads (N emulated ranks in one process).
 int wait_stream(gs_summary* h, const uint32_t* vals, uint64_t* value, int nvals, int stride) {
   if (!vals && hipStreamQuery(h->stream) == hipSuccess) return GS_OK;  // already idle (0.6 us, no launch)
   const unsigned long long seq = ++h->done_seq;
@@ -359,7 +360,7 @@ int wait_stream(gs_summary* h, const uint32_t* vals, uint64_t* value, int nvals,
 
 // Spin until the completion word reaches seq (its writer is queued on h->stream).
 int wait_done(gs_summary* h, unsigned long long seq) {
-  constexpr auto kSpinWait = std::chrono::milliseconds(20);
+  constexpr auto kSpinWait = std::chrono::microseconds(250);
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t i = 1;; ++i) {
     if (__atomic_load_n(h->h_done, __ATOMIC_ACQUIRE) >= seq) return GS_OK;
