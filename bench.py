@@ -280,7 +280,12 @@ def bench_er_latency(args):
     summ.sync()
     lat = []
     nrec = 0
-    ps, pd = src.data_ptr(), dst.data_ptr()  # window addresses as the JNI caller passes them (no tensor views)
+    # the C ABI called as the JNI glue calls it: raw addresses, arguments prepared once
+    import ctypes
+    ps, pd, prec, pcnt = src.data_ptr(), dst.data_ptr(), rec.data_ptr(), cnt.data_ptr()
+    take = gs.lib().gs_fold_take_device
+    k_host = ctypes.c_uint64()
+    k_ref = ctypes.byref(k_host)
     for step in range(args.warmup + 1):
         summ.reset()
         lat = []
@@ -288,10 +293,12 @@ def bench_er_latency(args):
         for o in range(0, E, B):
             t0 = time.perf_counter()
             # one window: fold (tracked) + delta records into device memory + completion
-            # (gs_fold_take_device: a single launch that signals the host, DESIGN.md section 7)
-            k = summ.fold_take(ps + 8 * o, pd + 8 * o, B, rec, cap, cnt)
+            # (gs_fold_take_device: a single launch that signals the host, DESIGN.md section 3)
+            rc = take(summ._h, ps + 8 * o, pd + 8 * o, B, prec, cap, pcnt, k_ref)
             lat.append(time.perf_counter() - t0)
-            nrec += k
+            if rc:
+                raise gs.GSError(rc, gs.lib().gs_last_error().decode())
+            nrec += k_host.value
     lat = np.array(lat) * 1e6
     tot = lat.sum() * 1e-6
     import oracle  # CPU baseline leg only: the 1-thread restatement on the first 64 windows

@@ -48,3 +48,22 @@ def test_connected_components_example_default_stream():
     with open(os.path.join(ROOT, "tests", "golden", "derived.json")) as f:
         golden = json.load(f)["cc_default_stream"]["emissions"]
     assert r.stdout.strip().splitlines() == golden
+
+
+@pytest.mark.parametrize("p", [1, 8])
+def test_dropin_operators_partitions_match_oracle(oracle_mod, tmp_path, p):
+    """the unchanged operators (SummaryBulkAggregation.run ->
+    UpdateCC per edge, a pooled fresh partial per (partition, window), CombineCC of the
+    partials, Merger into the running summary; S/SummaryBulkAggregation.java:68-130,
+    S/library/ConnectedComponents.java:83-126) at p = 1 and p = 8 partitions over an
+    RMAT-16 stream in 2^14-edge windows: the final labels equal the oracle's."""
+    import numpy as np
+    out = tmp_path / "labels.bin"
+    r = _run("dropin_bench", "16", "0x5EED0016", "20", "14", str(p), str(out))
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["partitions"] == p and res["windows"] == 64
+    lab = np.fromfile(out, dtype=np.int64).reshape(-1, 2)
+    s, d = oracle_mod.rmat_edges(0x5EED0016, 16, 0, 1 << 20, True)
+    ov, olab = oracle_mod.cc_labels(s, d)
+    assert np.array_equal(lab[:, 0], ov) and np.array_equal(lab[:, 1], olab)
