@@ -731,7 +731,9 @@ static int fold_host_impl(gs_handle h, const int64_t* src, const int64_t* dst, c
     int rc = fold_device_impl(h, ds, ds + kStageChunk, dwp, c, 1, 1, h->track);
     if (rc) return rc;
   }
-  // a direct last chunk still reads the caller's buffer until its copies are done
+  // a direct last chunk still reads the caller's buffer until its copies are done (only
+  // the last chunk can be direct: every earlier one has kStageChunk > kDirectCopyEdges edges)
+  static_assert(kStageChunk > kDirectCopyEdges, "direct copies only for a call's last chunk");
   if (direct_pending) GS_HIP(hipEventSynchronize(h->stage_ev[h->stage_next ^ 1]));
   return GS_OK;
 }
@@ -1051,6 +1053,7 @@ int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, siz
   if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
   if (!count_dev || !count || (cap && !rec)) return fail(GS_ERR_INVALID, "null argument");
   if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
+  if (h->side) return fail(GS_ERR_INVALID, "a group's summary exchanges its delta: no window take");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
   auto* cd = reinterpret_cast<unsigned long long*>(count_dev);
