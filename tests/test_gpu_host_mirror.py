@@ -50,6 +50,28 @@ def test_connected_components_example_default_stream():
     assert r.stdout.strip().splitlines() == golden
 
 
+def test_window_latency_driver_through_c_abi(gs, oracle_mod):
+    """host/examples/window_latency.cpp (config 5 through gs_fold_take_device alone, no
+    Python) on a small ER stream: every window completes, and the records taken name
+    at least every vertex merge the oracle sees (records >= vertices - components)."""
+    import numpy as np
+    import torch
+    logn, loge, logw = 14, 17, 10
+    r = _run("window_latency", str(logn), str(loge), str(logw))
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["windows"] == 1 << (loge - logw) and res["window_edges"] == 1 << logw
+    assert 0 < res["p50_us"] <= res["p99_us"] <= res["max_us"]
+    E = 1 << loge
+    src = torch.empty(E, dtype=torch.int64, device="cuda")
+    dst = torch.empty(E, dtype=torch.int64, device="cuda")
+    gs.gen_er(src, dst, 0, E, logn, 0x5EED00E5, True)
+    torch.cuda.synchronize()
+    hs, hd = src.cpu().numpy(), dst.cpu().numpy()
+    ov, olab = oracle_mod.cc_labels(hs, hd)
+    assert len(ov) - len(np.unique(olab)) <= res["delta_records"] <= 3 * E
+
+
 @pytest.mark.parametrize("p", [1, 8])
 def test_dropin_operators_partitions_match_oracle(oracle_mod, tmp_path, p):
     """the unchanged operators (SummaryBulkAggregation.run ->
