@@ -5,19 +5,19 @@
 // (ConnectedComponentsExample.java:109-118, BipartitenessCheckExample.java:97-106).
 //
 // Two launches + one scan, all HBM-streaming:
-//   k_count_lines : per 8 KiB tile, the number of '\n' (coalesced 16-B loads)
+//   k_count_lines : per 16 KiB tile, the number of '\n' (coalesced 16-B loads)
 //   exclusive scan of the tile counts (hipcub) -> '\n' before each tile
 //   k_parse       : per tile, the tile (+ 512 B of the next) is staged in LDS; every
-//                   thread owns 32 bytes, finds the line starts in them (byte after a
+//                   thread owns 64 bytes, finds the line starts in them (byte after a
 //                   '\n') and their ends ('\n' masks of its and the next two segments
 //                   in LDS), numbers the lines from the tile prefix + a block scan, and
 //                   parses them with the Java split/parseLong rules: SWAR from LDS words
 //                   (parse_line_swar), or one byte per step for long lines / fields;
 //                   malformed lines -> atomicMin(bad).
-// RMAT-26 text (684 MB, 2^24 lines): k_count_lines 126 us (5.4 TB/s); k_parse 771 us with
-// a per-character parse of compacted line starts, 592 us with the SWAR parse, 370 us
-// with lines parsed by the thread whose segment they start in (no start list: 9.8 KB
-// instead of 25 KB of LDS, 42 instead of 73 VGPRs, 8 instead of 6 blocks per CU).
+// RMAT-26 text (684 MB, 2^24 lines): k_count_lines 120-133 us (5.4 TB/s); k_parse 771 us
+// with a per-character parse of compacted line starts, 592 us with the SWAR parse, 370 us
+// with lines parsed by the thread whose 32-byte segment they start in (no start list),
+// 338-354 us with 16 KiB tiles (five 16-B loads in flight per thread instead of three).
 #include <hipcub/hipcub.hpp>
 
 #include "gs_ingest.h"
@@ -25,7 +25,7 @@
 
 namespace gs {
 
-constexpr uint32_t kTile = 8192;   // bytes per parse block (32 per thread in the start scan)
+constexpr uint32_t kTile = 16384;  // bytes per parse block (64 per thread in the start scan)
 constexpr uint32_t kOver = 512;    // bytes of the next tile staged for lines crossing the end
 
 __device__ __forceinline__ bool is_sep(uint8_t c, int sep) {
@@ -214,51 +214,58 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
                                                unsigned long long* __restrict__ bad, bool aligned) {
   constexpr uint32_t kSeg = kTile / 256;  // bytes per thread in the line-start scan
   constexpr uint32_t kExtra = 2;          // '\n' masks past the tile: lines that cross its end
+  constexpr uint32_t kSlots = (kTile + kOver + 4095) / 4096;
+  static_assert(kSeg == 64 && kSlots == 5, "one 64-bit mask and five staging slots per thread");
+  static_assert(kExtra * kSeg <= kOver, "the extra masks lie in the staged bytes");
   __shared__ __align__(16) uint8_t lds[kLds0 + kTile + kOver];
-  __shared__ uint32_t nlm[256 + kExtra];
+  __shared__ uint64_t nlm[256 + kExtra];
   __shared__ uint32_t wsum[4];
   const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
   const uint64_t staged_end = min(len, t0 + kTile + kOver);
   // stage [t0, staged_end) at lds[kLds0..] with 16-B stores; lds[kLds0 - 1] = byte t0 - 1.
-  // Every thread's global loads are issued before any is waited for.
+  // Every thread's global loads (five 16-B slots, 4 KiB apart) are issued before any is
+  // waited for; named registers, not an array (an indexed array of them went to scratch).
   if (threadIdx.x == 0) lds[kLds0 - 1] = t0 == 0 ? (uint8_t)'\n' : text[t0 - 1];
-  // three 16-B slots per thread (4 KiB apart); named registers, not an array: an
-  // indexed array of them went to scratch
-  static_assert(kTile + kOver <= 3 * 4096, "three staging slots per thread");
-  const uint32_t i0 = threadIdx.x * 16u, i1 = i0 + 4096u, i2 = i0 + 8192u;
-  const bool f0 = aligned && t0 + i0 + 16 <= staged_end;
-  const bool f1 = aligned && t0 + i1 + 16 <= staged_end;
-  const bool f2 = aligned && i2 < kTile + kOver && t0 + i2 + 16 <= staged_end;
-  uint4 v0 = {}, v1 = {}, v2 = {};
+  const uint32_t i0 = threadIdx.x * 16u;
+  auto full = [&](uint32_t i) { return aligned && i < kTile + kOver && t0 + i + 16 <= staged_end; };
+  const bool f0 = full(i0), f1 = full(i0 + 4096u), f2 = full(i0 + 8192u), f3 = full(i0 + 12288u),
+             f4 = full(i0 + 16384u);
+  uint4 v0 = {}, v1 = {}, v2 = {}, v3 = {}, v4 = {};
   if (f0) v0 = *reinterpret_cast<const uint4*>(text + t0 + i0);
-  if (f1) v1 = *reinterpret_cast<const uint4*>(text + t0 + i1);
-  if (f2) v2 = *reinterpret_cast<const uint4*>(text + t0 + i2);
-  auto put = [&](bool full, uint32_t i, const uint4& v) {
-    if (full) {
+  if (f1) v1 = *reinterpret_cast<const uint4*>(text + t0 + i0 + 4096u);
+  if (f2) v2 = *reinterpret_cast<const uint4*>(text + t0 + i0 + 8192u);
+  if (f3) v3 = *reinterpret_cast<const uint4*>(text + t0 + i0 + 12288u);
+  if (f4) v4 = *reinterpret_cast<const uint4*>(text + t0 + i0 + 16384u);
+  auto put = [&](bool f, uint32_t i, const uint4& v) {
+    if (f) {
       *reinterpret_cast<uint4*>(lds + kLds0 + i) = v;
     } else if (i < kTile + kOver) {  // the text's end (or an unaligned text): byte by byte
       for (uint64_t q = t0 + i; q < t0 + i + 16 && q < staged_end; ++q) lds[kLds0 + (q - t0)] = text[q];
     }
   };
   put(f0, i0, v0);
-  put(f1, i1, v1);
-  put(f2, i2, v2);
+  put(f1, i0 + 4096u, v1);
+  put(f2, i0 + 8192u, v2);
+  put(f3, i0 + 12288u, v3);
+  put(f4, i0 + 16384u, v4);
   __syncthreads();
-  // (1) each thread's 32-byte segment: its '\n' mask (to LDS: a line's end may lie in a
+  // (1) each thread's 64-byte segment: its '\n' mask (to LDS: a line's end may lie in a
   //     later segment) and its line starts (byte p - 1 is '\n', or p == 0); a block
   //     scan of the start counts numbers the lines.
-  static_assert(kSeg == 32, "one 32-bit mask per thread");
   const uint8_t* L = lds + kLds0;
   const uint32_t seg = threadIdx.x * kSeg;
   const uint64_t tile_end = min(len, t0 + kTile);
   const uint64_t vend = staged_end == len ? len - t0 : ~0ull;  // the text ends inside the staged bytes
-  const uint32_t nl = seg_nl_mask(L, threadIdx.x, vend);
+  auto mask64 = [&](uint32_t q) {
+    return (uint64_t)seg_nl_mask(L, 2 * q, vend) | ((uint64_t)seg_nl_mask(L, 2 * q + 1, vend) << 32);
+  };
+  const uint64_t nl = mask64(threadIdx.x);
   nlm[threadIdx.x] = nl;
-  if (threadIdx.x < kExtra) nlm[256 + threadIdx.x] = seg_nl_mask(L, 256 + threadIdx.x, vend);
-  uint32_t mine = (nl << 1) | (L[(int)seg - 1] == '\n' ? 1u : 0u);  // bit j: a line starts at seg + j
+  if (threadIdx.x < kExtra) nlm[256 + threadIdx.x] = mask64(256 + threadIdx.x);
+  uint64_t mine = (nl << 1) | (L[(int)seg - 1] == '\n' ? 1ull : 0ull);  // bit j: a line starts at seg + j
   const uint64_t valid = t0 + seg >= tile_end ? 0 : min<uint64_t>(kSeg, tile_end - (t0 + seg));
-  if (valid < 32) mine &= (1u << valid) - 1u;
-  const uint32_t c = __popc(mine);
+  if (valid < 64) mine &= (1ull << valid) - 1ull;
+  const uint32_t c = __popcll(mine);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t x = c;
 #pragma unroll
@@ -271,27 +278,27 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
   uint32_t wbase = 0;
   for (int q = 0; q < 4; ++q)
     if (q < wid) wbase += wsum[q];
-  // (2) each thread parses the lines that start in its segment (usually one); the k-th
-  //     start of the tile follows k '\n' of the tile if a line starts at t0, else k + 1
+  // (2) each thread parses the lines that start in its segment; the k-th start of the
+  //     tile follows k '\n' of the tile if a line starts at t0, else k + 1
   uint64_t line = tile_pre[blockIdx.x] + (L[-1] == '\n' ? 0u : 1u) + wbase + (x - c);
   const LineBuf b{lds, text, t0, len, staged_end};
   while (mine) {
-    const uint32_t j = __ffs(mine) - 1;
+    const uint32_t j = __ffsll((unsigned long long)mine) - 1;
     mine &= mine - 1;
     const int so = (int)(seg + j);
     // the line's '\n': the first one at or after its start, within this segment or
     // the next two (longer lines take the per-character path)
     int e = -1;
-    const uint32_t own = nl & (0xFFFFFFFFu << j);
+    const uint64_t own = nl & (~0ull << j);
     if (own) {
-      e = (int)seg + __builtin_ctz(own);
+      e = (int)seg + __builtin_ctzll(own);
     } else {
-      const uint32_t n1 = nlm[threadIdx.x + 1];
+      const uint64_t n1 = nlm[threadIdx.x + 1];
       if (n1) {
-        e = (int)seg + 32 + __builtin_ctz(n1);
+        e = (int)seg + 64 + __builtin_ctzll(n1);
       } else {
-        const uint32_t n2 = nlm[threadIdx.x + 2];
-        if (n2) e = (int)seg + 64 + __builtin_ctz(n2);
+        const uint64_t n2 = nlm[threadIdx.x + 2];
+        if (n2) e = (int)seg + 128 + __builtin_ctzll(n2);
       }
     }
     uint64_t q = t0 + (uint64_t)so;
