@@ -145,3 +145,40 @@ def test_parse_window_boundaries_and_junk(gs, oracle_mod, sep):
         got = _gpu_parse(gs, ln, sep)
         assert (got[2], got[3]) == (en, eb), ln
         assert np.array_equal(got[0], es) and np.array_equal(got[1], ed), ln
+
+
+def _text_with_newline_at(pos, end):
+    """Lines "0..01 2" (zero-padded to 30-80 bytes) whose newlines include byte `pos`;
+    the text is cut at `end` bytes (its last line may lack a newline)."""
+    out, k = bytearray(), 0
+
+    def line(n):  # n bytes before the newline
+        out.extend(b"0" * (n - 3) + b"1 2\n")
+
+    while pos - len(out) > 80:
+        k += 1
+        line(30 + (k * 7) % 21)
+    line(pos - len(out))  # 30..80 bytes: its newline is byte pos
+    while len(out) < end:
+        k += 1
+        line(30 + (k * 7) % 21)
+    return bytes(out[:end])
+
+
+@pytest.mark.parametrize("sep", [0, 1])
+def test_parse_newlines_at_tile_edges(gs, oracle_mod, sep):
+    """A newline at every byte around the parser's tile edges (8 and 16 KiB multiples,
+    and the 512 bytes of the next tile it stages), and texts that end there with and
+    without a last newline: line count, values and first malformed line vs the oracle."""
+    for base in (8192, 16384, 16384 + 512, 32768, 49152):
+        for d in range(-3, 4):
+            pos = base + d
+            for end in (pos, pos + 1, pos + 700):
+                text = _text_with_newline_at(pos, end)
+                if sep == 1:
+                    text = text.replace(b" ", b"\t")
+                assert end <= pos or text[pos] == 10
+                es, ed, en, eb = oracle_mod.parse_edges(text, sep)
+                got = _gpu_parse(gs, text, sep)
+                assert (got[2], got[3]) == (en, eb), (base, d, end)
+                assert np.array_equal(got[0], es) and np.array_equal(got[1], ed), (base, d, end)
