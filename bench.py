@@ -186,6 +186,25 @@ def bench_bip(args):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    # roofline of the signed k_fold (one GPU): HIP events around every launch over one extra
+    # serialised step, the same 48 B/edge algorithmic bytes as the CC fold (the parity rides
+    # in the link word); no PMC profile of this workload, so traffic is null
+    roof = None
+    if group is None and not args.no_profile_pass:
+        summ.set_profiling(True)
+        one_step()
+        summ.sync()
+        nf, fold_ms = summ.kernel_stats("fold")
+        summ.set_profiling(False)
+        fold_avg_ms = fold_ms / max(nf, 1)
+        per_launch = per / max(nf, 1)
+        achieved = BYTES_PER_EDGE_SPARSE * per_launch / (fold_avg_ms * 1e-3) / 1e9
+        step_gbs = BYTES_PER_EDGE_SPARSE * per / (el / args.steps) / 1e9
+        roof = {"kernel": "k_fold (signed)", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "achieved_step": round(step_gbs, 1), "frac_step": round(step_gbs / HBM_PEAK_GBS, 4),
+                "bytes_per_edge": BYTES_PER_EDGE_SPARSE, "edges_per_launch": int(per_launch),
+                "fold_avg_us": round(fold_avg_ms * 1e3, 2), "fold_launches": int(nf)}
     # odd-cycle variant (outside the timed region)
     inject = [E // 8, E // 4, E // 2, 3 * E // 4]
     gs.gen_bip(src, dst, start, per, logside, seed, [i for i in inject if start <= i < start + per],
@@ -253,6 +272,8 @@ def bench_bip(args):
                                  "sample": "first %d edges of the odd-cycle stream, Candidates.merge per edge "
                                            "(quirk-exact restatement, O(E x components)), 1 thread, %.2f s"
                                            % (cap, cpu_secs)}}
+        if roof is not None:
+            line["roofline"] = roof
         print(json.dumps(line), flush=True)
     if group is not None:
         group.close()
