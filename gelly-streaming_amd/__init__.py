@@ -208,7 +208,10 @@ class Summary:
         _check(lib().gs_fold(self._h, s.ctypes.data, d.ctypes.data, len(s)))
 
     def fold_device(self, src, dst, n=None, stride=1, w=None):
-        """Fold device-resident edges (torch tensors on this device or raw pointers)."""
+        """Fold device-resident edges (torch tensors on this device or raw pointers).
+        The fold is queued on the summary's stream (`self.stream`), not torch's: edges
+        written by torch kernels must be complete first (torch.cuda.synchronize(), or
+        that stream made to wait), as for any caller of gs_fold_device."""
         if n is None:
             n = src.numel() // (stride if stride > 1 else 1) if hasattr(src, "numel") else None
         _check(lib().gs_fold_device(self._h, _ptr(src), _ptr(dst), _ptr(w), int(n), int(stride)))
