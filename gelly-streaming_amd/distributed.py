@@ -53,6 +53,7 @@ class DeltaExchangeFold:
         self.count = torch.zeros((2, 1), dtype=torch.int64, device=self.dev)
         self.counts = torch.zeros((2, self.world), dtype=torch.int64, device=self.dev)
         if self.cuda:
+            torch.cuda.synchronize(self.dev)  # the fills ran on torch's stream; stages write on the summary's
             self.stream = torch.cuda.ExternalStream(summary.stream, device=self.dev)
             self.ev_staged = [torch.cuda.Event() for _ in range(2)]
             self.ev_data = [torch.cuda.Event() for _ in range(2)]

@@ -97,6 +97,7 @@ def test_config5_er_windows_with_delta_records(gs, oracle_mod):
     torch.cuda.synchronize()
     rec = torch.empty((B, 3), dtype=torch.int64, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # filled on torch's stream; the library writes on the summary's
     checkpoints = {1, 8, 64, E // B}
     with gs.Summary("cc", capacity_hint=1 << logn) as s, gs.Summary("cc", capacity_hint=1 << logn) as rep:
         s.set_delta_tracking(True)

@@ -295,6 +295,7 @@ def test_delta_exchange_reproduces_union(gs, oracle_mod):
     cap = 3 * B
     recs = [torch.empty((cap, 3), dtype=torch.int64, device="cuda") for _ in range(2)]
     cnts = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()  # filled on torch's stream; the library writes on the summary's
     total = 0
     for i in range(0, len(s), 2 * B):
         reps[0].fold(s[i:i + B], d[i:i + B])
@@ -322,6 +323,7 @@ def _stage_and_gather(gs, reps, width):
     cap = reps[0].delta_capacity()
     sends = [torch.empty((cap, width), dtype=torch.int64, device="cuda") for _ in range(world)]
     counts = torch.zeros(world, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # filled on torch's stream; the library writes on the summary's
     for r in range(world):
         reps[r].delta_stage(sends[r], cap, counts[r:r + 1], width)
         reps[r].sync()
@@ -595,6 +597,7 @@ def test_delta_list_full_error_leaves_capacity_tracking_intact(gs, oracle_mod):
         cap = s.delta_capacity()
         rec = torch.empty((cap, 3), dtype=torch.int64, device="cuda")
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()  # filled on torch's stream; the library writes on the summary's
         refused, worst, o = 0, 0.0, 0
         while o < n:
             t0 = time.perf_counter()

@@ -26,6 +26,7 @@ def test_fused_window_take_matches_oracle_and_replays(gs, oracle_mod, logn, logb
     torch.cuda.synchronize()
     rec = torch.empty((B, 3), dtype=torch.int64, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # filled on torch's stream; the library writes on the summary's
     hs, hd = src.cpu().numpy(), dst.cpu().numpy()
     ps, pd = src.data_ptr(), dst.data_ptr()
     with gs.Summary("cc", capacity_hint=1 << logn) as s, gs.Summary("cc", capacity_hint=1 << logn) as rep:
@@ -60,6 +61,7 @@ def test_fused_window_take_self_loops_and_growth(gs, oracle_mod):
     dst = torch.from_numpy(hd).cuda()
     rec = torch.empty((B, 3), dtype=torch.int64, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # filled on torch's stream; the library writes on the summary's
     with gs.Summary("cc", capacity_hint=1) as s, gs.Summary("cc", capacity_hint=1) as rep:
         s.set_delta_tracking(True)
         for o in range(0, n, B):
@@ -86,6 +88,7 @@ def test_fused_window_take_signed_verdict(gs, oracle_mod):
     assert first >= 0
     rec = torch.empty((B, 3), dtype=torch.int64, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # filled on torch's stream; the library writes on the summary's
     with gs.Summary("signed", capacity_hint=1 << 13) as c, gs.Summary("signed", capacity_hint=1 << 13) as rep:
         c.set_delta_tracking(True)
         for o in range(0, E, B):
@@ -109,6 +112,7 @@ def test_fused_window_take_truncates_and_counts(gs):
     cap = 100
     rec = torch.full((cap + 8, 3), -7, dtype=torch.int64, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # filled on torch's stream; the library writes on the summary's
     with gs.Summary("cc", capacity_hint=1 << 14) as s:
         s.set_delta_tracking(True)
         k = s.fold_take(src, dst, n, rec, cap, cnt)
@@ -131,6 +135,7 @@ def test_fused_window_take_includes_pending_records(gs, oracle_mod):
     B = 1 << 10
     rec = torch.empty((2 * B, 3), dtype=torch.int64, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # filled on torch's stream; the library writes on the summary's
     with gs.Summary("cc", capacity_hint=1 << 13) as s, gs.Summary("cc", capacity_hint=1 << 13) as rep:
         s.set_delta_tracking(True)
         s.fold_device(src[:B], dst[:B], n=B)  # tracked, not taken
