@@ -109,6 +109,7 @@ def test_config5_er_windows_with_delta_records(gs, oracle_mod):
             k = int(cnt.item())
             assert k <= B  # at most one record per folded edge
             rep.fold_records(rec, k)  # the records alone rebuild the summary
+            rep.sync()  # rec is reused by the next take
             if w + 1 in checkpoints:
                 v1, l1 = s.labels()
                 v2, l2 = rep.labels()

@@ -308,6 +308,7 @@ def test_delta_exchange_reproduces_union(gs, oracle_mod):
         total += sum(ns)
         for k in range(2):
             reps[1 - k].fold_records(recs[k], ns[k], track=False)
+            reps[1 - k].sync()  # rec is reused by the next take
     for r in reps:
         _assert_cc_equal(r, oracle_mod, s, d)
         r.close()

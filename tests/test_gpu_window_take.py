@@ -38,6 +38,7 @@ def test_fused_window_take_matches_oracle_and_replays(gs, oracle_mod, logn, logb
             assert k == int(cnt.item()) and 0 <= k <= B
             total += k
             rep.fold_records(rec, k)
+            rep.sync()  # rec is reused by the next take
             if w + 1 in (1, 2, 7, E // B):
                 ov, olab = oracle_mod.cc_labels(hs[:o + B], hd[:o + B])
                 v, lab = s.labels()
@@ -67,6 +68,7 @@ def test_fused_window_take_self_loops_and_growth(gs, oracle_mod):
         for o in range(0, n, B):
             k = s.fold_take(src[o:], dst[o:], B, rec, B, cnt)
             rep.fold_records(rec, k)
+            rep.sync()  # rec is reused by the next take
         ov, olab = oracle_mod.cc_labels(hs, hd)
         v, lab = s.labels()
         assert np.array_equal(v, ov) and np.array_equal(lab, olab)
@@ -97,6 +99,7 @@ def test_fused_window_take_signed_verdict(gs, oracle_mod):
                 assert k == 0  # a failed verdict is final: nothing folds, nothing recorded
             if first >= o + B:
                 rep.fold_records(rec, k)
+                rep.sync()  # rec is reused by the next take
                 assert rep.ok()
             assert c.ok() == (first >= o + B), (o, first)
 
@@ -141,8 +144,10 @@ def test_fused_window_take_includes_pending_records(gs, oracle_mod):
         s.fold_device(src[:B], dst[:B], n=B)  # tracked, not taken
         k = s.fold_take(src[B:], dst[B:], B, rec, 2 * B, cnt)
         rep.fold_records(rec, k)
+        rep.sync()  # rec is reused by the next take
         k = s.fold_take(src[2 * B:], dst[2 * B:], B, rec, 2 * B, cnt)
         rep.fold_records(rec, k)
+        rep.sync()  # rec is reused by the next take
         ov, olab = oracle_mod.cc_labels(hs, hd)
         v, lab = rep.labels()
         assert np.array_equal(v, ov) and np.array_equal(lab, olab)

@@ -85,7 +85,7 @@ def run_case(seed, diag=False, partials=True):
     hint = int(2 ** rng.uniform(0, 21))
     depth = int(rng.integers(1, 5))
     ts, td = torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()
-    mode = rng.choice(["plain", "reset", "combine", "serialize"])
+    mode = rng.choice(["plain", "reset", "combine", "serialize", "take"])
     key = "%s/%s/%s n=%d hint=%d depth=%d" % (kind, fam, mode, len(s), hint, depth)
     cut = None
     with gs.Summary(kind, capacity_hint=hint) as summ:
@@ -115,6 +115,23 @@ def run_case(seed, diag=False, partials=True):
                     print("cut", cut, "restored exact", check(kind, restored, s[:cut], d[:cut]), flush=True)
                 fold_all(rng, restored, s[cut:], d[cut:], ts[cut:], td[cut:])
                 return key, len(s), check(kind, restored, s, d)
+        elif mode == "take":  # latency-path windows (fold + take in one launch), replayed elsewhere
+            summ.set_delta_tracking(True)
+            w = int(2 ** rng.uniform(0, 16))
+            cap = w + 16  # at most one record per folded edge
+            rec = torch.empty((cap, 3), dtype=torch.int64, device="cuda")
+            cnt = torch.empty(1, dtype=torch.int64, device="cuda")
+            with gs.Summary(kind, capacity_hint=hint) as rep:
+                for o in range(0, len(s), w):
+                    got = summ.fold_take(ts[o:], td[o:], min(w, len(s) - o), rec, cap, cnt)
+                    if got > cap:
+                        return key, len(s), False
+                    rep.fold_records(rec, got)
+                    rep.sync()  # rec is reused by the next take
+                # a failed verdict travels in no record (an odd cycle closes inside one tree):
+                # the replica is compared while the stream is bipartite
+                if (kind == "cc" or summ.ok()) and not check(kind, rep, s, d):
+                    return key, len(s), False
         else:
             fold_all(rng, summ, s, d, ts, td)
         good = check(kind, summ, s, d)
