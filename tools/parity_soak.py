@@ -117,7 +117,7 @@ def run_case(seed, diag=False, partials=True):
                 return key, len(s), check(kind, restored, s, d)
         elif mode == "take":  # latency-path windows (fold + take in one launch), replayed elsewhere
             summ.set_delta_tracking(True)
-            w = int(2 ** rng.uniform(0, 16))
+            w = max(int(2 ** rng.uniform(0, 16)), len(s) >> 12)  # at most 4096 windows per case
             cap = w + 16  # at most one record per folded edge
             rec = torch.empty((cap, 3), dtype=torch.int64, device="cuda")
             cnt = torch.empty(1, dtype=torch.int64, device="cuda")
