@@ -9,12 +9,17 @@ min id of its component, written to HBM). Edges are generated into HBM before th
 timed region (each rank its own contiguous 1/N shard of the 2^30-edge stream).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--scale 26] [--log-batch 20]
-N > 1 is launched by torch.distributed.run (one process per GPU, RCCL).
+N > 1 runs one process per GPU (RCCL). Under torch.distributed.run the ranks come
+from the environment; without WORLD_SIZE, `--gpus N` starts the N ranks itself as a
+child torch.distributed.run (before anything touches the GPU) and relays rank 0's
+line. Every rank refuses to run unless the world that formed is exactly N.
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -98,7 +103,69 @@ def parse():
                    help="relabel-table capacity hint of the CC summary (log2 vertices; 0: 2^scale)")
     p.add_argument("--exchange-impl", choices=["native", "torch"], default="native",
                    help="native: RCCL inside libgs_summary (gs_group_*); torch: torch.distributed all-gather")
+    p.add_argument("--launch-check", action="store_true",
+                   help="launcher test (CPU, gloo): form the world exactly as the bench does, print one JSON line "
+                        "with the world that formed, touch no GPU")
     return p.parse_args()
+
+
+MULTI_RANK_WORKLOADS = ("rmat-cc", "bip")
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args):
+    """`--gpus N > 1` without a launcher: start N ranks as a CHILD torch.distributed.run
+    (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE from it) and return its exit code;
+    rank 0's JSON line reaches this process's stdout unchanged. None when this process
+    is a rank itself (WORLD_SIZE set) or N = 1. Runs before anything initialises HIP:
+    the parent never touches the GPU (device_count() does not initialise it)."""
+    if os.environ.get("WORLD_SIZE") or args.gpus <= 1:
+        return None
+    if args.workload not in MULTI_RANK_WORKLOADS:
+        raise SystemExit("--workload %s is single-GPU; --gpus %d refused" % (args.workload, args.gpus))
+    if not args.launch_check:
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            raise SystemExit("--gpus %d but only %d GPU(s) visible: refusing to measure fewer" % (args.gpus, have))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver (RCCL)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_world(args):
+    """(world, rank, local_rank) from the launcher; exits non-zero unless the world that
+    formed is exactly --gpus (a 1-rank world never stands in for N GPUs)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but the world that formed has %d rank(s)" % (args.gpus, world))
+    return world, rank, local
+
+
+def launch_check(args):
+    """CPU rehearsal of the multi-rank launch (tests/test_bench_launch.py): gloo process
+    group, world counted by an all-reduce, one JSON line on rank 0."""
+    world, rank, _ = check_world(args)
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        formed = int(t.item())
+        dist.destroy_process_group()
+    else:
+        formed = 1
+    if formed != args.gpus:
+        raise SystemExit("--gpus %d but %d rank(s) joined" % (args.gpus, formed))
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": formed, "workload": args.workload}), flush=True)
 
 
 class NativeExchange:
@@ -128,9 +195,9 @@ def bench_bip(args):
     replica's final verdict must equal the truth (the remote half of a window lands one exchange
     late, so a per-window flip is only defined at one GPU)."""
     import gsamd as gs
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = check_world(args)
+    if local >= torch.cuda.device_count():
+        raise SystemExit("rank %d: LOCAL_RANK %d but %d GPU(s) visible" % (rank, local, torch.cuda.device_count()))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     grouped = world > 1 or args.exchange
@@ -450,6 +517,12 @@ def bench_dropin(args):
 
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:  # this process only launched the ranks
+        sys.exit(rc)
+    if args.launch_check:
+        return launch_check(args)
+    world, rank, local = check_world(args)
     if args.workload == "dropin":
         return bench_dropin(args)
     if args.workload == "ingest":
@@ -458,11 +531,8 @@ def main():
         return bench_bip(args)
     if args.workload == "er-latency":
         return bench_er_latency(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if local >= torch.cuda.device_count():
+        raise SystemExit("rank %d: LOCAL_RANK %d but %d GPU(s) visible" % (rank, local, torch.cuda.device_count()))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1 or args.exchange:

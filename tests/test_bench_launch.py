@@ -1,0 +1,68 @@
+"""bench.py's multi-rank launch on CPU (gloo): `--gpus N` without a launcher starts N
+ranks itself and relays rank 0's line; a world that is not N is refused (VERDICT r2
+item 2). `--launch-check` forms the world exactly as the bench does and touches no GPU."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    return env
+
+
+def _last_json(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert lines, out
+    return json.loads(lines[-1])
+
+
+def test_self_launch_two_ranks():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check"], env=_env(), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 2 and line["launch_check"]
+    # exactly one line: only rank 0 prints
+    assert sum(ln.startswith("{") for ln in r.stdout.splitlines()) == 1
+
+
+def test_self_launch_bip_workload():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--workload", "bip", "--launch-check"], env=_env(),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _last_json(r.stdout)["n_gpus"] == 2
+
+
+def test_world_mismatch_is_refused():
+    # a rank that finds itself in a 1-rank world while --gpus says 2 must not print a line
+    env = _env()
+    env.update({"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode != 0
+    assert "world that formed" in r.stderr
+    assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
+
+
+def test_single_gpu_workload_refuses_many_gpus():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--workload", "er-latency", "--launch-check"],
+                       env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "single-GPU" in r.stderr
+
+
+def test_no_gpu_visible_refuses_before_launch():
+    # without --launch-check the parent counts GPUs first: none in this container
+    import torch
+    if torch.cuda.device_count() >= 2:
+        return
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1"], env=_env(), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode != 0 and "GPU(s) visible" in r.stderr
+    assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
