@@ -48,7 +48,10 @@ EXPORTED_SYMBOLS = (
     "gs_group_fold_batches_device", "gs_group_set_ramp", "gs_export_labels_part_device",
     "gs_delta_capacity", "gs_find_labels_device", "gs_capacity_stats",
     "gs_set_change_tracking", "gs_take_changes_device", "gs_take_changes",
+    "gs_fold_records_counted_device", "gs_reset_config", "gs_wait_event", "gs_wait_stream", "gs_fold_device_after",
 )
+
+FAIL_BIT = 1 << 62  # count words: a failed signed verdict (GS_FAIL_BIT)
 
 
 class GSError(RuntimeError):
@@ -88,8 +91,12 @@ def lib():
     L.gs_create.argtypes = [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int, _u64]
     L.gs_destroy.argtypes = [_vp]
     L.gs_reset.argtypes = [_vp]
+    L.gs_reset_config.argtypes = [_vp]
     L.gs_fold.argtypes = [_vp, _vp, _vp, _sz]
     L.gs_fold_device.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz]
+    L.gs_fold_device_after.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp]
+    L.gs_wait_event.argtypes = [_vp, _vp]
+    L.gs_wait_stream.argtypes = [_vp, _vp]
     L.gs_combine.argtypes = [_vp, _vp]
     L.gs_sync.argtypes = [_vp]
     L.gs_num_vertices.argtypes = [_vp, ctypes.POINTER(_u64)]
@@ -104,6 +111,7 @@ def lib():
     L.gs_take_delta_records.argtypes = [_vp, _vp, _sz, _vp]
     L.gs_fold_take_device.argtypes = [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp]
     L.gs_fold_records_device.argtypes = [_vp, _vp, _sz, ctypes.c_int]
+    L.gs_fold_records_counted_device.argtypes = [_vp, _vp, _sz, _vp, ctypes.c_int]
     L.gs_delta_stage.argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
     L.gs_fold_exchange_device.argtypes = [_vp, _vp, _vp, _sz, _sz, ctypes.c_int, ctypes.c_int]
     L.gs_delta_capacity.argtypes = [_vp, ctypes.POINTER(_u64)]
@@ -196,6 +204,11 @@ class Summary:
     def reset(self):
         _check(lib().gs_reset(self._h))
 
+    def reset_config(self):
+        """gs_reset_config: reset plus the default configuration (tracking off,
+        pipelining 1, profiling off), as a handle pool's release does."""
+        _check(lib().gs_reset_config(self._h))
+
     def sync(self):
         _check(lib().gs_sync(self._h))
 
@@ -207,14 +220,33 @@ class Summary:
         assert s.shape == d.shape
         _check(lib().gs_fold(self._h, s.ctypes.data, d.ctypes.data, len(s)))
 
-    def fold_device(self, src, dst, n=None, stride=1, w=None):
+    def fold_device(self, src, dst, n=None, stride=1, w=None, after=None):
         """Fold device-resident edges (torch tensors on this device or raw pointers).
         The fold is queued on the summary's stream (`self.stream`), not torch's: edges
-        written by torch kernels must be complete first (torch.cuda.synchronize(), or
-        that stream made to wait), as for any caller of gs_fold_device."""
+        written on another stream must be complete first -- pass that stream as
+        `after` (a torch.cuda.Stream, or "torch" for torch's current stream; the
+        summary's work then waits for it on the device, gs_wait_stream), or
+        synchronise, as for any caller of gs_fold_device."""
         if n is None:
             n = src.numel() // (stride if stride > 1 else 1) if hasattr(src, "numel") else None
+        if after is not None:
+            self.wait_stream(after)
         _check(lib().gs_fold_device(self._h, _ptr(src), _ptr(dst), _ptr(w), int(n), int(stride)))
+
+    def wait_stream(self, stream="torch"):
+        """Every later operation of the summary waits (on the device) for the work queued
+        on `stream` so far: a torch.cuda.Stream, a raw hipStream_t, or "torch" (torch's
+        current stream). gs_wait_stream."""
+        if isinstance(stream, str):
+            import torch
+            stream = torch.cuda.current_stream(self.device)
+        raw = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+        _check(lib().gs_wait_stream(self._h, raw))
+
+    def wait_event(self, event):
+        """Every later operation waits for a recorded torch.cuda.Event (or raw hipEvent_t)."""
+        raw = event.cuda_event if hasattr(event, "cuda_event") else int(event)
+        _check(lib().gs_wait_event(self._h, raw))
 
     def combine(self, other):
         _check(lib().gs_combine(self._h, other._h))
@@ -353,11 +385,13 @@ class Summary:
         """One latency-path window (gs_fold_take_device): fold n device edges (tracked),
         take the records since the previous take into `rec` (device int64 [cap, 3]) and
         their count into `count` (device int64 [1]); returns the count once the window
-        is complete."""
+        is complete. The full count word (| FAIL_BIT once a signed verdict failed) is
+        kept in `last_take_word`: replay it with fold_records(rec, last_take_word)."""
         c = _u64()
         _check(lib().gs_fold_take_device(self._h, _ptr(src), _ptr(dst), int(n), _ptr(rec), int(cap), _ptr(count),
                                          ctypes.byref(c)))
-        return c.value
+        self.last_take_word = c.value
+        return c.value & (FAIL_BIT - 1)
 
     def delta_stage(self, send, cap, count, width=3):
         """Stage every pending record into `send` (device int64 [cap, width]) and the
@@ -373,8 +407,14 @@ class Summary:
                                              int(skip_rank)))
 
     def fold_records(self, rec, n, track=False):
-        """Fold n device records {a, b, w} (another replica's delta)."""
+        """Fold n device records {a, b, w} (another replica's delta). n may be a take's
+        count word: FAIL_BIT ANDs a failed verdict into this summary."""
         _check(lib().gs_fold_records_device(self._h, _ptr(rec), int(n), 1 if track else 0))
+
+    def fold_records_counted(self, rec, cap, count, track=False):
+        """Replay a take with its count word read on the device (`count`: device int64
+        [1] as the take wrote it; at most `cap` rows): no host round trip."""
+        _check(lib().gs_fold_records_counted_device(self._h, _ptr(rec), int(cap), _ptr(count), 1 if track else 0))
 
     # --- introspection
     @property

@@ -81,10 +81,12 @@ void drain_profile(gs_summary* h) {
   h->prof_pending.clear();
 }
 
-// Order the handle's stream behind every fold still running on a lane.
+// Order the handle's stream behind every fold still running on a lane (every lane
+// that exists: pipelined folds use lanes 0..pipe_depth-1, a group's own folds lanes
+// 0..2, whatever the handle's pipelining depth).
 int join_pipe_lanes(gs_summary* h) {
   if (!h->lanes_dirty) return GS_OK;
-  for (int i = 0; i < h->pipe_depth; ++i) {
+  for (int i = 0; i < gs_summary::kLanes && h->lane[i]; ++i) {
     GS_HIP(hipEventRecord(h->lane_ev[i], h->lane[i]));
     GS_HIP(hipStreamWaitEvent(h->stream, h->lane_ev[i], 0));
   }
@@ -270,7 +272,7 @@ int ensure_capacity(gs_summary* h, size_t n) {
   // for reports below is then only back-pressure with enough folds queued to keep the
   // GPU busy, instead of a drain before every fold (RMAT-20, config 2: 1.07 -> 0.72
   // ms/step).
-  const uint64_t slack = 2ull * n * (uint64_t)(std::max(1, h->pipe_depth) + 1);
+  const uint64_t slack = 2ull * n * (uint64_t)(std::max({1, h->pipe_depth, h->group_lanes}) + 1);
   const bool slack_grow = h->cap < kSlackGrowMaxCap && (double)(h->nv_exact + slack) > limit;
   if (!slack_grow) {
     // wait for reports of the folds in flight (the GPU keeps working: no drain)
@@ -603,7 +605,8 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   for (int i = 0; i < 2; ++i)
     if (hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming) != hipSuccess)
       return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
-  if (hipEventCreateWithFlags(&h->main_ev, hipEventDisableTiming) != hipSuccess)
+  if (hipEventCreateWithFlags(&h->main_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ext_ev, hipEventDisableTiming) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
   memset(h->h_flags, 0, 16);
   if (hipHostMalloc(&h->rep, gs_summary::kRepRing * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -627,6 +630,7 @@ int gs_destroy(gs_handle h) {
     if (h->lane[i]) (void)hipStreamDestroy(h->lane[i]);
   }
   if (h->main_ev) (void)hipEventDestroy(h->main_ev);
+  if (h->ext_ev) (void)hipEventDestroy(h->ext_ev);
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 2; ++i) {
     if (h->stage_ev[i]) (void)hipEventDestroy(h->stage_ev[i]);
@@ -674,6 +678,23 @@ int gs_reset(gs_handle h) {
   reset_capacity_tracking(h, 0);
   for (uint64_t& f : h->delta_fill_ub) f = 0;
   return GS_OK;
+}
+
+int gs_reset_config(gs_handle h) {
+  if (int rc = check(h)) return rc;
+  if (h->side) return fail(GS_ERR_INVALID, "the summary belongs to an exchange group: destroy the group first");
+  DeviceGuard g(h->device);
+  if (int rc = join_lanes(h)) return rc;
+  if (h->changes)
+    if (int rc = gs_set_change_tracking(h, 0)) return rc;
+  if (h->track)
+    if (int rc = gs_set_delta_tracking(h, 0)) return rc;
+  h->changes_own_track = false;
+  if (h->profiling)
+    if (int rc = gs_set_profiling(h, 0)) return rc;
+  h->pipe_depth = 1;
+  h->lane_next = 0;
+  return gs_reset(h);
 }
 
 // Host edges, in chunks of up to 2^20 edges into a device staging buffer (two,
@@ -756,13 +777,63 @@ int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const ui
   return fold_device_impl(h, src, dst, w, n, stride, 1, h->track, true, fs);
 }
 
+// Cross-stream ordering for producers on other streams: every
+// later fold of the handle starts behind the producer's work. Folds run on the handle
+// stream, on pipelining lanes that wait for an event recorded on the handle stream at
+// each fold, or on a group's own-fold lanes that do the same at each call -- so one
+// wait on the handle stream orders all of them.
+int gs_wait_event(gs_handle h, void* event) {
+  if (int rc = check(h)) return rc;
+  if (!event) return fail(GS_ERR_INVALID, "null event");
+  DeviceGuard g(h->device);
+  GS_HIP(hipStreamWaitEvent(h->stream, static_cast<hipEvent_t>(event), 0));
+  return GS_OK;
+}
+
+int gs_wait_stream(gs_handle h, void* stream) {
+  if (int rc = check(h)) return rc;
+  DeviceGuard g(h->device);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (st == h->stream) return GS_OK;
+  GS_HIP(hipEventRecord(h->ext_ev, st));  // (stream 0 = the device's null stream)
+  GS_HIP(hipStreamWaitEvent(h->stream, h->ext_ev, 0));
+  return GS_OK;
+}
+
+int gs_fold_device_after(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
+                         size_t stride, void* ready) {
+  if (int rc = check(h)) return rc;
+  if (ready)
+    if (int rc = gs_wait_event(h, ready)) return rc;
+  return gs_fold_device(h, src, dst, w, n, stride);
+}
+
 int gs_fold_records_device(gs_handle h, const int64_t* rec, size_t n, int track) {
   if (int rc = check(h)) return rc;
+  // n may be a take's count word: bit 62 carries a failed signed verdict, which the
+  // replay ANDs into this summary before folding the rows (Candidates.merge :79-81)
+  const bool failed = (n & gs::kFailBit) != 0;
+  n &= gs::kFailBit - 1;
   if (n && !rec) return fail(GS_ERR_INVALID, "null records");
   if (track && !h->drec) return fail(GS_ERR_INVALID, "delta tracking was never enabled");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
+  if (failed && h->kind == GS_KIND_SIGNED)
+    GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_FAIL), 1, 1, h->stream));
   return fold_device_impl(h, rec, rec + 1, reinterpret_cast<const uint8_t*>(rec + 2), n, 3, 24, track != 0);
+}
+
+int gs_fold_records_counted_device(gs_handle h, const int64_t* rec, size_t cap, const uint64_t* count_dev, int track) {
+  if (int rc = check(h)) return rc;
+  if (!count_dev || (cap && !rec)) return fail(GS_ERR_INVALID, "null argument");
+  if (track && !h->drec) return fail(GS_ERR_INVALID, "delta tracking was never enabled");
+  DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
+  FoldSource fs;
+  fs.n_dev = reinterpret_cast<const unsigned long long*>(count_dev);  // rows (<= cap) and the verdict bit
+  // at least one thread reads the verdict of a failed window with no rows
+  const size_t n = std::max<size_t>(cap, h->kind == GS_KIND_SIGNED ? 1 : 0);
+  return fold_device_impl(h, rec, rec + 1, reinterpret_cast<const uint8_t*>(rec + 2), n, 3, 24, track != 0, true, fs);
 }
 
 int gs_sync(gs_handle h) {
@@ -1044,7 +1115,7 @@ int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count
   if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  return stage_delta(h, rec, cap, 3, reinterpret_cast<unsigned long long*>(count), false);
+  return stage_delta(h, rec, cap, 3, reinterpret_cast<unsigned long long*>(count), h->kind == GS_KIND_SIGNED);
 }
 
 int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, size_t n, int64_t* rec, size_t cap,
@@ -1063,8 +1134,9 @@ int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, siz
   const bool fused = n > 0 && n <= kMaxChunk && h->delta_fill_ub[h->dset] == 0 && !h->changes && !h->profiling;
   if (!fused) {
     if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, true)) return rc;
-    if (int rc = stage_delta(h, rec, cap, 3, cd, false)) return rc;
-    if (int rc = wait_stream(h, reinterpret_cast<const uint32_t*>(cd), count)) return rc;  // rows < 2^32
+    if (int rc = stage_delta(h, rec, cap, 3, cd, h->kind == GS_KIND_SIGNED)) return rc;
+    // the whole count word (rows | kFailBit) handed over with the wait
+    if (int rc = wait_stream(h, reinterpret_cast<const uint32_t*>(cd), count, -1)) return rc;
     return check_flags_now(h);
   }
   FoldSource fs;

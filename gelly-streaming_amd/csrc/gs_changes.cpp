@@ -101,11 +101,17 @@ int gs_set_change_tracking(gs_handle h, int on) {
   DeviceGuard g(h->device);
   if (int rc = join_lanes(h)) return rc;
   if (!on) {
+    if (h->changes && h->changes_own_track) {  // the delta tracking it turned on goes with it
+      h->changes = false;
+      h->changes_own_track = false;
+      return gs_set_delta_tracking(h, 0);
+    }
     h->changes = false;
     return GS_OK;
   }
   if (h->changes) return GS_OK;
   if (h->side) return fail(GS_ERR_INVALID, "a group's summary exchanges its delta: no change tracking");
+  h->changes_own_track = !h->track;
   if (!h->track)
     if (int rc = gs_set_delta_tracking(h, 1)) return rc;
   uint64_t nv = 0;
@@ -163,7 +169,13 @@ int gs_take_changes_device(gs_handle h, int64_t* v, int64_t* label, uint8_t* par
   uint64_t emitted = 0;  // (low word of the u64 counter: rows < 2^32)
   if (int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_EMIT), &emitted)) return rc;
   *n = emitted;
-  if (emitted > cap) return fail(GS_ERR_TRUNCATED, "emission rows above cap");
+  if (emitted > cap) {
+    // the emission's side effects (spliced lists, cleared new bits, advanced marks)
+    // happened: rows past cap cannot be emitted again by a retry, so the next take
+    // emits every vertex
+    h->chg_scan_all = true;
+    return fail(GS_ERR_TRUNCATED, "emission rows above cap");
+  }
   return GS_OK;
 }
 

@@ -473,6 +473,7 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
     h->side = g->as;
     h->side_ev = g->as_ev;
     h->side_dirty = false;
+    h->group_lanes = kGroupLanes;
   }
   typedef int (*InitRank)(void**, int, Id128, int);
   Id128 uid;
@@ -509,11 +510,11 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   // remote folds all run on other streams, so own folds go back to back.
   const bool lanes = !h->profiling && !g->no_lanes;  // (profiling serialises folds on the handle stream)
   if (lanes) {
-    if (h->pipe_depth < kGroupLanes) h->pipe_depth = kGroupLanes;
-    if (b == 0) {  // the lanes start behind the caller's earlier work (reset, previous folds)
-      GS_HIP(hipEventRecord(h->main_ev, h->stream));
-      for (int i = 0; i < kGroupLanes; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], h->main_ev, 0));
-    }
+    // Every call: the lanes start behind the caller's work on the handle stream (a reset,
+    // edges written there, a buffer reused after a sync through it), as gs_fold_device
+    // is ordered after it -- not only at the first exchange.
+    GS_HIP(hipEventRecord(h->main_ev, h->stream));
+    for (int i = 0; i < kGroupLanes; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], h->main_ev, 0));
     if (b >= (uint64_t)gs::kDeltaSets)
       for (int i = 0; i < kGroupLanes; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], g->staged[d], 0));
   } else if (b >= (uint64_t)gs::kDeltaSets) {
@@ -752,9 +753,11 @@ int gs_group_destroy(gs_group_t g) {
   if (g->as) {
     (void)hipStreamSynchronize(g->as);
     if (g->h->side == g->as) {
+      (void)join_lanes(g->h);  // (joins the side stream while it still exists)
       g->h->side = nullptr;
       g->h->side_ev = nullptr;
       g->h->side_dirty = false;
+      g->h->group_lanes = 0;
     }
     (void)hipStreamDestroy(g->as);
   }

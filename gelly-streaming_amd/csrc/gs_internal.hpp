@@ -103,6 +103,7 @@ struct gs_summary {
   uint64_t delta_fill_ub[gs::kDeltaSets] = {};  // worst-case per-shard fill of each set since its last stage
   // change tracking (gs_changes.cpp)
   bool changes = false;
+  bool changes_own_track = false;  // change tracking turned delta tracking on (and turns it off)
   uint32_t* nxt = nullptr;  // [cap + 1] circular member lists
   uint64_t nxt_slots = 0;
   unsigned long long* chg_scratch = nullptr;  // emission scratch: count, marks, big roots, staged records
@@ -141,10 +142,12 @@ struct gs_summary {
   // over lane streams so that fold b+1 may start while fold b drains; every other
   // entry point joins the lanes onto `stream` first (join_lanes)
   int pipe_depth = 1;
+  int group_lanes = 0;  // own-fold lanes of an exchange group using this summary (0: none)
   static constexpr int kLanes = 4;
   hipStream_t lane[kLanes] = {};
   hipEvent_t lane_ev[kLanes] = {};
   hipEvent_t main_ev = nullptr;
+  hipEvent_t ext_ev = nullptr;  // gs_wait_stream: recorded on a producer's stream
   int lane_next = 0;
   bool lanes_dirty = false;
   // side stream (a multi-GPU group's apply stream): folds of remote rows run there,

@@ -101,7 +101,8 @@ struct FoldArgs {
   int skip_rank;      // block whose rows are skipped (the caller's own)
   const unsigned long long* counts;  // exchange layout: live rows of block r (| kFailBit)
   uint32_t base;      // index of this launch's first element (chunked launches)
-  const unsigned long long* n_dev;   // optional: device element count (valid: base + i < *n_dev)
+  const unsigned long long* n_dev;   // optional: device count word (valid: base + i < low 62 bits;
+                                     // bit 62 = kFailBit, a failed verdict the SIGNED fold ANDs in)
   const uint32_t* fail_in;           // optional: failure flag of a combined summary (SIGNED)
   uint32_t shard0;    // first shard of this launch (rotates per launch: balanced shard fill)
   // fused window take (TAKE): rows -> take_out[take_cap][3], count -> *take_count; the
@@ -124,7 +125,10 @@ constexpr int kCombineRounds = 2;  // wave-level hook combining (combine_hooks)
 // completion word (system scope) that the host spins on. The table writes need no
 // fence: the next kernel of the stream starts after this one's end-of-kernel release,
 // and only the rows and the count are read before that (by the host or other streams).
-__device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, const int64_t* lrec, uint32_t lcnt) {
+// A signed summary's count word carries the verdict (| kFailBit once it failed): the
+// take's consumer replays the records AND the verdict (Candidates.merge :79-81).
+__device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, const int64_t* lrec, uint32_t lcnt,
+                                          bool signed_kind) {
   __shared__ unsigned long long base_sh;
   __shared__ uint32_t last_sh;
   const uint32_t nb = min(lcnt, kFoldBS);
@@ -156,13 +160,17 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
   if (threadIdx.x != 0) return;
   unsigned long long* take = reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE));
   const unsigned long long total = __hip_atomic_load(take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  *a.take_count = total;
+  // every block's verdict updates are memory-side atomics that preceded its ticket; the
+  // flag is read at the memory side too (an atomic), never from a possibly stale line
+  const bool failed = signed_kind && atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 0u) != 0u;
+  const unsigned long long word = total | (failed ? kFailBit : 0ull);
+  *a.take_count = word;
   atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_SENT)), total < a.take_cap ? total : a.take_cap);
   __hip_atomic_store(take, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(t.ctr + ctr_index(CTR_TAKE_DONE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __threadfence_system();
   __hip_atomic_store(a.done + 1, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(a.done + 2, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(a.done + 2, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(a.done, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -176,7 +184,13 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
     if (threadIdx.x == 0) lcnt = 0;
     __syncthreads();
   }
-  if (SIGNED && a.fail_in && blockIdx.x == 0 && threadIdx.x == 0 && *a.fail_in)
+  // Counts and flags written on another stream (a copy, a collective, another summary's
+  // export) are read with agent-scope loads: never from a line an XCD's L2 may hold.
+  unsigned long long n_word = 0;
+  if (a.n_dev) n_word = __hip_atomic_load(a.n_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (SIGNED && blockIdx.x == 0 && threadIdx.x == 0 &&
+      ((a.fail_in && __hip_atomic_load(a.fail_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ||
+       (n_word & kFailBit)))
     atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);  // the verdict is the AND (Candidates.java:79-81)
   // a failed verdict is final: no more work (a TAKE block still reaches its ticket)
   const bool failed = SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0;
@@ -184,10 +198,10 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
   const int shard = (int)((blockIdx.x + a.shard0) & (kShards - 1));
   const uint32_t i = blockIdx.x * kFoldBS + threadIdx.x;
   bool valid = i < a.n && !failed;
-  if (valid && a.n_dev) valid = (unsigned long long)(a.base + i) < *a.n_dev;
+  if (valid && a.n_dev) valid = (unsigned long long)(a.base + i) < (n_word & (kFailBit - 1));
   if (valid && a.rows) {  // exchange layout: the block's count word gives its live rows
     const uint32_t ig = a.base + i, r = ig / a.rows, j = ig - r * a.rows;
-    const unsigned long long cw = a.counts[r];
+    const unsigned long long cw = __hip_atomic_load(a.counts + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (SIGNED && j == 0 && (cw & kFailBit) && (int)r != a.skip_rank) atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);
     valid = (int)r != a.skip_rank && (unsigned long long)j < (cw & (kFailBit - 1));
   }
@@ -246,7 +260,7 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
   if (act) hook<SIGNED, TRACK, TAKE>(t, D, shard, ru, ru << 1, kru, rv, rv << 1, krv, need);
   if (TAKE) {
     __syncthreads();
-    take_tail(t, a, lrec, lcnt);
+    take_tail(t, a, lrec, lcnt, SIGNED);
   }
 }
 
@@ -461,6 +475,8 @@ __global__ __launch_bounds__(64) void k_headers(const unsigned long long* __rest
 __global__ __launch_bounds__(64) void k_signal(unsigned long long* out, unsigned long long seq, const uint32_t* vals,
                                                int nvals, int stride) {
   unsigned long long v = (vals && (int)threadIdx.x < nvals) ? vals[(size_t)threadIdx.x * stride] : 0ull;
+  if (nvals < 0)  // one u64 word (a count word with its flag bits) instead of u32 counters
+    v = (vals && threadIdx.x == 0) ? *reinterpret_cast<const unsigned long long*>(vals) : 0ull;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   if (threadIdx.x != 0) return;

@@ -114,7 +114,8 @@ class HandlePool {
     return h;
   }
   void release(gs_handle h, int kind, int device, uint64_t capacity_hint) {
-    if (gs_reset(h) != GS_OK) {  // a broken handle is not pooled
+    // the value AND the configuration (tracking, pipelining, profiling) of a fresh handle
+    if (gs_reset_config(h) != GS_OK) {  // a broken handle is not pooled
       gs_destroy(h);
       return;
     }

@@ -41,6 +41,9 @@ enum gs_status {
   GS_ERR_TRUNCATED = -4 /* output buffer too small; *n holds the required count */
 };
 
+/* Count words (delta takes, exchange stages) carry a failed signed verdict in bit 62. */
+#define GS_FAIL_BIT (1ull << 62)
+
 enum gs_kind {
   GS_KIND_CC = 0,     /* DisjointSet (DisjointSet.java:25-151) via ConnectedComponents */
   GS_KIND_SIGNED = 1  /* Candidates (Candidates.java:27-196) via BipartitenessCheck  */
@@ -68,6 +71,12 @@ int gs_destroy(gs_handle h);
  * (only the touched slots are re-initialised). */
 int gs_reset(gs_handle h);
 
+/* gs_reset plus the handle's default configuration: delta and change tracking off,
+ * pipelining depth 1, profiling off -- a pooled handle handed to the next summary
+ * behaves as a fresh gs_create (the per-window initial-value copy, INTEGRATION.md
+ * HandlePool). Not for a group's summary (destroy the group first). */
+int gs_reset_config(gs_handle h);
+
 /* Fold n edges from HOST memory: for each i, union(src[i], dst[i]).
  * Replaces UpdateCC.foldEdges -> DisjointSet.union (ConnectedComponents.java:83-86,
  * DisjointSet.java:92-118) and updateFunction.foldEdges ->
@@ -84,8 +93,21 @@ int gs_fold(gs_handle h, const int64_t* src, const int64_t* dst, size_t n);
  * interleaved pairs). `w` (device, optional, may be NULL) gives the required colour
  * parity per edge for GS_KIND_SIGNED (1 = different sides, the edge default;
  * 0 = same side, used when a serialized/exported summary is merged back). The
- * caller guarantees the inputs are complete before work on the handle's stream. */
+ * inputs must be complete before work on the handle's stream: written on that
+ * stream (gs_get_stream), synchronised, or ordered with gs_wait_event /
+ * gs_wait_stream / gs_fold_device_after below. */
 int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n, size_t stride);
+
+/* Cross-stream ordering for callers whose edges are produced on another stream (a
+ * decoder, a copy engine, torch): gs_wait_event makes every later operation of the
+ * handle wait for `event` (a hipEvent_t the producer recorded); gs_wait_stream for
+ * all work queued on `stream` (a hipStream_t) so far. No host synchronisation.
+ * gs_fold_device_after = gs_wait_event(ready) (skipped when ready is NULL) +
+ * gs_fold_device. Pipelined folds and a group's own folds are ordered too. */
+int gs_wait_event(gs_handle h, void* event);
+int gs_wait_stream(gs_handle h, void* stream);
+int gs_fold_device_after(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
+                         size_t stride, void* ready);
 
 /* Pipelined windows: with depth d (1..4), up to d consecutive gs_fold_device calls
  * may run concurrently on the device (fold b+1 starts while fold b drains), the way Flink
@@ -182,17 +204,24 @@ int gs_deserialize(gs_handle h, const void* buf, size_t len);
  *
  * gs_take_delta_records packs the delta accumulated since the previous take into
  * DEVICE records {a, b, w} (24 bytes; w bit 0 = parity, w bit 7 = skip), first
- * `cap` of them, and writes the total record count to the DEVICE word *count; both
- * complete on the handle's stream (no host synchronisation). gs_fold_records_device
- * folds such records (track = 0: apply another replica's delta without
- * re-recording it).
+ * `cap` of them, and writes the COUNT WORD to the DEVICE word *count: the total
+ * record count, | GS_FAIL_BIT (2^62) once a GS_KIND_SIGNED summary's verdict has
+ * failed -- a failed verdict travels with the records even when no record names
+ * the odd cycle (Candidates.merge :79-81). Both complete on the handle's stream (no
+ * host synchronisation). gs_fold_records_device folds such records (track = 0:
+ * apply another replica's delta without re-recording it); `n` may be a count word
+ * (rows | GS_FAIL_BIT): the failure is ANDed into the verdict before the rows fold.
+ * gs_fold_records_counted_device is the same replay with the count word read on the
+ * DEVICE (*count_dev as a take wrote it; at most `cap` rows), so a consumer replays a
+ * window with no host round trip.
  *
  * gs_fold_take_device is one small window of the latency path (BASELINE config 5:
  * per window fold + delta export + completion; PartialAgg.fold then CombineCC /
  * Merger, S/SummaryBulkAggregation.java:109-130, S/SummaryAggregation.java:107-119):
  * fold n device edges with tracking on, take the records since the previous take
  * as gs_take_delta_records does (rec, cap, DEVICE *count_dev), and return when the
- * window is complete with the record total in the HOST word *count. A window of at
+ * window is complete with the same count word (rows | GS_FAIL_BIT) in the HOST word
+ * *count. A window of at
  * most 2^22 edges with nothing else pending runs as ONE launch whose last workgroup
  * publishes the rows and signals the host through mapped memory. Tracking must be
  * on; change tracking (which consumes the records itself) takes the general path.
@@ -212,6 +241,7 @@ int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, siz
                         uint64_t* count_dev, uint64_t* count);
 int gs_delta_stage(gs_handle h, int64_t* send, size_t cap, int width, uint64_t* count);
 int gs_fold_records_device(gs_handle h, const int64_t* rec, size_t n, int track);
+int gs_fold_records_counted_device(gs_handle h, const int64_t* rec, size_t cap, const uint64_t* count_dev, int track);
 int gs_fold_exchange_device(gs_handle h, const int64_t* recv, const uint64_t* counts, size_t world, size_t rows,
                             int width, int skip_rank);
 

@@ -78,7 +78,9 @@ def test_fused_window_take_self_loops_and_growth(gs, oracle_mod):
 def test_fused_window_take_signed_verdict(gs, oracle_mod):
     """Signed kind: the parity rides in the records (w), the verdict flips in the truth's
     window, and after failure the fused launch still completes (every block reaches its
-    ticket) with no records."""
+    ticket) with no records. The count word carries the verdict (| FAIL_BIT), so a
+    replica that replays every window -- before AND after the flip -- holds the same
+    verdict and, while bipartite, the same colouring (Candidates.java:79-81)."""
     import torch
     logside, E, B = 12, 1 << 15, 1 << 11
     inject = [E // 4, E // 2]
@@ -86,7 +88,8 @@ def test_fused_window_take_signed_verdict(gs, oracle_mod):
     dst = torch.empty(E, dtype=torch.int64, device="cuda")
     gs.gen_bip(src, dst, 0, E, logside, 0x5EED0B1B, inject)
     torch.cuda.synchronize()
-    first = oracle_mod.bip_first_failure(src.cpu().numpy(), dst.cpu().numpy())
+    hs, hd = src.cpu().numpy(), dst.cpu().numpy()
+    first = oracle_mod.bip_first_failure(hs, hd)
     assert first >= 0
     rec = torch.empty((B, 3), dtype=torch.int64, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -95,13 +98,74 @@ def test_fused_window_take_signed_verdict(gs, oracle_mod):
         c.set_delta_tracking(True)
         for o in range(0, E, B):
             k = c.fold_take(src[o:], dst[o:], B, rec, B, cnt)
+            word = c.last_take_word
+            failed_now = first < o + B
+            assert bool(word & gs.FAIL_BIT) == failed_now, (o, first, word)
+            assert int(cnt.item()) == word  # the device count word is the same word
             if o >= first + B:
                 assert k == 0  # a failed verdict is final: nothing folds, nothing recorded
-            if first >= o + B:
-                rep.fold_records(rec, k)
-                rep.sync()  # rec is reused by the next take
-                assert rep.ok()
-            assert c.ok() == (first >= o + B), (o, first)
+            rep.fold_records(rec, word)
+            rep.sync()  # rec is reused by the next take
+            assert c.ok() == (not failed_now), (o, first)
+            assert rep.ok() == c.ok(), (o, first)
+            if o + B in (B, 4 * B):
+                ok, comp, v, sign = rep.colouring()
+                tok, tcomp, tv, tsign = oracle_mod.bip_truth(hs[:o + B], hd[:o + B])
+                assert ok and tok and np.array_equal(v, tv) and np.array_equal(comp, tcomp) and \
+                    np.array_equal(sign, tsign)
+
+
+def test_signed_take_word_general_path_and_device_replay(gs, oracle_mod):
+    """The general (unfused) take path -- records pending from an untaken tracked fold --
+    and gs_take_delta_records carry the verdict bit too; a device-side replay
+    (fold_records_counted: the count word read on the device) reproduces summary and
+    verdict with no host round trip."""
+    import torch
+    logside, E, B = 11, 1 << 14, 1 << 10
+    inject = [E // 2 + 17]
+    src = torch.empty(E, dtype=torch.int64, device="cuda")
+    dst = torch.empty(E, dtype=torch.int64, device="cuda")
+    gs.gen_bip(src, dst, 0, E, logside, 0x5EED0B1B, inject)
+    torch.cuda.synchronize()
+    hs, hd = src.cpu().numpy(), dst.cpu().numpy()
+    first = oracle_mod.bip_first_failure(hs, hd)
+    assert first >= 0
+    cap = 2 * B
+    rec = torch.empty((cap, 3), dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    with gs.Summary("signed", capacity_hint=1 << 12) as c, gs.Summary("signed", capacity_hint=1 << 12) as rep, \
+            gs.Summary("signed", capacity_hint=1 << 12) as rep2:
+        c.set_delta_tracking(True)
+        for o in range(0, E, 2 * B):
+            c.fold_device(src[o:], dst[o:], n=B)  # tracked, not taken: the next take is general
+            c.sync()
+            k = c.fold_take(src[o + B:], dst[o + B:], B, rec, cap, cnt)
+            word = c.last_take_word
+            assert bool(word & gs.FAIL_BIT) == (first < o + 2 * B), (o, first)
+            rep.fold_records(rec, word)
+            rep2.fold_records_counted(rec, cap, cnt)
+            rep.sync()
+            rep2.sync()
+            assert rep.ok() == c.ok() == rep2.ok() == (first >= o + 2 * B)
+            assert k <= cap
+        # gs_take_delta_records: the same word on the device
+        c.fold_device(src[:B], dst[:B], n=B)
+        c.take_delta_records(rec, cap, cnt)
+        c.sync()
+        assert int(cnt.item()) & gs.FAIL_BIT
+    # CC summaries never carry the bit; a counted replay of a CC take equals the summary
+    with gs.Summary("cc", capacity_hint=1 << 12) as c, gs.Summary("cc", capacity_hint=1 << 12) as rep:
+        c.set_delta_tracking(True)
+        for o in range(0, E, B):
+            c.fold_take(src[o:], dst[o:], B, rec, cap, cnt)
+            assert c.last_take_word & gs.FAIL_BIT == 0
+            rep.fold_records_counted(rec, cap, cnt)
+            rep.sync()
+        assert _labels_equal(c, rep)
+        ov, olab = oracle_mod.cc_labels(hs, hd)
+        v, lab = rep.labels()
+        assert np.array_equal(v, ov) and np.array_equal(lab, olab)
 
 
 def test_fused_window_take_truncates_and_counts(gs):

@@ -126,11 +126,9 @@ def run_case(seed, diag=False, partials=True):
                     got = summ.fold_take(ts[o:], td[o:], min(w, len(s) - o), rec, cap, cnt)
                     if got > cap:
                         return key, len(s), False
-                    rep.fold_records(rec, got)
+                    rep.fold_records(rec, summ.last_take_word)  # rows | FAIL_BIT: the verdict travels
                     rep.sync()  # rec is reused by the next take
-                # a failed verdict travels in no record (an odd cycle closes inside one tree):
-                # the replica is compared while the stream is bipartite
-                if (kind == "cc" or summ.ok()) and not check(kind, rep, s, d):
+                if not check(kind, rep, s, d):  # labels, or verdict + colouring, every case
                     return key, len(s), False
         else:
             fold_all(rng, summ, s, d, ts, td)
