@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = (
     "gs_delta_capacity", "gs_find_labels_device", "gs_capacity_stats",
     "gs_set_change_tracking", "gs_take_changes_device", "gs_take_changes",
     "gs_fold_records_counted_device", "gs_reset_config", "gs_wait_event", "gs_wait_stream", "gs_fold_device_after",
+    "gs_fold_parity",
 )
 
 FAIL_BIT = 1 << 62  # count words: a failed signed verdict (GS_FAIL_BIT)
@@ -93,6 +94,7 @@ def lib():
     L.gs_reset.argtypes = [_vp]
     L.gs_reset_config.argtypes = [_vp]
     L.gs_fold.argtypes = [_vp, _vp, _vp, _sz]
+    L.gs_fold_parity.argtypes = [_vp, _vp, _vp, _vp, _sz]
     L.gs_fold_device.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz]
     L.gs_fold_device_after.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp]
     L.gs_wait_event.argtypes = [_vp, _vp]
@@ -219,6 +221,15 @@ class Summary:
         d = np.ascontiguousarray(np.asarray(dst, dtype=np.int64))
         assert s.shape == d.shape
         _check(lib().gs_fold(self._h, s.ctypes.data, d.ctypes.data, len(s)))
+
+    def fold_parity(self, src, dst, w):
+        """Fold host edges with a required parity each (gs_fold_parity; signed kind:
+        w = 1 different sides, 0 same side)."""
+        s = np.ascontiguousarray(np.asarray(src, dtype=np.int64))
+        d = np.ascontiguousarray(np.asarray(dst, dtype=np.int64))
+        ww = np.ascontiguousarray(np.asarray(w, dtype=np.uint8))
+        assert s.shape == d.shape == ww.shape
+        _check(lib().gs_fold_parity(self._h, s.ctypes.data, d.ctypes.data, ww.ctypes.data, len(s)))
 
     def fold_device(self, src, dst, n=None, stride=1, w=None, after=None):
         """Fold device-resident edges (torch tensors on this device or raw pointers).

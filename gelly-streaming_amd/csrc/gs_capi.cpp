@@ -767,6 +767,14 @@ int gs_fold(gs_handle h, const int64_t* src, const int64_t* dst, size_t n) {
   return fold_host_impl(h, src, dst, nullptr, n);
 }
 
+int gs_fold_parity(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n) {
+  if (int rc = check(h)) return rc;
+  if (n && (!src || !dst || !w)) return fail(GS_ERR_INVALID, "null edge arrays");
+  DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
+  return fold_host_impl(h, src, dst, w, n);
+}
+
 int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n, size_t stride) {
   if (int rc = check(h)) return rc;
   if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");

@@ -401,7 +401,16 @@ int finish_data(gs_group* g, uint64_t e) {
 // so every replica missed those edges' vertices (tools/emu_check.py; DESIGN.md
 // section 5). Normal-priority streams, or the remote folds serialised on the handle
 // stream, were exact in every run.
-hipError_t create_comm_stream(hipStream_t* st) { return hipStreamCreateWithFlags(st, hipStreamNonBlocking); }
+// GS_GROUP_HIPRIO=1 (diagnostic, tools/lostwork_probe.py) brings the highest priority back.
+hipError_t create_comm_stream(hipStream_t* st) {
+  const char* e = getenv("GS_GROUP_HIPRIO");
+  if (e && atoi(e) != 0) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+      return hipStreamCreateWithPriority(st, hipStreamNonBlocking, hi);
+  }
+  return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
 
 }  // namespace
 

@@ -116,6 +116,22 @@ struct FoldArgs {
 
 constexpr int kCombineRounds = 2;  // wave-level hook combining (combine_hooks)
 
+#ifdef GS_BLOCKLOG
+// Diagnostic build (make -C gelly-streaming_amd blocklog): every CC
+// k_fold workgroup appends one record -- which XCD and CU ran it, its arguments, and
+// what its edges found -- so a lost-work run can tell "never dispatched" from "ran
+// with wrong arguments" from "ran, saw keys that should not be there".
+struct BlockLog {
+  unsigned long long t0, t1;   // wall clock at block start / end
+  unsigned long long src, tab; // launch arguments as the block saw them
+  uint32_t blk, nblk, n, xcc;  // blockIdx.x, gridDim.x, a.n, HW_REG_XCC_ID
+  uint32_t hwid, valid, fresh, hooks;  // HW_REG_HW_ID; edges valid, inserted vertices, hook attempts
+};
+__device__ BlockLog* g_blog = nullptr;
+__device__ unsigned long long g_blog_cap = 0;
+__device__ unsigned long long g_blog_n = 0;
+#endif
+
 // Tail of a fused window take (config 5's per-window fold + delta export + completion
 // in ONE launch instead of fold, stage and completion kernels, each a kernel boundary of
 // ~3 us). Each block reserves its rows in the output with one atomic and writes them
@@ -178,6 +194,14 @@ template <bool SIGNED, bool TRACK, bool TAKE>
 __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) {
   __shared__ int64_t lrec[TAKE ? kFoldBS * 3 : 1];
   __shared__ uint32_t lcnt;
+#ifdef GS_BLOCKLOG
+  __shared__ uint32_t dbg[3];
+  const unsigned long long dbg_t0 = wall_clock64();
+  if (!SIGNED) {
+    if (threadIdx.x < 3) dbg[threadIdx.x] = 0;
+    __syncthreads();
+  }
+#endif
   if (TAKE) {
     D.lrec = lrec;
     D.lcnt = &lcnt;
@@ -228,6 +252,9 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
     const uint32_t su = lookup_resolve(t, ks, hu, k0u, l0u, lu, nu);
     const uint32_t sv = lookup_resolve(t, kd, hv, k0v, l0v, lv, nv);
     note_new_vertices(t, shard, nu, su, nv, sv);
+#ifdef GS_BLOCKLOG
+    if (!SIGNED) atomicAdd(&dbg[1], (nu ? 1u : 0u) + ((nv && sv != su) ? 1u : 0u));
+#endif
     // Delta: a new vertex with an edge to another vertex is always named by a hook
     // record (as the hooked root or as the new parent: its singleton tree can only
     // change through a CAS on it or onto it), so only a new vertex seen through a
@@ -258,6 +285,32 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
   }
   if (__popcll(__ballot(act)) >= 2) combine_hooks(act, ru, kru, rv, krv, need, kCombineRounds);  // wave-uniform
   if (act) hook<SIGNED, TRACK, TAKE>(t, D, shard, ru, ru << 1, kru, rv, rv << 1, krv, need);
+#ifdef GS_BLOCKLOG
+  if (!SIGNED) {
+    if (valid) atomicAdd(&dbg[0], 1u);
+    if (act) atomicAdd(&dbg[2], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0 && g_blog) {
+      const unsigned long long k = atomicAdd(&g_blog_n, 1ull);
+      if (k < g_blog_cap) {
+        BlockLog r;
+        r.t0 = dbg_t0;
+        r.t1 = wall_clock64();
+        r.src = (unsigned long long)a.src;
+        r.tab = (unsigned long long)t.tab;
+        r.blk = blockIdx.x;
+        r.nblk = gridDim.x;
+        r.n = a.n;
+        r.xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
+        r.hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID (CU, SE, ...)
+        r.valid = dbg[0];
+        r.fresh = __hip_atomic_load(&dbg[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        r.hooks = dbg[2];
+        g_blog[k] = r;
+      }
+    }
+  }
+#endif
   if (TAKE) {
     __syncthreads();
     take_tail(t, a, lrec, lcnt, SIGNED);
@@ -517,6 +570,25 @@ __global__ __launch_bounds__(256) void k_find_batch(Table t, const int64_t* __re
 }
 
 // ---------------------------------------------------------------- launchers
+#ifdef GS_BLOCKLOG
+}  // namespace gs
+extern "C" int gs_debug_blocklog(void* buf, unsigned long long cap) {  // diagnostic build only
+  unsigned long long zero = 0;
+  gs::BlockLog* p = static_cast<gs::BlockLog*>(buf);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(gs::g_blog), &p, sizeof p) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(gs::g_blog_cap), &cap, sizeof cap) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(gs::g_blog_n), &zero, sizeof zero) != hipSuccess)
+    return -2;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -2;
+}
+extern "C" unsigned long long gs_debug_blocklog_count() {
+  unsigned long long n = 0;
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(&n, HIP_SYMBOL(gs::g_blog_n), sizeof n);
+  return n;
+}
+namespace gs {
+#endif
 void launch_init(Slot* tab, uint64_t nslots, hipStream_t st) {
   // one slot per thread: 2 GiB in 0.30 ms vs 0.48 ms with 8192 grid-strided blocks
   const uint64_t blocks = (nslots + 255) / 256;

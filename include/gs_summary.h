@@ -88,6 +88,13 @@ int gs_reset_config(gs_handle h);
  * have been copied to the device when the call returns, so the caller may reuse them. */
 int gs_fold(gs_handle h, const int64_t* src, const int64_t* dst, size_t n);
 
+/* Same with a required colour parity per edge from HOST memory (GS_KIND_SIGNED; w[i]
+ * bit 0: 1 = different sides, as every edge of the stream; 0 = same side). This is a
+ * general Candidates merged in component by component (Candidates.merge :77-139 with
+ * an input that is not a one-edge candidate: each vertex against its component's
+ * anchor, parity = the two signs differ). A CC summary ignores w. */
+int gs_fold_parity(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n);
+
 /* Same, from DEVICE memory already resident on the handle's device. Element i is
  * src[i*stride], dst[i*stride] (stride 1: two arrays; stride 2 with dst = src + 1:
  * interleaved pairs). `w` (device, optional, may be NULL) gives the required colour

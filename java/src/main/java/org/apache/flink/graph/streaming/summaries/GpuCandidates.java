@@ -1,0 +1,179 @@
+/*
+ * GPU-backed Candidates: the drop-in initial value of BipartitenessCheck
+ * (S/library/BipartitenessCheck.java:50-52: `new GpuCandidates(true)` instead of
+ * `new Candidates(true)`). updateFunction.foldEdges (:93-95) calls
+ * candidates.merge(edgeToCandidate(v1, v2)) once per edge and combineFunction.reduce
+ * (:128-130) calls c1.merge(c2); both stay unchanged. The signed forest (parity of
+ * every vertex to its parent in the link word) lives in HBM behind a gs_handle.
+ *
+ * Replaces S/summaries/Candidates.java:44-196:
+ *   getSuccess :44-46    -> gs_bip_status
+ *   getMap     :48-50    -> gs_export_colouring, as TreeMap<comp, TreeMap<v, SignedVertex>>
+ *   add        :52-74    -> buffered edges (vertex against the component key, parity from the signs)
+ *   merge      :77-139   -> one-edge candidate: buffered edge, gs_fold per micro-batch;
+ *                           GpuCandidates: gs_combine (the verdict is the AND, :79-81);
+ *                           any other Candidates: its components folded vertex by vertex
+ *   fail       :194-196  -> the sticky device verdict; getMap() is then {} -> "(false,{})"
+ * The output is the canonical colouring (components keyed by their minimum id, sign =
+ * same side as that minimum), which equals the reference's exactly in its exact
+ * regime and the mathematical truth everywhere (DESIGN.md section 2); the reference's
+ * order-dependent quirks are not reproduced.
+ */
+package org.apache.flink.graph.streaming.summaries;
+
+import java.util.Map;
+import java.util.TreeMap;
+
+import org.apache.flink.graph.streaming.util.SignedVertex;
+
+public class GpuCandidates extends Candidates implements GpuSummary {
+	private static final long serialVersionUID = 1L;
+	static final int BATCH = GpuDisjointSet.BATCH;
+
+	private transient long handle;
+	private transient long[] src = new long[BATCH];
+	private transient long[] dst = new long[BATCH];
+	private transient byte[] par = new byte[BATCH];
+	private transient int n;
+	private transient boolean plain = true;  // every buffered edge has parity 1 (a stream edge)
+
+	public GpuCandidates() {
+		this(true);
+	}
+
+	public GpuCandidates(boolean success) {
+		super(success);
+		handle = HandlePool.SIGNED.acquire();
+		if (!success) {
+			GsNative.markFailed(handle);
+		}
+	}
+
+	public GpuCandidates(boolean success, Candidates input) throws Exception {  // :36-42
+		this(success);
+		merge(input);
+	}
+
+	private void buffer(long a, long b, boolean differentSides) {
+		src[n] = a;
+		dst[n] = b;
+		par[n] = (byte) (differentSides ? 1 : 0);
+		plain &= differentSides;
+		if (++n == BATCH) {
+			flush();
+		}
+	}
+
+	@Override
+	public boolean add(long component, Map<Long, SignedVertex> vertices) throws Exception {
+		for (SignedVertex v : vertices.values()) {
+			add(component, v);
+		}
+		return true;  // a conflict surfaces in the verdict (getSuccess), as merge's does
+	}
+
+	/** The component key is taken with sign true, as every Candidates built through
+	 *  add / edgeToCandidate has it (the first vertex added under a key is the key). */
+	@Override
+	public boolean add(long component, SignedVertex vertex) throws Exception {
+		buffer(component, vertex.getVertex(), !vertex.getSign());
+		return true;
+	}
+
+	@Override
+	public Candidates merge(Candidates input) throws Exception {
+		if (input instanceof GpuCandidates) {  // combineFunction.reduce: c1.merge(c2)
+			GpuCandidates o = (GpuCandidates) input;
+			flush();
+			o.flush();
+			GsNative.combine(handle, o.handle);  // rows + verdict, ordered behind both handles
+			return this;
+		}
+		if (!input.getSuccess()) {  // :79-81
+			flush();
+			GsNative.markFailed(handle);
+			return this;
+		}
+		for (Map.Entry<Long, Map<Long, SignedVertex>> comp : input.getMap().entrySet()) {
+			Map<Long, SignedVertex> members = comp.getValue();
+			SignedVertex anchor = null;
+			for (SignedVertex v : members.values()) {
+				if (anchor == null) {
+					anchor = v;
+					// a lone vertex (a self-loop's candidate) still becomes a vertex
+					if (members.size() == 1) {
+						buffer(v.getVertex(), v.getVertex(), true);
+					}
+					continue;
+				}
+				// edgeToCandidate(u, v) = {min: {min: +, max: -}}: one buffered stream edge
+				buffer(anchor.getVertex(), v.getVertex(), anchor.getSign() != v.getSign());
+			}
+		}
+		return this;
+	}
+
+	@Override
+	public boolean getSuccess() {
+		flush();
+		f0 = GsNative.bipStatus(handle);
+		return f0;
+	}
+
+	@Override
+	public TreeMap<Long, Map<Long, SignedVertex>> getMap() {
+		flush();
+		TreeMap<Long, Map<Long, SignedVertex>> map = new TreeMap<>();
+		int c = (int) GsNative.numVertices(handle);
+		long[] comp = new long[c];
+		long[] v = new long[c];
+		byte[] sign = new byte[c];
+		int got = GsNative.exportColouring(handle, comp, v, sign);  // 0 rows once the verdict failed
+		for (int i = 0; i < got; i++) {
+			map.computeIfAbsent(comp[i], k -> new TreeMap<>()).put(v[i], new SignedVertex(v[i], sign[i] != 0));
+		}
+		f1 = map;
+		return map;
+	}
+
+	@Override
+	public String toString() {  // Tuple2.toString: "(true,{1={1=(1,true), 3=(3,false)}, ...})"
+		boolean ok = getSuccess();
+		getMap();
+		f0 = ok;
+		return super.toString();
+	}
+
+	// ---- GpuSummary
+	@Override
+	public void flush() {
+		if (n > 0) {
+			if (plain) {
+				GsNative.fold(handle, src, dst, n);  // every edge: different sides
+			} else {
+				GsNative.foldParity(handle, src, dst, par, n);
+			}
+			n = 0;
+			plain = true;
+		}
+	}
+
+	@Override
+	public long handle() {
+		return handle;
+	}
+
+	@Override
+	public void release() {
+		if (handle != 0) {
+			n = 0;
+			HandlePool.SIGNED.release(handle);
+			handle = 0;
+		}
+	}
+
+	@Override
+	protected void finalize() {
+		release();
+	}
+}

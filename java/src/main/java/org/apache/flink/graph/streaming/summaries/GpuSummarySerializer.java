@@ -1,0 +1,56 @@
+/*
+ * Kryo serializer for the GPU-backed summaries. S extends Serializable
+ * (S/SummaryAggregation.java:22) but Flink serialises a generic S with Kryo, whose
+ * default FieldSerializer skips transient fields -- the handle would be lost. This
+ * serializer writes the gs_serialize image (Merger checkpoints, snapshotState /
+ * restoreState :127-135, and network shuffles of partials), reads it into a pooled
+ * handle (gs_deserialize resets it first), and copies through the allocation-free
+ * gs_combine into a pooled handle (Flink's per-window copy of the initial value,
+ * S/SummaryBulkAggregation.java:79-80).
+ *
+ * Registration, once per job next to SimpleEdgeStream.aggregate:
+ *   env.getConfig().registerTypeWithKryoSerializer(GpuDisjointSet.class, GpuSummarySerializer.class);
+ *   env.getConfig().registerTypeWithKryoSerializer(GpuCandidates.class, GpuSummarySerializer.class);
+ */
+package org.apache.flink.graph.streaming.summaries;
+
+import com.esotericsoftware.kryo.Kryo;
+import com.esotericsoftware.kryo.Serializer;
+import com.esotericsoftware.kryo.io.Input;
+import com.esotericsoftware.kryo.io.Output;
+
+public class GpuSummarySerializer extends Serializer<GpuSummary> {
+
+	@Override
+	public void write(Kryo kryo, Output out, GpuSummary s) {
+		s.flush();
+		byte[] image = GsNative.serialize(s.handle());  // header (kind, verdict) + (v, label, parity) rows
+		out.writeInt(image.length);
+		out.writeBytes(image);
+	}
+
+	@Override
+	public GpuSummary read(Kryo kryo, Input in, Class<GpuSummary> type) {
+		GpuSummary s = fresh(type);
+		GsNative.deserialize(s.handle(), in.readBytes(in.readInt()));
+		return s;
+	}
+
+	@Override
+	public GpuSummary copy(Kryo kryo, GpuSummary original) {
+		GpuSummary c = fresh(original.getClass());
+		original.flush();
+		GsNative.combine(c.handle(), original.handle());  // the verdict travels with the rows
+		return c;
+	}
+
+	private static GpuSummary fresh(Class<?> type) {
+		if (type == GpuCandidates.class) {
+			return new GpuCandidates(true);
+		}
+		if (type == GpuDisjointSet.class) {
+			return new GpuDisjointSet();
+		}
+		throw new IllegalArgumentException("not a GPU summary: " + type);
+	}
+}
