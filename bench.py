@@ -48,24 +48,47 @@ def _lib_sha16():
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
-def _matching_pmc_profile(args, batch):
-    """roofline.traffic (HBM bytes per k_fold launch) from the committed rocprofv3 PMC
-    summary (profiles/pmc_fold_traffic.json, tools/rocprof_summary.py), used only when
-    it was taken of THIS library build, workload, micro-batch and pipeline depth;
-    otherwise null."""
-    path = os.path.join(ROOT, "profiles", "pmc_fold_traffic.json")
+# Calibrated ceiling of random 16-B reads from a table far larger than L2: one L2->fabric
+# request each, 52-55 G requests/s on cached, uncached and fine-grained memory alike
+# (tools/calib_uncached.hip, tools/calib_tlb.hip: profiles/r02_calib_uncached.txt,
+# profiles/r02f_calib_tlb.txt). The fold is bound by this request rate, not by bytes.
+REQUEST_CEILING_PER_S = 53.5e9
+
+
+def _matching_pmc(fname, want):
+    """The committed rocprofv3 PMC summary of a workload's dominant kernel
+    (profiles/<fname>, written by tools/rocprof_summary.py), used only when it was taken
+    of THIS library build and configuration; otherwise (None, note)."""
+    path = os.path.join(ROOT, "profiles", fname)
     if not os.path.exists(path):
-        return None, {}
+        return None, {"traffic_note": "no PMC profile (profiles/%s)" % fname}
     with open(path) as f:
         pm = json.load(f)
-    want = {"workload": "rmat%d-cc-stream" % args.scale, "batch": batch, "pipeline": args.pipeline,
-            "lib_sha16": _lib_sha16()}
+    want = dict(want, lib_sha16=_lib_sha16())
     if any(pm.get(k) != v for k, v in want.items()):
-        return None, {"traffic_note": "no PMC profile of this build / configuration (profiles/pmc_fold_traffic.json "
-                                      "is of %s)" % pm.get("round")}
-    extra = {"traffic_source": pm.get("source"), "read_requests_per_edge": pm.get("read_requests_per_edge"),
-             "l2_hit_rate": pm.get("l2_hit_rate")}
-    return int(pm["hbm_bytes_per_launch"]), extra
+        return None, {"traffic_note": "no PMC profile of this build / configuration (profiles/%s is of %s)"
+                                      % (fname, pm.get("round"))}
+    return pm, {}
+
+
+def _traffic_fields(pm, launches, step_s):
+    """roofline.traffic = L2->fabric request bytes per launch of the dominant kernel
+    (TCC_EA0_RDREQ x 128 B + WRITE_SIZE; Infinity-Cache hits included, so an upper bound
+    of HBM bytes, not HBM bytes) and the request rate against the calibrated ceiling."""
+    out = {"traffic_kind": "L2->fabric request bytes per launch (Infinity-Cache hits included; not HBM bytes)",
+           "traffic_source": pm.get("source"), "l2_hit_rate": pm.get("l2_hit_rate"),
+           "read_requests_per_launch": pm.get("read_requests_per_launch")}
+    if pm.get("read_requests_per_edge") is not None:
+        out["read_requests_per_edge"] = pm["read_requests_per_edge"]
+    if launches and step_s:
+        rps = pm["read_requests_per_launch"] * launches / step_s
+        out["fabric_request_gbs_step"] = round(pm["fabric_bytes_per_launch"] * launches / step_s / 1e9, 1)
+        out["read_requests_per_s_step"] = round(rps / 1e9, 2) * 1e9
+        out["request_ceiling_per_s"] = REQUEST_CEILING_PER_S
+        out["request_frac_step"] = round(rps / REQUEST_CEILING_PER_S, 3)
+    if "sq" in pm:
+        out["sq"] = {k: round(v, 4) for k, v in pm["sq"].items()}
+    return int(pm["fabric_bytes_per_launch"]), out
 
 
 def parse():
@@ -255,7 +278,7 @@ def bench_bip(args):
         el = float(t.item())
     # roofline of the signed k_fold (one GPU): HIP events around every launch over one extra
     # serialised step, the same 48 B/edge algorithmic bytes as the CC fold (the parity rides
-    # in the link word); no PMC profile of this workload, so traffic is null
+    # in the link word); traffic from the workload's PMC profile of this build
     roof = None
     if group is None and not args.no_profile_pass:
         summ.set_profiling(True)
@@ -267,11 +290,17 @@ def bench_bip(args):
         per_launch = per / max(nf, 1)
         achieved = BYTES_PER_EDGE_SPARSE * per_launch / (fold_avg_ms * 1e-3) / 1e9
         step_gbs = BYTES_PER_EDGE_SPARSE * per / (el / args.steps) / 1e9
+        pm, extra = _matching_pmc("pmc_bip_traffic.json", {"workload": "bip-config4", "batch": B,
+                                                             "pipeline": args.pipeline})
+        traffic = None
+        if pm is not None:
+            traffic, extra = _traffic_fields(pm, nf, el / args.steps)
         roof = {"kernel": "k_fold (signed)", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "achieved_step": round(step_gbs, 1), "frac_step": round(step_gbs / HBM_PEAK_GBS, 4),
                 "bytes_per_edge": BYTES_PER_EDGE_SPARSE, "edges_per_launch": int(per_launch),
                 "fold_avg_us": round(fold_avg_ms * 1e3, 2), "fold_launches": int(nf)}
+        roof.update(extra)
     # odd-cycle variant (outside the timed region)
     inject = [E // 8, E // 4, E // 2, 3 * E // 4]
     gs.gen_bip(src, dst, start, per, logside, seed, [i for i in inject if start <= i < start + per],
@@ -450,6 +479,19 @@ def bench_ingest(args):
     c0 = time.perf_counter()
     oracle.parse_edges(sample, 0)
     cpu_el = time.perf_counter() - c0
+    roof = {"kernel": "k_count_lines + k_parse", "bound": "hbm", "achieved": round(alg / el / 1e9, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / el / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": None, "note": "algorithmic bytes = text + 16 B/edge; wall time incl. sync"}
+    pm, extra = _matching_pmc("pmc_ingest_traffic.json", {"workload": "ingest-rmat26-text"})
+    if pm is not None:  # both kernels' fabric bytes per parse, and the parse's VALU/LDS activity
+        t_parse, extra = _traffic_fields(pm, 0, 0)
+        t_count = int(pm.get("count_lines", {}).get("fabric_bytes_per_launch", 0))
+        roof["traffic"] = t_parse + t_count
+        extra["traffic_k_parse"] = t_parse
+        extra["traffic_k_count_lines"] = t_count
+        extra["k_parse_avg_us_rocprof"] = pm.get("avg_us_rocprof")
+        extra["k_count_lines_avg_us_rocprof"] = pm.get("count_lines", {}).get("avg_us_rocprof")
+    roof.update(extra)
     line = {"metric": "text edge ingest: edges/sec parsed from device-resident text", "value": round(E / el, 1),
             "unit": "edges/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el * 1e3, 3), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
@@ -458,9 +500,7 @@ def bench_ingest(args):
                        "text_GBps": round(nbytes / el / 1e9, 1),
                        "host_fold_text_edges_per_s": round(nf / host_el, 1),
                        "host_fold_text_GBps": round(nbytes / host_el / 1e9, 2)},
-            "roofline": {"kernel": "k_count_lines + k_parse", "bound": "hbm", "achieved": round(alg / el / 1e9, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / el / 1e9 / HBM_PEAK_GBS, 4),
-                         "traffic": None, "note": "algorithmic bytes = text + 16 B/edge; wall time incl. sync"},
+            "roofline": roof,
             "cpu_baseline": {"value": round(m / cpu_el, 1), "unit": "edges/s", "cores": 1, "kind": "port",
                              "sample": "first 2^20 lines, split + Long.parseLong restatement (oracle/gs_oracle.cpp)"}}
     print(json.dumps(line), flush=True)
@@ -640,7 +680,11 @@ def main():
         edges_per_launch = per / max(nf, 1) if not grouped else 1 << 20  # own micro-batches dominate
         achieved = BYTES_PER_EDGE_SPARSE * edges_per_launch / (fold_avg_ms * 1e-3) / 1e9
         step_gbs = BYTES_PER_EDGE_SPARSE * per / (elapsed / args.steps) / 1e9
-        traffic, extra = _matching_pmc_profile(args, B)
+        pm, extra = _matching_pmc("pmc_fold_traffic.json", {"workload": "rmat%d-cc-stream" % args.scale,
+                                                              "batch": B, "pipeline": args.pipeline})
+        traffic = None
+        if pm is not None and not grouped:  # fabric request bytes (PMC, per launch) over the pipelined step
+            traffic, extra = _traffic_fields(pm, nf, elapsed / args.steps)
         roof = {"kernel": "k_fold", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "achieved_step": round(step_gbs, 1), "frac_step": round(step_gbs / HBM_PEAK_GBS, 4),
@@ -649,10 +693,6 @@ def main():
                 "stage_avg_us": round(stage_ms * 1e3 / max(ns, 1), 2), "stage_launches": int(ns),
                 "export_ms": round(exp_ms, 3)}
         roof.update(extra)
-        if traffic and not grouped:  # measured HBM bytes (PMC, per launch) over the pipelined step
-            tgbs = traffic * nf / (elapsed / args.steps) / 1e9
-            roof["traffic_gbs_step"] = round(tgbs, 1)
-            roof["traffic_frac_step"] = round(tgbs / HBM_PEAK_GBS, 4)
         if grouped:
             roof["note"] = ("exchange path: fold launches include the other ranks' gathered rows (side stream); "
                             "achieved assumes 2^20 own edges per launch")

@@ -18,7 +18,7 @@ step() {  # name, limit, command...
 step gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_n1 300 python bench.py --steps 20 --warmup 2
-step bench_r20 120 python bench.py --scale 20 --steps 20 --warmup 2 --no-cpu-baseline
+step bench_r20 200 python bench.py --scale 20 --steps 20 --warmup 2
 step bench_bip 120 python bench.py --workload bip --steps 10
 step bench_er 120 python bench.py --workload er-latency --steps 1
 step bench_ingest 120 python bench.py --workload ingest --steps 10

@@ -86,6 +86,25 @@ def main():
         s.sync()
         return time.perf_counter() - t0
 
+    # the same shard as a group's tracked own folds (1 rank, in-process communicator: 3 fold
+    # lanes, per-exchange stage + count/data collectives, no remote rows) vs the plain fold
+    os.environ["GS_GROUP_FAKE_COMM"] = "1"
+    g = gs.Group(s, gs.group_unique_id(), 1, 0, B)
+
+    def run_tracked():
+        s.reset()
+        s.sync()
+        t0 = time.perf_counter()
+        g.fold_batches(src, dst, per, B)
+        g.finish()
+        s.sync()
+        return time.perf_counter() - t0
+
+    tt = timed(run_tracked)
+    g.close()
+    print("tracked own fold (1-rank group, exchange every 2^22): %.2f ms (%.2f G edges/s, %.3f x the plain fold)"
+          % (tt * 1e3, per / tt / 1e9, tt / te), flush=True)
+    s.set_pipelining(3)
     ta = timed(lambda: run_records(None))
     tb = timed(lambda: run_records(per))
     tc = timed(lambda: run_records(0))

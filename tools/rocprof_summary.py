@@ -1,24 +1,27 @@
-"""Summarise a tools/rocprof_round.sh output directory into profiles/<tag>_*.{json,md}.
+"""Summarise a tools/rocprof_round.sh / tools/pmc_workload.sh output directory into
+profiles/<tag>_*.{json,md} and, for the workload's dominant kernel, the per-launch
+traffic file bench.py reads (profiles/pmc_<workload>_traffic.json; the headline fold's
+is profiles/pmc_fold_traffic.json) -- used only when its library hash matches.
 
 Per kernel: dispatches, average duration (kernel trace), and per-dispatch averages of
-every PMC counter collected in the separate --pmc passes. HBM traffic per k_fold
-launch is derived from FETCH_SIZE/WRITE_SIZE (KiB) with the gfx950 note of
-MI355X_MICROARCH.md (HBM section): FETCH_SIZE tallies 128-B requests at 64 B, i.e.
-reads x2 for wide requests; TCC_EA0_RDREQ gives the request count directly.
-Also the k_fold busy time of the traced step: the union of its dispatch intervals
-(pipelined folds overlap), which must not exceed the bench's ms_per_step.
-Usage: python tools/rocprof_summary.py gpurun_out/rocprof_r02 r02 <pipeline depth> [batch]
+every PMC counter collected in the separate --pmc passes. Traffic per launch is
+L2 -> fabric REQUEST bytes: TCC_EA0_RDREQ x 128 B (+ WRITE_SIZE). On gfx950 FETCH_SIZE
+tallies each 128-B request at 64 B (MI355X_MICROARCH.md HBM section: x2), and these
+counters count Infinity-Cache hits too -- so the figure is what the L2 asks of the
+fabric, an upper bound of HBM bytes, not HBM bytes.
+For ingest, the SQ pass gives VALU and LDS activity and LDS bank conflicts.
+Usage: python tools/rocprof_summary.py <dir> <tag> <pipeline> [batch] [--workload rmat-cc|bip|ingest]
 """
-import glob
-import json
-import os
-import sqlite3
-import sys
-from collections import defaultdict
-
-d, tag = sys.argv[1], sys.argv[2]
-pipeline = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-batch = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 20
+argv = list(sys.argv[1:])
+workload = "rmat-cc"
+if "--workload" in argv:
+    i = argv.index("--workload")
+    workload = argv[i + 1]
+    del argv[i:i + 2]
+d, tag = argv[0], argv[1]
+pipeline = int(argv[2]) if len(argv) > 2 else 3
+batch = int(argv[3]) if len(argv) > 3 else 1 << 20
+DOMINANT = {"rmat-cc": "k_fold", "bip": "k_fold", "ingest": "k_parse"}[workload]
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out = {"tag": tag, "pipeline": pipeline, "kernels": {}}
 
@@ -45,7 +48,7 @@ for name, calls, tot, avg, pct in db.execute("select name,total_calls,total_dura
 # busy time of the fold: union of its dispatch intervals in the traced step
 views = [r[0] for r in db.execute("select name from sqlite_master where type in ('view','table')")]
 src = "kernels" if "kernels" in views else [v for v in views if "kernel" in v.lower()][0]
-iv = sorted((s_, e_) for n_, s_, e_ in db.execute("select name, start, end from %s" % src) if "k_fold" in n_)
+iv = sorted((s_, e_) for n_, s_, e_ in db.execute("select name, start, end from %s" % src) if DOMINANT in n_)
 busy, cur_s, cur_e = 0, None, None
 for s_, e_ in iv:
     if cur_e is None or s_ > cur_e:
@@ -56,8 +59,8 @@ for s_, e_ in iv:
         cur_e = max(cur_e, e_)
 if cur_e is not None:
     busy += cur_e - cur_s
-out["k_fold_busy_ms_per_step"] = round(busy / 1e6, 3)
-out["k_fold_span_ms"] = round((iv[-1][1] - iv[0][0]) / 1e6, 3) if iv else None
+out["%s_busy_ms_per_step" % DOMINANT] = round(busy / 1e6, 3)
+out["%s_span_ms" % DOMINANT] = round((iv[-1][1] - iv[0][0]) / 1e6, 3) if iv else None
 
 for pdir in sorted(glob.glob(os.path.join(d, "pmc_*"))):
     dbs = glob.glob(os.path.join(pdir, "*.db"))
@@ -72,9 +75,18 @@ for pdir in sorted(glob.glob(os.path.join(d, "pmc_*"))):
         for cname, vals in cs.items():
             out["kernels"].setdefault(k, {})["pmc_" + cname] = round(sum(vals) / len(vals), 3)
 
-fold = [k for k in out["kernels"] if k.startswith("k_fold")]
-for k in fold:
+for k in list(out["kernels"]):
     r = out["kernels"][k]
+    if "pmc_SQ_WAVE_CYCLES" in r:
+        r["derived_sq"] = {
+            # VALU instruction-issue cycles per wave-cycle, LDS conflict cycles per LDS-active cycle
+            "valu_active_per_wave_cycle": r.get("pmc_SQ_ACTIVE_INST_VALU", 0) / max(r["pmc_SQ_WAVE_CYCLES"], 1),
+            "lds_active_per_wave_cycle": r.get("pmc_SQ_ACTIVE_INST_LDS", 0) / max(r["pmc_SQ_WAVE_CYCLES"], 1),
+            "lds_bank_conflict_per_lds_active": r.get("pmc_SQ_LDS_BANK_CONFLICT", 0) /
+            max(r.get("pmc_SQ_ACTIVE_INST_LDS", 0), 1),
+            "valu_insts_per_wave": r.get("pmc_SQ_INSTS_VALU", 0) / max(r.get("pmc_SQ_WAVES", 0), 1),
+            "lds_insts_per_wave": r.get("pmc_SQ_INSTS_LDS", 0) / max(r.get("pmc_SQ_WAVES", 0), 1),
+        }
     if "pmc_FETCH_SIZE" in r:
         rd_req = r.get("pmc_TCC_EA0_RDREQ_sum")
         r["derived"] = {
@@ -90,35 +102,52 @@ for k in fold:
 os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
 with open(os.path.join(root, "profiles", "%s_rocprof_summary.json" % tag), "w") as f:
     json.dump(out, f, indent=1)
-# per-launch HBM traffic of the plain CC fold, read by bench.py for roofline.traffic
-plain = "k_fold<false, false, false>"  # <SIGNED, TRACK, TAKE>
-r = out["kernels"].get(plain, {})
+# per-launch traffic of the workload's dominant kernel, read by bench.py (roofline.traffic)
+TARGET = {"rmat-cc": ("k_fold<false, false, false>", "rmat26-cc-stream", "pmc_fold_traffic.json"),  # <SIGNED, TRACK, TAKE>
+          "bip": ("k_fold<true, false, false>", "bip-config4", "pmc_bip_traffic.json"),
+          "ingest": ("k_parse", "ingest-rmat26-text", "pmc_ingest_traffic.json")}[workload]
+kname, wname, fname = TARGET
+r = out["kernels"].get(kname, {})
 if "derived" in r and r["derived"].get("read_requests"):
     import hashlib
     with open(os.path.join(root, "gelly-streaming_amd", "lib", "libgs_summary.so"), "rb") as f:
         lib_sha16 = hashlib.sha256(f.read()).hexdigest()[:16]
     dv = r["derived"]
     traffic = {
-        "round": tag, "workload": "rmat26-cc-stream", "batch": batch, "pipeline": pipeline, "lib_sha16": lib_sha16,
-        "kernel": plain, "read_requests_per_edge": round(dv["read_requests"] / batch, 3),
-        "k_fold_busy_ms_per_step": out["k_fold_busy_ms_per_step"],
-        "avg_us_rocprof": r.get("avg_us"), "read_requests_per_launch": dv["read_requests"],
-        "bytes_per_read_request": 128, "write_bytes_per_launch": dv["write_bytes"],
-        "hbm_bytes_per_launch": dv["hbm_read_bytes"] + dv["write_bytes"],
+        "round": tag, "workload": wname, "batch": batch, "pipeline": pipeline, "lib_sha16": lib_sha16,
+        "kernel": kname, "avg_us_rocprof": r.get("avg_us"), "calls": r.get("calls"),
+        "read_requests_per_launch": dv["read_requests"], "bytes_per_read_request": 128,
+        "write_bytes_per_launch": dv["write_bytes"],
+        "fabric_bytes_per_launch": dv["hbm_read_bytes"] + dv["write_bytes"],
         "fetch_size_kib_raw": r["pmc_FETCH_SIZE"], "l2_hit_rate": dv["l2_hit_rate"],
-        "method": "separate rocprofv3 --pmc passes (tools/rocprof_round.sh, bench defaults: pipeline %d) over one "
-                  "bench step; " % pipeline +
+        "busy_ms_per_step": out.get("%s_busy_ms_per_step" % DOMINANT),
+        "traffic_kind": "L2->fabric request bytes (TCC_EA0_RDREQ x 128 B + WRITE_SIZE): Infinity-Cache hits "
+                        "included, so an upper bound of HBM bytes",
+        "method": "separate rocprofv3 --pmc passes (tools/pmc_workload.sh / tools/rocprof_round.sh, bench defaults: "
+                  "pipeline %d) over one bench step; " % pipeline +
                   "read bytes = TCC_EA0_RDREQ x 128 B: on gfx950 one L2->fabric read request moves 128 B both "
                   "for 16-B/lane streaming (256 MiB = 2.10 M requests) and for random 16-B loads (same request "
                   "ceiling), see profiles/r01_calib_random_pmc.json; FETCH_SIZE tallies 64 B per request "
                   "(MI355X_MICROARCH.md HBM section: x2); writes = WRITE_SIZE (KiB)",
         "source": "profiles/%s_rocprof_summary.json" % tag,
     }
-    with open(os.path.join(root, "profiles", "pmc_fold_traffic.json"), "w") as f:
+    if workload in ("rmat-cc", "bip"):
+        traffic["read_requests_per_edge"] = round(dv["read_requests"] / batch, 3)
+    if "derived_sq" in r:
+        traffic["sq"] = r["derived_sq"]
+    if workload == "ingest":  # the whole parse: count pass + parse pass
+        cl = out["kernels"].get("k_count_lines", {})
+        if "derived" in cl:
+            traffic["count_lines"] = {"avg_us_rocprof": cl.get("avg_us"),
+                                      "fabric_bytes_per_launch": cl["derived"]["hbm_read_bytes"] +
+                                      cl["derived"]["write_bytes"], "sq": cl.get("derived_sq")}
+    with open(os.path.join(root, "profiles", fname), "w") as f:
         json.dump(traffic, f, indent=1)
 lines = ["# rocprofv3 summary %s" % tag, "", "| kernel | calls | avg us | total us | % | extra |", "|---|---|---|---|---|---|"]
 for k, r in sorted(out["kernels"].items(), key=lambda kv: -kv[1].get("total_us", 0)):
     extra = ", ".join("%s=%s" % (a[4:], b) for a, b in r.items() if a.startswith("pmc_"))
+    if "derived_sq" in r:
+        extra += "; " + ", ".join("%s=%.3f" % kv for kv in r["derived_sq"].items())
     lines.append("| %s | %s | %s | %s | %s | %s |" % (k, r.get("calls"), r.get("avg_us"), r.get("total_us"), r.get("pct"), extra))
 with open(os.path.join(root, "profiles", "%s_rocprof_summary.md" % tag), "w") as f:
     f.write("\n".join(lines) + "\n")
