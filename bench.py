@@ -109,6 +109,8 @@ def parse():
     p.add_argument("--bip-prefix-log2", type=int, default=15,
                    help="bip: edges of the prefix the quirk-exact Candidates oracle folds (O(E x components))")
     p.add_argument("--cpu-sample-log2", type=int, default=24)
+    p.add_argument("--cpu-threads", type=int, default=1,
+                   help="also time the partitioned P-thread CPU baseline (CombineCC of the partials)")
     p.add_argument("--no-profile-pass", action="store_true")
     p.add_argument("--pipeline", type=int, default=3,
                    help="pipelined windows at N=1 (gs_set_pipelining depth; 1 = strictly in order)")
@@ -126,6 +128,8 @@ def parse():
                    help="relabel-table capacity hint of the CC summary (log2 vertices; 0: 2^scale)")
     p.add_argument("--exchange-impl", choices=["native", "torch"], default="native",
                    help="native: RCCL inside libgs_summary (gs_group_*); torch: torch.distributed all-gather")
+    p.add_argument("--er-mode", choices=["launch", "server"], default="server",
+                   help="er-latency: which window mode `value` reports (both are measured)")
     p.add_argument("--launch-check", action="store_true",
                    help="launcher test (CPU, gloo): form the world exactly as the bench does, print one JSON line "
                         "with the world that formed, touch no GPU")
@@ -381,7 +385,12 @@ def bench_bip(args):
 def bench_er_latency(args):
     """BASELINE config 5: Erdos-Renyi G(n = 2^22, m = 2^26), 1024 windows of 2^16 edges. Per
     window: fold (delta tracking on) + delta export into device memory (the records the
-    Merger/combine consumes) + completion; host steady-clock latency per window, p50/p99."""
+    Merger/combine consumes) + completion; host steady-clock latency per window, p50/p99.
+    Two ways to run a window, both timed on this box: one fused launch per window
+    (gs_fold_take_device), and the resident window server (gs_set_window_server: one
+    persistent launch, windows posted through host-mapped memory). `value` is the p50 of
+    --er-mode (default server). The line checks itself: both modes' summaries must be
+    equal (device lookups of every vertex) and the first 8 windows oracle-exact."""
     import gsamd as gs
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -395,46 +404,77 @@ def bench_er_latency(args):
     rec = torch.empty(cap * 3, dtype=torch.int64, device=dev)
     cnt = torch.empty(1, dtype=torch.int64, device=dev)
     summ.sync()
-    lat = []
-    nrec = 0
     # the C ABI called as the JNI glue calls it: raw addresses, arguments prepared once
     import ctypes
     ps, pd, prec, pcnt = src.data_ptr(), dst.data_ptr(), rec.data_ptr(), cnt.data_ptr()
     take = gs.lib().gs_fold_take_device
     k_host = ctypes.c_uint64()
     k_ref = ctypes.byref(k_host)
-    for step in range(args.warmup + 1):
-        summ.reset()
-        lat = []
-        nrec = 0
-        for o in range(0, E, B):
-            t0 = time.perf_counter()
-            # one window: fold (tracked) + delta records into device memory + completion
-            # (gs_fold_take_device: a single launch that signals the host)
-            rc = take(summ._h, ps + 8 * o, pd + 8 * o, B, prec, cap, pcnt, k_ref)
-            lat.append(time.perf_counter() - t0)
-            if rc:
-                raise gs.GSError(rc, gs.lib().gs_last_error().decode())
-            nrec += k_host.value
-    lat = np.array(lat) * 1e6
-    tot = lat.sum() * 1e-6
-    import oracle  # CPU baseline leg only: the 1-thread restatement on the first 64 windows
-    nw = 64
+    res = {}
+    for mode in ("launch", "server"):
+        summ.set_window_server(mode == "server")
+        for step in range(args.warmup + 1):
+            summ.reset()
+            lat = []
+            nrec = 0
+            for o in range(0, E, B):
+                t0 = time.perf_counter()
+                # one window: fold (tracked) + delta records into device memory + completion
+                rc = take(summ._h, ps + 8 * o, pd + 8 * o, B, prec, cap, pcnt, k_ref)
+                lat.append(time.perf_counter() - t0)
+                if rc:
+                    raise gs.GSError(rc, gs.lib().gs_last_error().decode())
+                nrec += k_host.value
+        lat = np.array(lat) * 1e6
+        res[mode] = {"p50_us": round(float(np.percentile(lat, 50)), 2), "p99_us": round(float(np.percentile(lat, 99)), 2),
+                     "max_us": round(float(lat.max()), 2), "total_ms": round(lat.sum() * 1e-3, 3),
+                     "edges_per_s": round(E / (lat.sum() * 1e-6), 1), "delta_records": nrec}
+        if mode == "server":
+            res[mode]["server"] = summ.window_server_stats()
+        # keep this mode's final summary for the cross-check
+        nv = summ.num_vertices()
+        v = torch.empty(nv + 1, dtype=torch.int64, device=dev)
+        lab = torch.empty(nv + 1, dtype=torch.int64, device=dev)
+        summ.export_labels_device(v, lab)
+        res[mode]["_v"], res[mode]["_lab"], res[mode]["_nv"] = v[:nv], lab[:nv], nv
+    # self-check: the two modes' summaries are equal (every vertex looked up on the device)
+    got = torch.empty_like(res["launch"]["_v"])
+    fnd = torch.empty(res["launch"]["_nv"], dtype=torch.uint8, device=dev)
+    summ.find_labels_device(res["launch"]["_v"], got, fnd)
+    summ.sync()
+    agree = (res["launch"]["_nv"] == res["server"]["_nv"] and bool(fnd.all().item()) and
+             bool(torch.equal(got, res["launch"]["_lab"])))
+    for m in res.values():
+        for k in ("_v", "_lab", "_nv"):
+            m.pop(k)
+    import oracle  # checker and CPU baseline legs only
+    nchk = 8
+    summ.set_window_server(args.er_mode == "server")
+    summ.reset()
+    for o in range(0, nchk * B, B):
+        take(summ._h, ps + 8 * o, pd + 8 * o, B, prec, cap, pcnt, k_ref)
+    v8, l8 = summ.labels()
+    ov, olab = oracle.cc_labels(src[:nchk * B].cpu().numpy(), dst[:nchk * B].cpu().numpy())
+    prefix_ok = bool(np.array_equal(v8, ov) and np.array_equal(l8, olab))
+    nw = 64  # CPU baseline leg only: the 1-thread restatement on the first 64 windows
     cl = oracle.cpu_window_latency_cc(src[:nw * B].cpu().numpy(), dst[:nw * B].cpu().numpy(), B) * 1e6
     cpu = {"value": round(float(np.percentile(cl, 50)), 2), "unit": "us", "cores": 1, "kind": "port",
            "p99_us": round(float(np.percentile(cl, 99)), 2),
            "sample": "first %d windows of the same stream, DisjointSet.union per edge + CombineCC/Merger per "
                      "window (oracle/gs_oracle.cpp), 1 thread, %.1f s" % (nw, cl.sum() * 1e-6)}
+    sel = res[args.er_mode]
     line = {"metric": "per-window latency p50 (us) for streaming CC on ER (config 5)",
-            "value": round(float(np.percentile(lat, 50)), 2), "unit": "us", "n_gpus": 1, "steps": 1,
-            "warmup": args.warmup, "ms_per_step": round(tot * 1e3, 3), "higher_is_better": False,
+            "value": sel["p50_us"], "unit": "us", "n_gpus": 1, "steps": 1,
+            "warmup": args.warmup, "ms_per_step": sel["total_ms"], "higher_is_better": False,
             "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
             "config": {"workload": "er-latency-config5", "n": 1 << logn, "edges": E, "micro_batch": B,
-                       "windows": E // B, "p50_us": round(float(np.percentile(lat, 50)), 2),
-                       "p99_us": round(float(np.percentile(lat, 99)), 2), "max_us": round(float(lat.max()), 2),
-                       "edges_per_s": round(E / tot, 1), "delta_records": nrec,
+                       "windows": E // B, "mode": args.er_mode, "p50_us": sel["p50_us"], "p99_us": sel["p99_us"],
+                       "max_us": sel["max_us"], "edges_per_s": sel["edges_per_s"],
+                       "delta_records": sel["delta_records"], "modes": res,
+                       "modes_agree": agree, "first_%d_windows_oracle_exact" % nchk: prefix_ok,
                        "per_window": "fold + delta export to device + completion (host steady clock; "
-                                     "gs_fold_take_device)"},
+                                     "gs_fold_take_device; launch = one fused launch per window, server = the "
+                                     "resident window server)"},
             "cpu_baseline": cpu}
     print(json.dumps(line), flush=True)
     summ.close()
@@ -658,10 +698,34 @@ def main():
     total_edges = E * args.steps
     value = total_edges / elapsed
     labelled = nlabels[0]
+    checks = {}
     if world > 1:  # vertices labelled by all ranks' slices (outside the timed region)
         c = torch.tensor([labelled], dtype=torch.int64, device=dev)
         dist.all_reduce(c)
         labelled = int(c.item())
+        # every replica holds the same vertex count, and the slices cover it exactly
+        nv = summ.num_vertices()
+        lo = torch.tensor([nv], dtype=torch.int64, device=dev)
+        hi = torch.tensor([nv], dtype=torch.int64, device=dev)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        checks["replicas_same_vertex_count"] = int(lo.item()) == int(hi.item()) == labelled
+    else:  # the label pass covers every distinct endpoint of the stream (4 slices of the id space)
+        distinct = 0
+        for lo_bits in range(4):
+            parts = [x[(x & 3) == lo_bits] for x in (src, dst)]
+            distinct += int(torch.unique(torch.cat(parts)).numel())
+            del parts
+        checks["vertices_equal_distinct_endpoints"] = distinct == labelled
+    if rank == 0:  # the stream's first 2^24 edges (rank 0's shard starts there) vs the oracle
+        import oracle  # checker leg only
+        m = min(1 << 24, per)
+        with gs.Summary("cc", device=local, capacity_hint=1 << 20) as chk:
+            for o in range(0, m, 1 << 20):
+                chk.fold_device(src[o:], dst[o:], n=min(1 << 20, m - o))
+            cv, cl = chk.labels()
+        ov, olab = oracle.cc_labels(src[:m].cpu().numpy(), dst[:m].cpu().numpy())
+        checks["prefix_%d_edges_oracle_exact" % m] = bool(np.array_equal(cv, ov) and np.array_equal(cl, olab))
 
     # Roofline of the dominant kernel (k_fold). Per launch: HIP events around every
     # launch on the stream it runs on, over one extra full step (profiling serialises
@@ -704,17 +768,21 @@ def main():
         hs = src[:m].cpu().numpy()
         hd = dst[:m].cpu().numpy()
         secs1 = oracle.cpu_baseline_cc(hs, hd, B, threads=1)
-        # BASELINE.md plan (b): p threads, each folding a 1/p partition of every window,
-        # then CombineCC of the partials and the Merger (the box's CPU share: OMP_NUM_THREADS)
-        p = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+        # BASELINE.md plan (b), opt-in (--cpu-threads P): P threads, each folding a 1/P
+        # partition of every window, then CombineCC of the partials and the Merger. It
+        # measured slower than one thread (0.66 vs 0.91 M edges/s, r02: the combines
+        # dominate) and cost 25 s of the run, so the default line times one thread.
+        p = max(1, args.cpu_threads)
         secsp = oracle.cpu_baseline_cc(hs, hd, B, threads=p) if p > 1 else secs1
         best_p, best = (p, secsp) if secsp < secs1 else (1, secs1)
         cpu = {"value": round(m / best, 1), "unit": "edges/s", "cores": best_p, "kind": "port",
-               "value_1thread": round(m / secs1, 1), "value_%dthreads" % p: round(m / secsp, 1),
+               "value_1thread": round(m / secs1, 1),
                "sample": "first 2^%d edges of the same RMAT-%d stream, %d-edge windows, C++ restatement of "
-                         "DisjointSet.union + CombineCC/Merger per window (oracle/gs_oracle.cpp); 1 thread %.1f s, "
-                         "%d threads (partitioned fold + CombineCC) %.1f s; value = the faster"
-                         % (args.cpu_sample_log2, args.scale, B, secs1, p, secsp)}
+                         "DisjointSet.union + CombineCC/Merger per window (oracle/gs_oracle.cpp); 1 thread %.1f s"
+                         % (args.cpu_sample_log2, args.scale, B, secs1)}
+        if p > 1:
+            cpu["value_%dthreads" % p] = round(m / secsp, 1)
+            cpu["sample"] += "; %d threads (partitioned fold + CombineCC) %.1f s; value = the faster" % (p, secsp)
 
     if rank == 0:
         line = {
@@ -738,7 +806,7 @@ def main():
                        "combine": "delta exchange (native RCCL group)" if grouped else "none at 1 GPU (same cadence)",
                        "ids": "sparse 64-bit (scrambled)",
                        "capacity_hint": 1 << (args.capacity_log2 or xlog),
-                       "vertices_labelled": int(labelled),
+                       "vertices_labelled": int(labelled), "self_check": checks,
                        "parallelism": ("edge-shard x%d, per-batch delta all-gather (%s)" % (world, args.exchange_impl))
                        if xch is not None else "single GPU"},
             "roofline": roof,

@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "gs_delta_capacity", "gs_find_labels_device", "gs_capacity_stats",
     "gs_set_change_tracking", "gs_take_changes_device", "gs_take_changes",
     "gs_fold_records_counted_device", "gs_reset_config", "gs_wait_event", "gs_wait_stream", "gs_fold_device_after",
-    "gs_fold_parity",
+    "gs_fold_parity", "gs_set_window_server", "gs_window_server_stats",
 )
 
 FAIL_BIT = 1 << 62  # count words: a failed signed verdict (GS_FAIL_BIT)
@@ -95,6 +95,8 @@ def lib():
     L.gs_reset_config.argtypes = [_vp]
     L.gs_fold.argtypes = [_vp, _vp, _vp, _sz]
     L.gs_fold_parity.argtypes = [_vp, _vp, _vp, _vp, _sz]
+    L.gs_set_window_server.argtypes = [_vp, ctypes.c_int]
+    L.gs_window_server_stats.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]
     L.gs_fold_device.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz]
     L.gs_fold_device_after.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp]
     L.gs_wait_event.argtypes = [_vp, _vp]
@@ -403,6 +405,16 @@ class Summary:
                                          ctypes.byref(c)))
         self.last_take_word = c.value
         return c.value & (FAIL_BIT - 1)
+
+    def set_window_server(self, on=True):
+        """gs_set_window_server: fold_take windows (<= 2^16 edges) go to one resident
+        launch instead of a launch each."""
+        _check(lib().gs_set_window_server(self._h, 1 if on else 0))
+
+    def window_server_stats(self):
+        a, b = _u64(), _u64()
+        _check(lib().gs_window_server_stats(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return {"launches": a.value, "windows": b.value}
 
     def delta_stage(self, send, cap, count, width=3):
         """Stage every pending record into `send` (device int64 [cap, width]) and the

@@ -335,7 +335,36 @@ int ensure_lanes(gs_summary* h, int n) {
   return GS_OK;
 }
 
+// ---- resident window server (gs_set_window_server) -------------------------------
+// Stop: the stop word, then the stream (the launch leaves within a poll interval).
+int server_stop(gs_summary* h) {
+  if (!h->srv_running) return GS_OK;
+  __atomic_store_n(&h->srv_box->seq, gs::kServerStop | h->srv_seq, __ATOMIC_RELEASE);
+  h->srv_running = false;
+  GS_HIP(hipStreamSynchronize(h->stream));
+  return GS_OK;
+}
+
+// Start a session whose first window is srv_seq + 1. The blocks' broadcast word starts
+// at srv_seq (copied on the stream from the pinned mailbox, before the launch), so no
+// block mistakes the previous session's stop word for this session's.
+int server_start(gs_summary* h) {
+  gs::ServerBox* b = h->srv_box;
+  memset(b, 0, sizeof(gs::ServerBox));
+  b->seq = h->srv_seq;
+  b->pad[0] = h->srv_seq;
+  GS_HIP(hipMemcpyAsync(&h->srv_bc->seq, &b->pad[0], 8, hipMemcpyHostToDevice, h->stream));
+  // ~250 ms without a window: the launch leaves on its own (wall clock 100 MHz)
+  gs::launch_window_server(h->kind == GS_KIND_SIGNED, h->table(), h->delta(), h->srv_box, h->srv_bc, h->done_dev,
+                           h->srv_seq, 25000000ull, h->stream);
+  GS_HIP(hipGetLastError());
+  h->srv_running = true;
+  h->srv_launches++;
+  return GS_OK;
+}
+
 int join_lanes(gs_summary* h) {
+  if (int rc = server_stop(h)) return rc;
   if (int rc = join_pipe_lanes(h)) return rc;
   if (h->side_dirty) {
     GS_HIP(hipEventRecord(h->side_ev, h->side));
@@ -631,6 +660,8 @@ int gs_destroy(gs_handle h) {
   }
   if (h->main_ev) (void)hipEventDestroy(h->main_ev);
   if (h->ext_ev) (void)hipEventDestroy(h->ext_ev);
+  if (h->srv_box) (void)hipHostFree(h->srv_box);
+  if (h->srv_bc) (void)hipFree(h->srv_bc);
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 2; ++i) {
     if (h->stage_ev[i]) (void)hipEventDestroy(h->stage_ev[i]);
@@ -692,6 +723,7 @@ int gs_reset_config(gs_handle h) {
   h->changes_own_track = false;
   if (h->profiling)
     if (int rc = gs_set_profiling(h, 0)) return rc;
+  h->srv_on = false;
   h->pipe_depth = 1;
   h->lane_next = 0;
   return gs_reset(h);
@@ -1126,6 +1158,70 @@ int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count
   return stage_delta(h, rec, cap, 3, reinterpret_cast<unsigned long long*>(count), h->kind == GS_KIND_SIGNED);
 }
 
+// One window through the resident server: post it in the mailbox, spin on the
+// completion word. A server that left on its own (idle) before it saw the window is
+// started again and the window posted again.
+static int server_take(gs_handle h, const int64_t* src, const int64_t* dst, size_t n, int64_t* rec, size_t cap,
+                       unsigned long long* cd, uint64_t* count) {
+  if (int rc = ensure_capacity(h, n)) return rc;  // (its slow path stops the server)
+  const unsigned long long seq = h->srv_seq + 1, dseq = ++h->done_seq;
+  for (int attempt = 0;; ++attempt) {
+    if (!h->srv_running)
+      if (int rc = server_start(h)) return rc;
+    gs::ServerBox* b = h->srv_box;
+    b->src = (unsigned long long)src;
+    b->dst = (unsigned long long)dst;
+    b->n = n;
+    b->rec = (unsigned long long)rec;
+    b->cap = cap;
+    b->cnt = (unsigned long long)cd;
+    b->done_seq = dseq;
+    __atomic_store_n(&b->seq, seq, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    bool left = false;
+    for (uint32_t i = 1;; ++i) {
+      if (__atomic_load_n(h->h_done, __ATOMIC_ACQUIRE) >= dseq) break;
+      if (__atomic_load_n(&b->exited, __ATOMIC_ACQUIRE)) {
+        if (__atomic_load_n(h->h_done, __ATOMIC_ACQUIRE) >= dseq) break;
+        left = true;
+        break;
+      }
+      if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+        return fail(GS_ERR_HIP, "window server: no completion within 5 s");
+      __builtin_ia32_pause();
+    }
+    if (!left) break;
+    h->srv_running = false;  // it left before this window: join it, start again
+    GS_HIP(hipStreamSynchronize(h->stream));
+    if (attempt >= 3) return fail(GS_ERR_HIP, "window server: left before the window three times");
+  }
+  h->srv_seq = seq;
+  h->srv_windows++;
+  note_exact_count(h, __atomic_load_n(h->h_done + 1, __ATOMIC_ACQUIRE));
+  *count = __atomic_load_n(h->h_done + 2, __ATOMIC_ACQUIRE);
+  return check_flags_now(h);
+}
+
+int gs_set_window_server(gs_handle h, int on) {
+  if (int rc = check(h)) return rc;
+  DeviceGuard g(h->device);
+  if (int rc = join_lanes(h)) return rc;  // stops a running server
+  if (on && !h->srv_box) {
+    GS_HIP(hipHostMalloc(&h->srv_box, sizeof(gs::ServerBox), hipHostMallocMapped | hipHostMallocCoherent));
+    GS_HIP(hipMalloc(&h->srv_bc, sizeof(gs::ServerBcast)));
+    memset(h->srv_box, 0, sizeof(gs::ServerBox));
+  }
+  h->srv_on = on != 0;
+  return GS_OK;
+}
+
+int gs_window_server_stats(gs_handle h, uint64_t* launches, uint64_t* windows) {
+  if (int rc = check(h)) return rc;
+  if (launches) *launches = h->srv_launches;
+  if (windows) *windows = h->srv_windows;
+  return GS_OK;
+}
+
 int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, size_t n, int64_t* rec, size_t cap,
                         uint64_t* count_dev, uint64_t* count) {
   if (int rc = check(h)) return rc;
@@ -1134,8 +1230,13 @@ int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, siz
   if (!h->track) return fail(GS_ERR_INVALID, "delta tracking is off");
   if (h->side) return fail(GS_ERR_INVALID, "a group's summary exchanges its delta: no window take");
   DeviceGuard g(h->device);
-  if (int rc_ = join_lanes(h)) return rc_;
   auto* cd = reinterpret_cast<unsigned long long*>(count_dev);
+  // the resident server takes a window of at most one launch's worth of edges when
+  // nothing else is pending on the handle
+  if (h->srv_on && n > 0 && n <= gs::kServerMaxEdges && h->delta_fill_ub[h->dset] == 0 && !h->changes &&
+      !h->profiling && !h->lanes_dirty && !h->side_dirty)
+    return server_take(h, src, dst, n, rec, cap, cd, count);
+  if (int rc_ = join_lanes(h)) return rc_;
   // One launch when the window fits one k_fold launch and nothing else is pending in
   // the delta set (earlier tracked folds' records belong to this take too), and no
   // change emission consumes the records.

@@ -156,6 +156,13 @@ struct gs_summary {
   hipStream_t side = nullptr;
   hipEvent_t side_ev = nullptr;
   bool side_dirty = false;
+  // resident window server (gs_set_window_server): one persistent launch serves the
+  // latency path's windows; every other entry point stops it first (join_lanes)
+  bool srv_on = false, srv_running = false;
+  gs::ServerBox* srv_box = nullptr;      // host-mapped mailbox
+  gs::ServerBcast* srv_bc = nullptr;     // device: block 0 -> other blocks
+  unsigned long long srv_seq = 0;        // last window posted and completed
+  uint64_t srv_launches = 0, srv_windows = 0;
   // profiling
   bool profiling = false;
   struct Pending {

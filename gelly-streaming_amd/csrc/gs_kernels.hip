@@ -144,7 +144,7 @@ __device__ unsigned long long g_blog_n = 0;
 // A signed summary's count word carries the verdict (| kFailBit once it failed): the
 // take's consumer replays the records AND the verdict (Candidates.merge :79-81).
 __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, const int64_t* lrec, uint32_t lcnt,
-                                          bool signed_kind) {
+                                          bool signed_kind, uint32_t nblocks) {
   __shared__ unsigned long long base_sh;
   __shared__ uint32_t last_sh;
   const uint32_t nb = min(lcnt, kFoldBS);
@@ -166,7 +166,7 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
   // alone does not wait for global stores); no L2 writeback needed for write-through rows
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (threadIdx.x == 0) last_sh = atomicAdd(t.ctr + ctr_index(CTR_TAKE_DONE), 1u) == gridDim.x - 1;
+  if (threadIdx.x == 0) last_sh = atomicAdd(t.ctr + ctr_index(CTR_TAKE_DONE), 1u) == nblocks - 1;
   __syncthreads();
   if (!last_sh || threadIdx.x >= 64) return;
   unsigned long long nv = __hip_atomic_load(t.ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED,
@@ -189,6 +189,10 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
   __hip_atomic_store(a.done + 2, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(a.done, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+
+template <bool SIGNED, bool TRACK, bool TAKE>
+__device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const FoldArgs& a, uint32_t blk,
+                                           bool failed, unsigned long long n_word, uint32_t* dbg);
 
 template <bool SIGNED, bool TRACK, bool TAKE>
 __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) {
@@ -219,8 +223,48 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
   // a failed verdict is final: no more work (a TAKE block still reaches its ticket)
   const bool failed = SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0;
   if (failed && !TAKE) return;
-  const int shard = (int)((blockIdx.x + a.shard0) & (kShards - 1));
-  const uint32_t i = blockIdx.x * kFoldBS + threadIdx.x;
+#ifdef GS_BLOCKLOG
+  fold_block<SIGNED, TRACK, TAKE>(t, D, a, blockIdx.x, failed, n_word, SIGNED ? nullptr : dbg);
+#else
+  fold_block<SIGNED, TRACK, TAKE>(t, D, a, blockIdx.x, failed, n_word, nullptr);
+#endif
+#ifdef GS_BLOCKLOG
+  if (!SIGNED) {
+    __syncthreads();
+    if (threadIdx.x == 0 && g_blog) {
+      const unsigned long long k = atomicAdd(&g_blog_n, 1ull);
+      if (k < g_blog_cap) {
+        BlockLog r;
+        r.t0 = dbg_t0;
+        r.t1 = wall_clock64();
+        r.src = (unsigned long long)a.src;
+        r.tab = (unsigned long long)t.tab;
+        r.blk = blockIdx.x;
+        r.nblk = gridDim.x;
+        r.n = a.n;
+        r.xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
+        r.hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID (CU, SE, ...)
+        r.valid = dbg[0];
+        r.fresh = dbg[1];
+        r.hooks = dbg[2];
+        g_blog[k] = r;
+      }
+    }
+  }
+#endif
+  if (TAKE) {
+    __syncthreads();
+    take_tail(t, a, lrec, lcnt, SIGNED, gridDim.x);
+  }
+}
+
+// The fold of one block's edges (edge i = blk * kFoldBS + threadIdx.x): relabel probes,
+// shortcut, finds, wave-combined hooks. Shared by k_fold and the resident window server.
+template <bool SIGNED, bool TRACK, bool TAKE>
+__device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const FoldArgs& a, uint32_t blk,
+                                           bool failed, unsigned long long n_word, uint32_t* dbg) {
+  const int shard = (int)((blk + a.shard0) & (kShards - 1));
+  const uint32_t i = blk * kFoldBS + threadIdx.x;
   bool valid = i < a.n && !failed;
   if (valid && a.n_dev) valid = (unsigned long long)(a.base + i) < (n_word & (kFailBit - 1));
   if (valid && a.rows) {  // exchange layout: the block's count word gives its live rows
@@ -252,9 +296,7 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
     const uint32_t su = lookup_resolve(t, ks, hu, k0u, l0u, lu, nu);
     const uint32_t sv = lookup_resolve(t, kd, hv, k0v, l0v, lv, nv);
     note_new_vertices(t, shard, nu, su, nv, sv);
-#ifdef GS_BLOCKLOG
-    if (!SIGNED) atomicAdd(&dbg[1], (nu ? 1u : 0u) + ((nv && sv != su) ? 1u : 0u));
-#endif
+    if (dbg) atomicAdd(&dbg[1], (nu ? 1u : 0u) + ((nv && sv != su) ? 1u : 0u));
     // Delta: a new vertex with an edge to another vertex is always named by a hook
     // record (as the hooked root or as the new parent: its singleton tree can only
     // change through a CAS on it or onto it), so only a new vertex seen through a
@@ -285,35 +327,111 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
   }
   if (__popcll(__ballot(act)) >= 2) combine_hooks(act, ru, kru, rv, krv, need, kCombineRounds);  // wave-uniform
   if (act) hook<SIGNED, TRACK, TAKE>(t, D, shard, ru, ru << 1, kru, rv, rv << 1, krv, need);
-#ifdef GS_BLOCKLOG
-  if (!SIGNED) {
+  if (dbg) {
     if (valid) atomicAdd(&dbg[0], 1u);
     if (act) atomicAdd(&dbg[2], 1u);
-    __syncthreads();
-    if (threadIdx.x == 0 && g_blog) {
-      const unsigned long long k = atomicAdd(&g_blog_n, 1ull);
-      if (k < g_blog_cap) {
-        BlockLog r;
-        r.t0 = dbg_t0;
-        r.t1 = wall_clock64();
-        r.src = (unsigned long long)a.src;
-        r.tab = (unsigned long long)t.tab;
-        r.blk = blockIdx.x;
-        r.nblk = gridDim.x;
-        r.n = a.n;
-        r.xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
-        r.hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID (CU, SE, ...)
-        r.valid = dbg[0];
-        r.fresh = __hip_atomic_load(&dbg[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        r.hooks = dbg[2];
-        g_blog[k] = r;
+  }
+}
+
+// Resident window server: one launch serves every window of a session (config 5's
+// latency path without a kernel launch per window). Windows run one after another; in
+// each, block b folds edges [256 b, 256 b + 256) exactly as k_fold<SIGNED, true, true>
+// does and the window's last block publishes it (take_tail). The table needs no kernel
+// boundary between windows: every access is already correct on stale lines (the
+// concurrency model in gs_device.hpp), as between the blocks of one launch. Hand-offs:
+//   host -> block 0: mailbox in host-mapped memory, seq stored last (x86 release), read
+//     with system-scope loads;
+//   block 0 -> blocks: the descriptor stored with agent-scope (write-through) stores,
+//     each storing lane's `s_waitcnt vmcnt(0)`, then the seq word; polled and read with
+//     agent-scope loads by one lane per block, handed to its block through LDS behind a
+//     barrier (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms);
+//   window -> host: take_tail's rows, count word and completion word.
+// Exit conditions every wave reaches: a stop request, or no window for idle_ticks
+// (block 0 then tells the others and the host), or -- for the other blocks -- twice
+// that without any word from block 0.
+template <bool SIGNED>
+__global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, ServerBox* box, ServerBcast* bc,
+                                                           unsigned long long* done, unsigned long long seq0,
+                                                           unsigned long long idle_ticks) {
+  __shared__ int64_t lrec[kFoldBS * 3];
+  __shared__ uint32_t lcnt;
+  __shared__ unsigned long long w[8];
+  D.lrec = lrec;
+  D.lcnt = &lcnt;
+  unsigned long long last = seq0;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const unsigned long long t0 = wall_clock64();
+      unsigned long long s = 0;
+      if (blockIdx.x == 0) {
+        for (;;) {
+          s = __hip_atomic_load(&box->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (s != last) break;
+          if (wall_clock64() - t0 > idle_ticks) {
+            s = kServerStop | last;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        unsigned long long f[8];
+        f[0] = s;
+        if (!(s & kServerStop)) {
+#pragma unroll
+          for (int k = 1; k < 8; ++k)
+            f[k] = __hip_atomic_load(&box->seq + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+          for (int k = 1; k < 8; ++k) __hip_atomic_store(&bc->seq + k, f[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // every descriptor store (write-through, agent scope) acknowledged before the seq word
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&bc->seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s & kServerStop) __hip_atomic_store(&box->exited, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = f[k];
+      } else {
+        for (;;) {
+          s = __hip_atomic_load(&bc->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (s != last) break;
+          if (wall_clock64() - t0 > 2 * idle_ticks) {
+            s = kServerStop | last;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        w[0] = s;
+        if (!(s & kServerStop)) {
+#pragma unroll
+          for (int k = 1; k < 8; ++k) w[k] = __hip_atomic_load(&bc->seq + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
-  }
-#endif
-  if (TAKE) {
     __syncthreads();
-    take_tail(t, a, lrec, lcnt, SIGNED);
+    const unsigned long long s = w[0];
+    if (s & kServerStop) return;  // block-uniform
+    last = s;
+    FoldArgs a{};
+    a.src = reinterpret_cast<const int64_t*>(w[1]);
+    a.dst = reinterpret_cast<const int64_t*>(w[2]);
+    a.n = (uint32_t)w[3];
+    a.stride = 1;
+    a.w_stride = 1;
+    a.skip_rank = -1;
+    a.shard0 = (uint32_t)(s * gridDim.x);
+    a.take_out = reinterpret_cast<int64_t*>(w[4]);
+    a.take_cap = w[5];
+    a.take_count = reinterpret_cast<unsigned long long*>(w[6]);
+    a.done = done;
+    a.seq = w[7];
+    if (threadIdx.x == 0) lcnt = 0;
+    // a failed verdict is final (no kernel boundary here: read it at the memory side)
+    const bool failed = SIGNED && __builtin_amdgcn_readfirstlane(
+                                      __hip_atomic_load(&t.ctr[ctr_index(CTR_FAIL)], __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT)) != 0;
+    __syncthreads();
+    fold_block<SIGNED, true, true>(t, D, a, blockIdx.x, failed, 0ull, nullptr);
+    __syncthreads();
+    take_tail(t, a, lrec, lcnt, SIGNED, gridDim.x);
+    __syncthreads();  // LDS (lrec, lcnt, w) is reused by the next window
   }
 }
 
@@ -619,6 +737,17 @@ void launch_fold(bool sign, bool track, const Table& t, const Delta& D, const Fo
   if (!sign && track) hipLaunchKernelGGL((k_fold<false, true, false>), g, b, 0, st, t, D, a);
   if (sign && !track) hipLaunchKernelGGL((k_fold<true, false, false>), g, b, 0, st, t, D, a);
   if (sign && track) hipLaunchKernelGGL((k_fold<true, true, false>), g, b, 0, st, t, D, a);
+}
+
+void launch_window_server(bool sign, const Table& t, const Delta& D, ServerBox* box, ServerBcast* bc,
+                          unsigned long long* done, unsigned long long seq0, unsigned long long idle_ticks,
+                          hipStream_t st) {
+  if (sign)
+    hipLaunchKernelGGL(k_window_server<true>, dim3(kServerBlocks), dim3(kFoldBS), 0, st, t, D, box, bc, done, seq0,
+                       idle_ticks);
+  else
+    hipLaunchKernelGGL(k_window_server<false>, dim3(kServerBlocks), dim3(kFoldBS), 0, st, t, D, box, bc, done, seq0,
+                       idle_ticks);
 }
 
 void launch_export(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, hipStream_t st, int part,

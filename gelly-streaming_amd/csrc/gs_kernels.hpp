@@ -31,6 +31,26 @@ struct FoldLaunch {
   unsigned long long seq = 0;
 };
 
+// Resident window server (latency path, gs_set_window_server): the host posts each
+// window into a host-mapped mailbox; block 0 polls it and hands the window to the other
+// blocks through device memory; every block folds its 256 edges, and the window's last
+// block publishes rows, count word and the completion word as the fused take does.
+constexpr uint32_t kServerBlocks = 256;                       // one per CU: a 2^16-edge window
+constexpr uint64_t kServerMaxEdges = (uint64_t)kServerBlocks * kFoldBS;
+constexpr unsigned long long kServerStop = 1ull << 63;        // mailbox seq bit: leave
+struct ServerBox {                 // host-mapped; written by the host, read by block 0
+  unsigned long long seq;          // window number (stored last, release) | kServerStop
+  unsigned long long src, dst, n, rec, cap, cnt, done_seq;
+  unsigned long long exited;       // block 0 stores 1 when the server leaves (stop or idle)
+  unsigned long long pad[7];
+};
+struct ServerBcast {               // device memory: block 0 -> the other blocks
+  unsigned long long seq, src, dst, n, rec, cap, cnt, done_seq;
+};
+void launch_window_server(bool sign, const Table& t, const Delta& D, ServerBox* box, ServerBcast* bc,
+                          unsigned long long* done, unsigned long long seq0, unsigned long long idle_ticks,
+                          hipStream_t st);
+
 void launch_init(Slot* tab, uint64_t nslots, hipStream_t st);
 void launch_reset_list(const Table& t, uint32_t* nxt, uint64_t bound, hipStream_t st);
 void launch_fold(bool sign, bool track, const Table& t, const Delta& D, const FoldLaunch& f, hipStream_t st);

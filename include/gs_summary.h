@@ -247,6 +247,20 @@ int gs_take_delta_records(gs_handle h, int64_t* rec, size_t cap, uint64_t* count
 int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, size_t n, int64_t* rec, size_t cap,
                         uint64_t* count_dev, uint64_t* count);
 int gs_delta_stage(gs_handle h, int64_t* send, size_t cap, int width, uint64_t* count);
+
+/* Resident window server for gs_fold_take_device (the latency path without a kernel
+ * launch per window). With it on, a window of at most 2^16 edges with nothing else
+ * pending is posted to ONE persistent launch through host-mapped memory: its block 0
+ * polls the mailbox and hands the window to the other blocks, every block folds 256
+ * edges, and the window's last block publishes rows, count word and completion word
+ * exactly as the fused launch does. Results are identical; any other call on the
+ * handle stops the server first (it restarts at the next window), and a server idle
+ * for ~250 ms leaves on its own. The edge buffers of a window must be complete before
+ * the window is posted and must not be rewritten while the server runs (each window
+ * reads its edges once; a stream pre-staged in HBM, as BASELINE config 5 has it).
+ * gs_window_server_stats: server launches and windows served. */
+int gs_set_window_server(gs_handle h, int on);
+int gs_window_server_stats(gs_handle h, uint64_t* launches, uint64_t* windows);
 int gs_fold_records_device(gs_handle h, const int64_t* rec, size_t n, int track);
 int gs_fold_records_counted_device(gs_handle h, const int64_t* rec, size_t cap, const uint64_t* count_dev, int track);
 int gs_fold_exchange_device(gs_handle h, const int64_t* recv, const uint64_t* counts, size_t world, size_t rows,

@@ -216,3 +216,55 @@ def test_fused_window_take_includes_pending_records(gs, oracle_mod):
         v, lab = rep.labels()
         assert np.array_equal(v, ov) and np.array_equal(lab, olab)
         assert _labels_equal(s, rep)
+
+
+@pytest.mark.parametrize("kind", ["cc", "signed"])
+def test_window_server_equals_fused_launch(gs, oracle_mod, kind):
+    """The resident window server (gs_set_window_server) gives the same windows as the
+    fused launch: the same count words (rows | FAIL_BIT) and record sets, replays to the
+    same summary, oracle-exact; reads mid-stream stop it and the next window restarts it;
+    an idle pause longer than its timeout makes it leave on its own and come back; a tiny
+    capacity hint makes the table grow between windows (the server is stopped for it)."""
+    import time
+    import torch
+    E, B = 1 << 18, 1 << 14
+    src = torch.empty(E, dtype=torch.int64, device="cuda")
+    dst = torch.empty(E, dtype=torch.int64, device="cuda")
+    if kind == "cc":
+        gs.gen_er(src, dst, 0, E, 15, 0x5EED00E5, True)
+    else:
+        gs.gen_bip(src, dst, 0, E, 13, 0x5EED0B1B, [E // 2 + 5])
+    torch.cuda.synchronize()
+    hs, hd = src.cpu().numpy(), dst.cpu().numpy()
+    recs = [torch.empty((B, 3), dtype=torch.int64, device="cuda") for _ in range(2)]
+    cnts = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+    with gs.Summary(kind, capacity_hint=1) as srv, gs.Summary(kind, capacity_hint=1 << 16) as ref, \
+            gs.Summary(kind, capacity_hint=1 << 16) as rep:
+        srv.set_delta_tracking(True)
+        ref.set_delta_tracking(True)
+        srv.set_window_server(True)
+        for w in range(E // B):
+            o = w * B
+            k1 = srv.fold_take(src[o:], dst[o:], B, recs[0], B, cnts[0])
+            k2 = ref.fold_take(src[o:], dst[o:], B, recs[1], B, cnts[1])
+            # the verdict bit agrees; the row counts may differ by a self-loop record (which
+            # thread inserts a vertex seen twice in one window is a race), the summaries not
+            assert (srv.last_take_word ^ ref.last_take_word) & gs.FAIL_BIT == 0, w
+            assert int(cnts[0].item()) == srv.last_take_word and k1 <= B and k2 <= B
+            rep.fold_records(recs[0], srv.last_take_word)
+            rep.sync()
+            if w == 3:
+                srv.labels()  # any other call stops the server; the next window restarts it
+            if w == 6:
+                time.sleep(0.6)  # longer than the idle timeout: the server leaves by itself
+        st = srv.window_server_stats()
+        assert st["windows"] >= E // B - 2 and st["launches"] >= 3, st
+        if kind == "cc":
+            ov, olab = oracle_mod.cc_labels(hs, hd)
+            for s in (srv, ref, rep):
+                v, lab = s.labels()
+                assert np.array_equal(v, ov) and np.array_equal(lab, olab)
+        else:
+            tok = oracle_mod.bip_truth(hs, hd)[0]
+            assert srv.ok() == ref.ok() == rep.ok() == tok
