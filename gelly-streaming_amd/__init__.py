@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "gs_delta_capacity", "gs_find_labels_device", "gs_capacity_stats",
     "gs_set_change_tracking", "gs_take_changes_device", "gs_take_changes",
     "gs_fold_records_counted_device", "gs_reset_config", "gs_wait_event", "gs_wait_stream", "gs_fold_device_after",
-    "gs_fold_parity", "gs_set_window_server", "gs_window_server_stats",
+    "gs_fold_parity", "gs_set_window_server", "gs_window_server_stats", "gs_set_batch_dedup",
 )
 
 FAIL_BIT = 1 << 62  # count words: a failed signed verdict (GS_FAIL_BIT)
@@ -96,6 +96,7 @@ def lib():
     L.gs_fold.argtypes = [_vp, _vp, _vp, _sz]
     L.gs_fold_parity.argtypes = [_vp, _vp, _vp, _vp, _sz]
     L.gs_set_window_server.argtypes = [_vp, ctypes.c_int]
+    L.gs_set_batch_dedup.argtypes = [_vp, ctypes.c_int]
     L.gs_window_server_stats.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]
     L.gs_fold_device.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz]
     L.gs_fold_device_after.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp]
@@ -410,6 +411,11 @@ class Summary:
         """gs_set_window_server: fold_take windows (<= 2^16 edges) go to one resident
         launch instead of a launch each."""
         _check(lib().gs_set_window_server(self._h, 1 if on else 0))
+
+    def set_batch_dedup(self, on=True):
+        """gs_set_batch_dedup: exact repeats of an edge within a fold's chunk are dropped
+        by a hashing pre-pass before the fold (identical result)."""
+        _check(lib().gs_set_batch_dedup(self._h, 1 if on else 0))
 
     def window_server_stats(self):
         a, b = _u64(), _u64()

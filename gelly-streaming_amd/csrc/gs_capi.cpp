@@ -487,6 +487,31 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     f.n = c;
     f.stride = (uint32_t)stride;
     f.w_stride = (uint32_t)w_stride;
+    if (h->dedup && !w && stride == 1 && fs.rows == 0 && !fs.n_dev) {
+      // micro-batch dedup on the fold's own stream: exact repeats of a pair in this
+      // chunk are marked skip (w bit 7) before the fold reads them
+      int set = 0;
+      if (st == h->side) set = gs_summary::kDedupSets - 1;
+      for (int li = 0; li < gs_summary::kLanes; ++li)
+        if (st == h->lane[li]) set = 1 + li;
+      if (h->dd_edges[set] < c) {
+        GS_HIP(hipStreamSynchronize(st));  // the set's previous user is done
+        (void)hipFree(h->dd_tab[set]);
+        (void)hipFree(h->dd_w[set]);
+        h->dd_tab[set] = nullptr;
+        h->dd_w[set] = nullptr;
+        const uint64_t e = next_pow2(c);
+        GS_HIP(hipMalloc(&h->dd_tab[set], 2 * e * 16));
+        GS_HIP(hipMalloc(&h->dd_w[set], e));
+        h->dd_edges[set] = e;
+      }
+      const uint64_t slots = 2 * next_pow2(c);  // load factor <= 1/2
+      GS_HIP(hipMemsetAsync(h->dd_tab[set], 0xFF, slots * 16, st));
+      gs::launch_dedup(f.src, f.dst, c, h->dd_tab[set], (uint32_t)(slots - 1), h->dd_w[set], st);
+      GS_HIP(hipGetLastError());
+      f.w = h->dd_w[set];
+      f.w_stride = 1;
+    }
     f.rows = fs.rows;
     f.skip_rank = fs.skip_rank;
     f.counts = fs.counts;
@@ -660,6 +685,10 @@ int gs_destroy(gs_handle h) {
   }
   if (h->main_ev) (void)hipEventDestroy(h->main_ev);
   if (h->ext_ev) (void)hipEventDestroy(h->ext_ev);
+  for (int i = 0; i < gs_summary::kDedupSets; ++i) {
+    (void)hipFree(h->dd_tab[i]);
+    (void)hipFree(h->dd_w[i]);
+  }
   if (h->srv_box) (void)hipHostFree(h->srv_box);
   if (h->srv_bc) (void)hipFree(h->srv_bc);
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
@@ -724,6 +753,7 @@ int gs_reset_config(gs_handle h) {
   if (h->profiling)
     if (int rc = gs_set_profiling(h, 0)) return rc;
   h->srv_on = false;
+  h->dedup = false;
   h->pipe_depth = 1;
   h->lane_next = 0;
   return gs_reset(h);
@@ -1215,6 +1245,14 @@ int gs_set_window_server(gs_handle h, int on) {
   return GS_OK;
 }
 
+int gs_set_batch_dedup(gs_handle h, int on) {
+  if (int rc = check(h)) return rc;
+  DeviceGuard g(h->device);
+  if (int rc = join_lanes(h)) return rc;
+  h->dedup = on != 0;
+  return GS_OK;
+}
+
 int gs_window_server_stats(gs_handle h, uint64_t* launches, uint64_t* windows) {
   if (int rc = check(h)) return rc;
   if (launches) *launches = h->srv_launches;
@@ -1234,7 +1272,7 @@ int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, siz
   // the resident server takes a window of at most one launch's worth of edges when
   // nothing else is pending on the handle
   if (h->srv_on && n > 0 && n <= gs::kServerMaxEdges && h->delta_fill_ub[h->dset] == 0 && !h->changes &&
-      !h->profiling && !h->lanes_dirty && !h->side_dirty)
+      !h->profiling && !h->dedup && !h->lanes_dirty && !h->side_dirty)
     return server_take(h, src, dst, n, rec, cap, cd, count);
   if (int rc_ = join_lanes(h)) return rc_;
   // One launch when the window fits one k_fold launch and nothing else is pending in

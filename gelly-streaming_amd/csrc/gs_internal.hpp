@@ -156,6 +156,14 @@ struct gs_summary {
   hipStream_t side = nullptr;
   hipEvent_t side_ev = nullptr;
   bool side_dirty = false;
+  // micro-batch dedup by hashing (gs_set_batch_dedup): one scratch set per stream a
+  // fold may run on (handle stream, lanes, side stream): pair table + skip marks
+  bool dedup = false;
+  static constexpr int kDedupSets = kLanes + 2;
+  unsigned long long* dd_tab[kDedupSets] = {};
+  uint8_t* dd_w[kDedupSets] = {};
+  uint64_t dd_edges[kDedupSets] = {};  // edges a set holds (its table has 2x that, a power of two)
+  uint64_t dd_kept_hint = 0;
   // resident window server (gs_set_window_server): one persistent launch serves the
   // latency path's windows; every other entry point stops it first (join_lanes)
   bool srv_on = false, srv_running = false;

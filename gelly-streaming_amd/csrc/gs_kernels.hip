@@ -435,6 +435,56 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
   }
 }
 
+// Micro-batch dedup by hashing (north_star's staging stage, gs_set_batch_dedup): every
+// edge of the batch is inserted as its unordered pair (min, max) into an open-addressing
+// table of 16-B slots {a, b} (2 x batch slots, all bytes 0xFF = empty), and w[i] = 0x81
+// (bit 7: skip) marks an edge whose pair another edge of the batch already stored;
+// kept edges get w[i] = 1 (the stream edge's parity: different sides). The fold then
+// skips the marked edges. Union is idempotent, so dropping an exact repeat is exact.
+// The slot's a word is claimed by a 64-bit CAS and its b word stored by the claimer
+// afterwards; a thread that finds a claimed slot whose b is not yet visible keeps its
+// edge (never a wait on another thread): an edge is dropped only when its pair is
+// fully stored by the edge that keeps it. Ids equal to the empty marker (-1) are
+// never deduplicated.
+__global__ __launch_bounds__(256) void k_dedup(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                               uint32_t n, unsigned long long* __restrict__ tab, uint32_t mask,
+                                               uint8_t* __restrict__ w) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t u = __builtin_nontemporal_load(src + i), v = __builtin_nontemporal_load(dst + i);
+  const int64_t a = u < v ? u : v, b = u < v ? v : u;
+  uint8_t out = 1;
+  if (a != -1 && b != -1) {
+    uint32_t h = (uint32_t)(((uint64_t)a * 0x9E3779B97F4A7C15ull ^ (uint64_t)b * 0xC2B2AE3D27D4EB4Full) >> 32) & mask;
+    for (uint32_t probes = 0; probes <= mask; ++probes) {
+      unsigned long long* slot = tab + 2 * (size_t)h;
+      unsigned long long ka = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ka == ~0ull) {
+        ka = atomicCAS(slot, ~0ull, (unsigned long long)a);
+        if (ka == ~0ull) {  // claimed: this edge keeps the pair
+          __hip_atomic_store(slot + 1, (unsigned long long)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      if (ka == (unsigned long long)a) {
+        const unsigned long long kb = __hip_atomic_load(slot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (kb == (unsigned long long)b) {
+          out = 0x81;  // a repeat of a stored pair
+          break;
+        }
+        if (kb == ~0ull) break;  // claimed, not yet stored: keep the edge
+      }
+      h = (h + 1) & mask;
+    }
+  }
+  w[i] = out;
+}
+
+void launch_dedup(const int64_t* src, const int64_t* dst, uint32_t n, unsigned long long* tab, uint32_t mask,
+                  uint8_t* w, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_dedup, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, n, tab, mask, w);
+}
+
 // Export (vertex, label, parity) of every occupied slot of [s_begin, s_end). Each
 // thread owns kExportPer slots of a kExportPer x kExportBS-slot tile (coalesced 16-B
 // loads); the block reserves its output range with ONE atomic per tile.

@@ -52,6 +52,9 @@ void launch_window_server(bool sign, const Table& t, const Delta& D, ServerBox* 
                           hipStream_t st);
 
 void launch_init(Slot* tab, uint64_t nslots, hipStream_t st);
+// micro-batch dedup: w[i] = 1 (keep) or 0x81 (skip: a repeat of an earlier pair of the batch)
+void launch_dedup(const int64_t* src, const int64_t* dst, uint32_t n, unsigned long long* tab, uint32_t mask,
+                  uint8_t* w, hipStream_t st);
 void launch_reset_list(const Table& t, uint32_t* nxt, uint64_t bound, hipStream_t st);
 void launch_fold(bool sign, bool track, const Table& t, const Delta& D, const FoldLaunch& f, hipStream_t st);
 void launch_export(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, hipStream_t st,

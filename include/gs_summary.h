@@ -105,6 +105,16 @@ int gs_fold_parity(gs_handle h, const int64_t* src, const int64_t* dst, const ui
  * gs_wait_stream / gs_fold_device_after below. */
 int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n, size_t stride);
 
+/* Micro-batch dedup by hashing (north_star's staging stage). With it on, every fold of
+ * edges without a parity array (gs_fold, gs_fold_device with stride 1, the window take)
+ * first inserts each edge's unordered pair into a batch hash table and marks exact
+ * repeats of a pair within the launch's chunk; the fold skips them (union is
+ * idempotent: the result is identical). It pays one batch-table insert per edge, so it
+ * is off by default: it wins on streams with many repeated edges (the reference's
+ * bipartite example repeats every edge 10 times, BipartitenessCheckExample.java:109-118)
+ * and loses on RMAT, whose repeats are rare. */
+int gs_set_batch_dedup(gs_handle h, int on);
+
 /* Cross-stream ordering for callers whose edges are produced on another stream (a
  * decoder, a copy engine, torch): gs_wait_event makes every later operation of the
  * handle wait for `event` (a hipEvent_t the producer recorded); gs_wait_stream for
