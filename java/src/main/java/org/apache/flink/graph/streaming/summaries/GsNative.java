@@ -53,6 +53,10 @@ final class GsNative {
 	static native void setDeltaTracking(long h, boolean on);
 	static native long foldTake(long h, long srcDev, long dstDev, long n, long recDev, long cap, long cntDev);
 	static native void foldRecords(long h, long recDev, long countWord);
+	static native void setWindowServer(long h, boolean on);  // gs_set_window_server: one resident launch
+
+	// ---- staging (gs_set_batch_dedup): repeats of an edge within a flush are dropped first
+	static native void setBatchDedup(long h, boolean on);
 
 	// ---- multi-GPU group (include/gs_group.h)
 	static native byte[] groupUniqueId();

@@ -287,6 +287,16 @@ JNIEXPORT void JNICALL FN(foldRecords)(JNIEnv* env, jclass c, jlong h, jlong rec
   CHECK(gs_fold_records_device(H(h), (const int64_t*)(intptr_t)rec, (size_t)countWord, 0));
 }
 
+JNIEXPORT void JNICALL FN(setWindowServer)(JNIEnv* env, jclass c, jlong h, jboolean on) {
+  (void)c;
+  CHECK(gs_set_window_server(H(h), on ? 1 : 0));
+}
+
+JNIEXPORT void JNICALL FN(setBatchDedup)(JNIEnv* env, jclass c, jlong h, jboolean on) {
+  (void)c;
+  CHECK(gs_set_batch_dedup(H(h), on ? 1 : 0));
+}
+
 /* ---- multi-GPU group ------------------------------------------------------ */
 
 JNIEXPORT jbyteArray JNICALL FN(groupUniqueId)(JNIEnv* env, jclass c) {
