@@ -130,6 +130,9 @@ def parse():
                    help="native: RCCL inside libgs_summary (gs_group_*); torch: torch.distributed all-gather")
     p.add_argument("--er-mode", choices=["launch", "server"], default="server",
                    help="er-latency: which window mode `value` reports (both are measured)")
+    p.add_argument("--profile-only", action="store_true",
+                   help="profiling runs (tools/pmc_workload.sh): only the timed work -- no checks, no host legs, "
+                        "so that every dispatch of the profiled kernel is of the measured shape")
     p.add_argument("--launch-check", action="store_true",
                    help="launcher test (CPU, gloo): form the world exactly as the bench does, print one JSON line "
                         "with the world that formed, touch no GPU")
@@ -305,6 +308,13 @@ def bench_bip(args):
                 "bytes_per_edge": BYTES_PER_EDGE_SPARSE, "edges_per_launch": int(per_launch),
                 "fold_avg_us": round(fold_avg_ms * 1e3, 2), "fold_launches": int(nf)}
         roof.update(extra)
+    if args.profile_only:  # profiling run: the timed steps only
+        if group is not None:
+            group.close()
+        summ.close()
+        if world > 1 or args.exchange:
+            dist.destroy_process_group()
+        return
     # odd-cycle variant (outside the timed region)
     inject = [E // 8, E // 4, E // 2, 3 * E // 4]
     gs.gen_bip(src, dst, start, per, logside, seed, [i for i in inject if start <= i < start + per],
@@ -505,6 +515,8 @@ def bench_ingest(args):
     for _ in range(args.steps):
         n, bad = gs.parse_edges_device(text, ps, pd)
     el = (time.perf_counter() - t0) / args.steps
+    if args.profile_only:  # profiling run: the device-resident parses only
+        return
     ok = n == E and bad == -1 and bool(torch.equal(ps, src)) and bool(torch.equal(pd, dst))
     nbytes = int(text.numel())
     alg = nbytes + 16 * E  # text read once + int64 pair written per edge

@@ -295,6 +295,7 @@ struct gs_group {
   int nranks = 1, rank = 0;
   int width = 3;                 // int64 per exchange row: {a, b} for CC (16 B), {a, b, parity} signed
   bool exchange = false;         // false: tree-combine-only group
+  bool prev_track = false;       // the summary's delta tracking before the group turned it on
   bool self_apply = false;       // test knob (GS_GROUP_SELF_APPLY=1): also fold this rank's own rows back
   uint64_t batch = 0, rows_cap = 0;
   // exchange b uses buffer set b % kLag (send, counts, headers, receive) and delta set b % kDeltaSets
@@ -457,6 +458,7 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
     if (int rc = join_lanes(h)) return bail(rc);
     if (int rc = ensure_lanes(h, kGroupLanes)) return bail(rc);  // own folds rotate over the lanes
     if (int rc = ensure_delta_list(h, batch_edges)) return bail(rc);
+    g->prev_track = h->track;
     if (int rc = gs_set_delta_tracking(h, 1)) return bail(rc);
     g->rows_cap = (uint64_t)gs::kShards * h->delta_shard_cap;
     bool ok = hipHostMalloc(&g->hdr_host, kLag * (size_t)(nranks + 1) * 8,
@@ -767,6 +769,7 @@ int gs_group_destroy(gs_group_t g) {
       g->h->side_ev = nullptr;
       g->h->side_dirty = false;
       g->h->group_lanes = 0;
+      if (!g->prev_track) (void)gs_set_delta_tracking(g->h, 0);  // as before the group
     }
     (void)hipStreamDestroy(g->as);
   }

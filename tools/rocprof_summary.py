@@ -12,6 +12,13 @@ fabric, an upper bound of HBM bytes, not HBM bytes.
 For ingest, the SQ pass gives VALU and LDS activity and LDS bank conflicts.
 Usage: python tools/rocprof_summary.py <dir> <tag> <pipeline> [batch] [--workload rmat-cc|bip|ingest]
 """
+import glob
+import json
+import os
+import sqlite3
+import sys
+from collections import defaultdict
+
 argv = list(sys.argv[1:])
 workload = "rmat-cc"
 if "--workload" in argv:
@@ -87,6 +94,13 @@ for k in list(out["kernels"]):
             "valu_insts_per_wave": r.get("pmc_SQ_INSTS_VALU", 0) / max(r.get("pmc_SQ_WAVES", 0), 1),
             "lds_insts_per_wave": r.get("pmc_SQ_INSTS_LDS", 0) / max(r.get("pmc_SQ_WAVES", 0), 1),
         }
+        if r.get("pmc_GRBM_GUI_ACTIVE"):  # rocprofv3's derived formulas (rocprofv3 -L, gfx94x fallback), CU_NUM 256
+            g = r["pmc_GRBM_GUI_ACTIVE"] * 256.0
+            r["derived_sq"]["VALUBusy_pct"] = 100.0 * r.get("pmc_SQ_ACTIVE_INST_VALU", 0) / g
+            r["derived_sq"]["LDSBankConflict_pct"] = 100.0 * r.get("pmc_SQ_LDS_BANK_CONFLICT", 0) / g
+            if "pmc_SQ_LDS_IDX_ACTIVE" in r:
+                r["derived_sq"]["lds_conflict_per_idx_cycle"] = r.get("pmc_SQ_LDS_BANK_CONFLICT", 0) / max(
+                    r["pmc_SQ_LDS_IDX_ACTIVE"] - r.get("pmc_SQ_LDS_BANK_CONFLICT", 0), 1)
     if "pmc_FETCH_SIZE" in r:
         rd_req = r.get("pmc_TCC_EA0_RDREQ_sum")
         r["derived"] = {
