@@ -169,25 +169,32 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
   if (threadIdx.x == 0) last_sh = atomicAdd(t.ctr + ctr_index(CTR_TAKE_DONE), 1u) == nblocks - 1;
   __syncthreads();
   if (!last_sh || threadIdx.x >= 64) return;
+  // one round of loads, issued together (each is a dependent memory hop of the window's
+  // latency): the 64 shard counts, the take total (lane 0) and, signed, the verdict
+  // (lane 1; every block's verdict updates are memory-side atomics that preceded its
+  // ticket, so the flag is read at the memory side too, never from a stale line)
+  unsigned long long* take = reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE));
   unsigned long long nv = __hip_atomic_load(t.ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long tot = threadIdx.x == 0 ? __hip_atomic_load(take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+  const uint32_t fl = (signed_kind && threadIdx.x == 1) ? atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 0u) : 0u;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) nv += __shfl_xor(nv, o, 64);
+  const bool failed = __shfl(fl, 1, 64) != 0u;
   if (threadIdx.x != 0) return;
-  unsigned long long* take = reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE));
-  const unsigned long long total = __hip_atomic_load(take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // every block's verdict updates are memory-side atomics that preceded its ticket; the
-  // flag is read at the memory side too (an atomic), never from a possibly stale line
-  const bool failed = signed_kind && atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 0u) != 0u;
+  const unsigned long long total = tot;
   const unsigned long long word = total | (failed ? kFailBit : 0ull);
-  *a.take_count = word;
+  __hip_atomic_store(a.take_count, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
   atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_SENT)), total < a.take_cap ? total : a.take_cap);
   __hip_atomic_store(take, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(t.ctr + ctr_index(CTR_TAKE_DONE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __threadfence_system();
   __hip_atomic_store(a.done + 1, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(a.done + 2, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(a.done, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // one system release (L2 write-back) for everything above, its wait explicit
+  // (MI355X_MICROARCH.md compiler hazard), then the completion word
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <bool SIGNED, bool TRACK, bool TAKE>
