@@ -64,11 +64,12 @@ enum CounterBlock : int {
   CTR_SCAN_ALL,                  // change emission: emit every vertex (after a table rebuild)
   CTR_TAKE,                      // fused window take (k_fold TAKE): output rows reserved (u64)
   CTR_TAKE_HI,
-  CTR_TAKE_DONE,                 //   block ticket
+  CTR_TAKE_DONE,                 //   block ticket, top level: shards whose blocks are all done
   CTR_DBG_HOOKS,                 // debug build (-DGS_DEBUG_COUNTERS): hook calls,
   CTR_DBG_ITERS,                 //   hook-loop iterations,
   CTR_DBG_CASFAIL,               //   failed hook CASes
-  CTR_COUNT
+  CTR_TAKE_SHARD,                // [kTicketShards] block tickets, first level (block b -> shard b mod 16)
+  CTR_COUNT = CTR_TAKE_SHARD + 16
 };
 __host__ __device__ constexpr int ctr_index(int c) { return c * kCtrStride; }
 

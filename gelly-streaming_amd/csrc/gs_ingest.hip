@@ -20,6 +20,9 @@
 // 338-354 us with 16 KiB tiles (five 16-B loads in flight per thread instead of three).
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "gs_ingest.h"
 #include "gs_ingest.hpp"
 
@@ -208,10 +211,48 @@ __device__ __forceinline__ uint32_t seg_nl_mask(const uint8_t* L, uint32_t q, ui
   return nl;
 }
 
+// '\n' mask (bit j: byte 16 c + j) of the 16-byte LDS chunk c of the tile, with the
+// same end-of-text rule as seg_nl_mask. Chunks are read block-contiguously (lane i of a
+// wave reads bytes 16 i ..): conflict-free 16-B LDS reads, where a thread reading its own
+// 64-byte segment put the lanes of a wave 64 B apart (16-way bank conflicts).
+__device__ __forceinline__ uint32_t chunk_nl_mask(const uint8_t* L, uint32_t c, uint64_t vend) {
+  const uint4 w = *reinterpret_cast<const uint4*>(L + 16 * c);
+  const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+  uint32_t nl = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) nl |= (((ww[k] >> (8 * bb)) & 0xFFu) == '\n' ? 1u : 0u) << (4 * k + bb);
+  const uint64_t b0 = 16ull * c;
+  if (vend < b0 + 16) nl = vend <= b0 ? (vend == b0 ? 1u : 0u) : ((nl & ((1u << (vend - b0)) - 1u)) | (1u << (vend - b0)));
+  return nl;
+}
+
+__device__ __attribute__((noinline)) void parse_tile(const uint8_t* __restrict__ text, uint64_t len, int sep,
+                                           const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
+                                           int64_t* __restrict__ dst, uint64_t cap,
+                                           unsigned long long* __restrict__ bad, bool aligned, uint64_t tile);
+
+// Each block parses `tpb` consecutive tiles, one after another (the block's LDS is
+// reused; its loads are not prefetched across tiles: that took the kernel from 42 to
+// 111 VGPRs in round 2). Longer-lived blocks, fewer of them.
 __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                                const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                                int64_t* __restrict__ dst, uint64_t cap,
-                                               unsigned long long* __restrict__ bad, bool aligned) {
+                                               unsigned long long* __restrict__ bad, bool aligned, uint64_t tiles,
+                                               uint32_t tpb) {
+  const uint64_t first = (uint64_t)blockIdx.x * tpb;
+  const uint64_t last = min(tiles, first + tpb);
+  for (uint64_t tile = first; tile < last; ++tile) {
+    parse_tile(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile);
+    __syncthreads();  // the next tile restages the LDS
+  }
+}
+
+__device__ __attribute__((noinline)) void parse_tile(const uint8_t* __restrict__ text, uint64_t len, int sep,
+                                           const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
+                                           int64_t* __restrict__ dst, uint64_t cap,
+                                           unsigned long long* __restrict__ bad, bool aligned, uint64_t tile) {
   constexpr uint32_t kSeg = kTile / 256;  // bytes per thread in the line-start scan
   constexpr uint32_t kExtra = 2;          // '\n' masks past the tile: lines that cross its end
   constexpr uint32_t kSlots = (kTile + kOver + 4095) / 4096;
@@ -220,7 +261,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
   __shared__ __align__(16) uint8_t lds[kLds0 + kTile + kOver];
   __shared__ uint64_t nlm[256 + kExtra];
   __shared__ uint32_t wsum[4];
-  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  const uint64_t t0 = tile * kTile;
   const uint64_t staged_end = min(len, t0 + kTile + kOver);
   // stage [t0, staged_end) at lds[kLds0..] with 16-B stores; lds[kLds0 - 1] = byte t0 - 1.
   // Every thread's global loads (five 16-B slots, 4 KiB apart) are issued before any is
@@ -256,13 +297,17 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
   const uint32_t seg = threadIdx.x * kSeg;
   const uint64_t tile_end = min(len, t0 + kTile);
   const uint64_t vend = staged_end == len ? len - t0 : ~0ull;  // the text ends inside the staged bytes
-  auto mask64 = [&](uint32_t q) {
-    return (uint64_t)seg_nl_mask(L, 2 * q, vend) | ((uint64_t)seg_nl_mask(L, 2 * q + 1, vend) << 32);
-  };
-  const uint64_t nl = mask64(threadIdx.x);
-  nlm[threadIdx.x] = nl;
-  if (threadIdx.x < kExtra) nlm[256 + threadIdx.x] = mask64(256 + threadIdx.x);
-  uint64_t mine = (nl << 1) | (L[(int)seg - 1] == '\n' ? 1ull : 0ull);  // bit j: a line starts at seg + j
+  // 16-bit chunk masks written as the u16 quarters of nlm (little endian: nlm[q] is
+  // then segment q's 64-bit mask); 4 chunks per thread + the kExtra segments' chunks
+  uint16_t* m16 = reinterpret_cast<uint16_t*>(nlm);
+#pragma unroll
+  for (uint32_t r = 0; r < 4; ++r) m16[r * 256 + threadIdx.x] = (uint16_t)chunk_nl_mask(L, r * 256 + threadIdx.x, vend);
+  if (threadIdx.x < 4 * kExtra) m16[1024 + threadIdx.x] = (uint16_t)chunk_nl_mask(L, 1024 + threadIdx.x, vend);
+  __syncthreads();
+  const uint64_t nl = nlm[threadIdx.x];
+  // bit j: a line starts at seg + j (byte seg + j - 1 is '\n': the previous segment's top bit)
+  const bool prev_nl = threadIdx.x == 0 ? L[-1] == '\n' : (nlm[threadIdx.x - 1] >> 63) != 0;
+  uint64_t mine = (nl << 1) | (prev_nl ? 1ull : 0ull);
   const uint64_t valid = t0 + seg >= tile_end ? 0 : min<uint64_t>(kSeg, tile_end - (t0 + seg));
   if (valid < 64) mine &= (1ull << valid) - 1ull;
   const uint32_t c = __popcll(mine);
@@ -280,7 +325,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
     if (q < wid) wbase += wsum[q];
   // (2) each thread parses the lines that start in its segment; the k-th start of the
   //     tile follows k '\n' of the tile if a line starts at t0, else k + 1
-  uint64_t line = tile_pre[blockIdx.x] + (L[-1] == '\n' ? 0u : 1u) + wbase + (x - c);
+  uint64_t line = tile_pre[tile] + (L[-1] == '\n' ? 0u : 1u) + wbase + (x - c);
   const LineBuf b{lds, text, t0, len, staged_end};
   while (mine) {
     const uint32_t j = __ffsll((unsigned long long)mine) - 1;
@@ -347,8 +392,12 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
   if (hipcub::DeviceScan::ExclusiveSum(s.cub_tmp, tmp, s.tile_cnt, s.tile_pre, (int)tiles, st) != hipSuccess)
     return -1;
   if (hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess) return -1;
-  hipLaunchKernelGGL(k_parse, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, s.tile_pre, src, dst,
-                     (uint64_t)cap, s.bad, aligned);
+  static const uint32_t tpb = [] {
+    const char* e = getenv("GS_PARSE_TPB");  // experiment knob: tiles per k_parse block
+    return (uint32_t)(e ? std::max(1, atoi(e)) : 1);
+  }();
+  hipLaunchKernelGGL(k_parse, dim3((unsigned)((tiles + tpb - 1) / tpb)), dim3(256), 0, st, t, (uint64_t)len, sep,
+                     s.tile_pre, src, dst, (uint64_t)cap, s.bad, aligned, tiles, tpb);
   hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
                      s.bad, s.res);
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -144,7 +144,7 @@ __device__ unsigned long long g_blog_n = 0;
 // A signed summary's count word carries the verdict (| kFailBit once it failed): the
 // take's consumer replays the records AND the verdict (Candidates.merge :79-81).
 __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, const int64_t* lrec, uint32_t lcnt,
-                                          bool signed_kind, uint32_t nblocks) {
+                                          bool signed_kind, uint32_t blk, uint32_t nblocks) {
   __shared__ unsigned long long base_sh;
   __shared__ uint32_t last_sh;
   const uint32_t nb = min(lcnt, kFoldBS);
@@ -166,7 +166,20 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
   // alone does not wait for global stores); no L2 writeback needed for write-through rows
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (threadIdx.x == 0) last_sh = atomicAdd(t.ctr + ctr_index(CTR_TAKE_DONE), 1u) == nblocks - 1;
+  // Two-level ticket: same-address atomics serialise at the memory side (11.4 ns each,
+  // profiles/r01_calib_atomic.log), so 256 blocks on one counter cost ~2.9 us of the
+  // window. Block b counts on shard b mod 16; the shard's last block counts on the top
+  // word; the last of those is the window's last block. (Each count is a memory-side
+  // atomic made after the counting block's rows were acknowledged: the chain of
+  // returned values orders every block's rows before the last block's reads.)
+  if (threadIdx.x == 0) {
+    constexpr uint32_t kTS = 16;
+    const uint32_t shard = blk % kTS;
+    const uint32_t in_shard = (nblocks - shard + kTS - 1) / kTS;  // blocks b < nblocks with b mod 16 == shard
+    bool last = atomicAdd(t.ctr + ctr_index(CTR_TAKE_SHARD + shard), 1u) == in_shard - 1;
+    if (last) last = atomicAdd(t.ctr + ctr_index(CTR_TAKE_DONE), 1u) == min(nblocks, kTS) - 1;
+    last_sh = last;
+  }
   __syncthreads();
   if (!last_sh || threadIdx.x >= 64) return;
   // one round of loads, issued together (each is a dependent memory hop of the window's
@@ -188,6 +201,9 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
   atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_SENT)), total < a.take_cap ? total : a.take_cap);
   __hip_atomic_store(take, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(t.ctr + ctr_index(CTR_TAKE_DONE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    __hip_atomic_store(t.ctr + ctr_index(CTR_TAKE_SHARD + k), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(a.done + 1, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(a.done + 2, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   // one system release (L2 write-back) for everything above, its wait explicit
@@ -261,7 +277,7 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
 #endif
   if (TAKE) {
     __syncthreads();
-    take_tail(t, a, lrec, lcnt, SIGNED, gridDim.x);
+    take_tail(t, a, lrec, lcnt, SIGNED, blockIdx.x, gridDim.x);
   }
 }
 
@@ -429,15 +445,20 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
     a.take_count = reinterpret_cast<unsigned long long*>(w[6]);
     a.done = done;
     a.seq = w[7];
-    if (threadIdx.x == 0) lcnt = 0;
-    // a failed verdict is final (no kernel boundary here: read it at the memory side)
-    const bool failed = SIGNED && __builtin_amdgcn_readfirstlane(
-                                      __hip_atomic_load(&t.ctr[ctr_index(CTR_FAIL)], __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT)) != 0;
-    __syncthreads();
-    fold_block<SIGNED, true, true>(t, D, a, blockIdx.x, failed, 0ull, nullptr);
-    __syncthreads();
-    take_tail(t, a, lrec, lcnt, SIGNED, gridDim.x);
+    // only the blocks that hold edges of this window take part (a small window is one
+    // block's ticket, not the whole grid's)
+    const uint32_t active = (a.n + kFoldBS - 1) / kFoldBS;
+    if (blockIdx.x < active) {
+      if (threadIdx.x == 0) lcnt = 0;
+      // a failed verdict is final (no kernel boundary here: read it at the memory side)
+      const bool failed = SIGNED && __builtin_amdgcn_readfirstlane(
+                                        __hip_atomic_load(&t.ctr[ctr_index(CTR_FAIL)], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)) != 0;
+      __syncthreads();
+      fold_block<SIGNED, true, true>(t, D, a, blockIdx.x, failed, 0ull, nullptr);
+      __syncthreads();
+      take_tail(t, a, lrec, lcnt, SIGNED, blockIdx.x, active);
+    }
     __syncthreads();  // LDS (lrec, lcnt, w) is reused by the next window
   }
 }
