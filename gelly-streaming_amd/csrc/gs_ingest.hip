@@ -228,19 +228,27 @@ __device__ __forceinline__ uint32_t chunk_nl_mask(const uint8_t* L, uint32_t c, 
   return nl;
 }
 
-__device__ __attribute__((noinline)) void parse_tile(const uint8_t* __restrict__ text, uint64_t len, int sep,
+__device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                            const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                            int64_t* __restrict__ dst, uint64_t cap,
                                            unsigned long long* __restrict__ bad, bool aligned, uint64_t tile);
 
-// Each block parses `tpb` consecutive tiles, one after another (the block's LDS is
-// reused; its loads are not prefetched across tiles: that took the kernel from 42 to
-// 111 VGPRs in round 2). Longer-lived blocks, fewer of them.
+// One tile per block (44 VGPRs, 8 blocks per CU).
 __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                                const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                                int64_t* __restrict__ dst, uint64_t cap,
-                                               unsigned long long* __restrict__ bad, bool aligned, uint64_t tiles,
-                                               uint32_t tpb) {
+                                               unsigned long long* __restrict__ bad, bool aligned) {
+  parse_tile(text, len, sep, tile_pre, src, dst, cap, bad, aligned, blockIdx.x);
+}
+
+// Experiment (GS_PARSE_TPB > 1): each block parses `tpb` consecutive tiles, one after
+// another (LDS reused, no prefetch across tiles). The loop costs registers (88 VGPRs,
+// 5 blocks per CU).
+__global__ __launch_bounds__(256) void k_parse_multi(const uint8_t* __restrict__ text, uint64_t len, int sep,
+                                                     const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
+                                                     int64_t* __restrict__ dst, uint64_t cap,
+                                                     unsigned long long* __restrict__ bad, bool aligned,
+                                                     uint64_t tiles, uint32_t tpb) {
   const uint64_t first = (uint64_t)blockIdx.x * tpb;
   const uint64_t last = min(tiles, first + tpb);
   for (uint64_t tile = first; tile < last; ++tile) {
@@ -249,7 +257,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
   }
 }
 
-__device__ __attribute__((noinline)) void parse_tile(const uint8_t* __restrict__ text, uint64_t len, int sep,
+__device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                            const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                            int64_t* __restrict__ dst, uint64_t cap,
                                            unsigned long long* __restrict__ bad, bool aligned, uint64_t tile) {
@@ -396,8 +404,12 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
     const char* e = getenv("GS_PARSE_TPB");  // experiment knob: tiles per k_parse block
     return (uint32_t)(e ? std::max(1, atoi(e)) : 1);
   }();
-  hipLaunchKernelGGL(k_parse, dim3((unsigned)((tiles + tpb - 1) / tpb)), dim3(256), 0, st, t, (uint64_t)len, sep,
-                     s.tile_pre, src, dst, (uint64_t)cap, s.bad, aligned, tiles, tpb);
+  if (tpb > 1)
+    hipLaunchKernelGGL(k_parse_multi, dim3((unsigned)((tiles + tpb - 1) / tpb)), dim3(256), 0, st, t, (uint64_t)len,
+                       sep, s.tile_pre, src, dst, (uint64_t)cap, s.bad, aligned, tiles, tpb);
+  else
+    hipLaunchKernelGGL(k_parse, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, s.tile_pre, src, dst,
+                       (uint64_t)cap, s.bad, aligned);
   hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
                      s.bad, s.res);
   return hipGetLastError() == hipSuccess ? 0 : -1;

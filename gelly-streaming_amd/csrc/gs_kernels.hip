@@ -148,10 +148,13 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
   __shared__ unsigned long long base_sh;
   __shared__ uint32_t last_sh;
   const uint32_t nb = min(lcnt, kFoldBS);
+  // a one-block window owns the whole output: no reservation and no ticket (two
+  // dependent atomics of a small window's latency)
+  const bool solo = nblocks == 1;
   if (threadIdx.x == 0)
-    base_sh = nb ? atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE)),
-                             (unsigned long long)nb)
-                 : 0ull;
+    base_sh = (nb && !solo) ? atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE)),
+                                        (unsigned long long)nb)
+                            : 0ull;
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < nb; j += kFoldBS) {
     const unsigned long long pos = base_sh + j;
@@ -172,12 +175,18 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
   // word; the last of those is the window's last block. (Each count is a memory-side
   // atomic made after the counting block's rows were acknowledged: the chain of
   // returned values orders every block's rows before the last block's reads.)
+  // (Up to 16 blocks count on the top word directly; one block needs no ticket.)
   if (threadIdx.x == 0) {
     constexpr uint32_t kTS = 16;
-    const uint32_t shard = blk % kTS;
-    const uint32_t in_shard = (nblocks - shard + kTS - 1) / kTS;  // blocks b < nblocks with b mod 16 == shard
-    bool last = atomicAdd(t.ctr + ctr_index(CTR_TAKE_SHARD + shard), 1u) == in_shard - 1;
-    if (last) last = atomicAdd(t.ctr + ctr_index(CTR_TAKE_DONE), 1u) == min(nblocks, kTS) - 1;
+    bool last = true;
+    if (nblocks > kTS) {
+      const uint32_t shard = blk % kTS;
+      const uint32_t in_shard = (nblocks - shard + kTS - 1) / kTS;  // blocks b < nblocks with b mod 16 == shard
+      last = atomicAdd(t.ctr + ctr_index(CTR_TAKE_SHARD + shard), 1u) == in_shard - 1;
+      if (last) last = atomicAdd(t.ctr + ctr_index(CTR_TAKE_DONE), 1u) == kTS - 1;
+    } else if (nblocks > 1) {
+      last = atomicAdd(t.ctr + ctr_index(CTR_TAKE_DONE), 1u) == nblocks - 1;
+    }
     last_sh = last;
   }
   __syncthreads();
@@ -189,7 +198,9 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
   unsigned long long* take = reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE));
   unsigned long long nv = __hip_atomic_load(t.ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
-  unsigned long long tot = threadIdx.x == 0 ? __hip_atomic_load(take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+  unsigned long long tot = threadIdx.x == 0 ? (solo ? (unsigned long long)lcnt
+                                                    : __hip_atomic_load(take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                            : 0ull;
   const uint32_t fl = (signed_kind && threadIdx.x == 1) ? atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 0u) : 0u;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) nv += __shfl_xor(nv, o, 64);
@@ -199,11 +210,15 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
   const unsigned long long word = total | (failed ? kFailBit : 0ull);
   __hip_atomic_store(a.take_count, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
   atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_SENT)), total < a.take_cap ? total : a.take_cap);
-  __hip_atomic_store(take, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(t.ctr + ctr_index(CTR_TAKE_DONE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!solo) {
+    __hip_atomic_store(take, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(t.ctr + ctr_index(CTR_TAKE_DONE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (nblocks > 16) {
 #pragma unroll
-  for (int k = 0; k < 16; ++k)
-    __hip_atomic_store(t.ctr + ctr_index(CTR_TAKE_SHARD + k), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < 16; ++k)
+      __hip_atomic_store(t.ctr + ctr_index(CTR_TAKE_SHARD + k), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __hip_atomic_store(a.done + 1, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(a.done + 2, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   // one system release (L2 write-back) for everything above, its wait explicit
