@@ -16,11 +16,10 @@ import numpy as np
 
 # Pipelined folds run on up to four lane streams beside the handle stream (and a group
 # adds its communication streams). HIP maps streams onto GPU_MAX_HW_QUEUES hardware
-# queues (default 4) and streams that share a queue run in submission order: with the
-# default, RMAT-26 folds measured 47.7-48.4 ms per pass instead of 40.1 (tools run
-# without the bench's setting, this round). Ask for 8 unless the caller chose; it takes
-# effect only if HIP has not initialised yet (bench.py sets it before importing torch).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# queues (default 4) and streams that share a queue run in submission order; the
+# library is arranged for the default (lanes created on first use, a group's lanes
+# ordered behind the handle stream only when it has new work: DESIGN.md section 5), so
+# the binding does not change the process's setting.
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libgs_summary.so")

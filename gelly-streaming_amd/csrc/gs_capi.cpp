@@ -315,6 +315,7 @@ int ensure_capacity(gs_summary* h, size_t n) {
 
 int check(gs_handle h) {
   if (!h) return fail(GS_ERR_INVALID, "null handle");
+  ++h->api_calls;  // (a group orders its own-fold lanes behind the handle stream after any call)
   return GS_OK;
 }
 
@@ -385,7 +386,7 @@ int wait_stream(gs_summary* h, const uint32_t* vals, uint64_t* value, int nvals,
   gs::launch_signal(h->done_dev, seq, vals, nvals, stride, h->stream);
   GS_HIP(hipGetLastError());
   if (int rc = wait_done(h, seq)) return rc;
-  if (value) *value = __atomic_load_n(h->h_done + 1, __ATOMIC_ACQUIRE);
+  if (value) return done_value_read(h, 1, seq, value);
   return GS_OK;
 }
 
@@ -401,6 +402,23 @@ int wait_done(gs_summary* h, unsigned long long seq) {
   GS_HIP(hipStreamSynchronize(h->stream));
   if (__atomic_load_n(h->h_done, __ATOMIC_ACQUIRE) < seq) return fail(GS_ERR_HIP, "completion word not written");
   return GS_OK;
+}
+
+// Value i (1, 2) of the completion record written with sequence number seq: tagged
+// with seq mod 2^16 (gs::done_value); once the sequence word is seen the value has
+// landed too (its writer drains it first), the tag check makes that explicit.
+int done_value_read(gs_summary* h, int i, unsigned long long seq, uint64_t* out) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t k = 1;; ++k) {
+    const unsigned long long w = __atomic_load_n(h->h_done + i, __ATOMIC_ACQUIRE);
+    if ((w >> 48) == (seq & 0xFFFFull)) {
+      *out = gs::done_decode(w);
+      return GS_OK;
+    }
+    if ((k & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1))
+      return fail(GS_ERR_HIP, "completion record value not tagged with its sequence number");
+    __builtin_ia32_pause();
+  }
 }
 
 // Error flags, read with ONE host synchronisation. Also refreshes whether the
@@ -1198,14 +1216,16 @@ static int server_take(gs_handle h, const int64_t* src, const int64_t* dst, size
   for (int attempt = 0;; ++attempt) {
     if (!h->srv_running)
       if (int rc = server_start(h)) return rc;
+    // the descriptor words tagged with seq (the server reads the whole line in one load
+    // round and takes it when every tag matches), then seq itself
     gs::ServerBox* b = h->srv_box;
-    b->src = (unsigned long long)src;
-    b->dst = (unsigned long long)dst;
-    b->n = n;
-    b->rec = (unsigned long long)rec;
-    b->cap = cap;
-    b->cnt = (unsigned long long)cd;
-    b->done_seq = dseq;
+    b->src = gs::tag_word(seq, (unsigned long long)src);
+    b->dst = gs::tag_word(seq, (unsigned long long)dst);
+    b->n = gs::tag_word(seq, n);
+    b->rec = gs::tag_word(seq, (unsigned long long)rec);
+    b->cap = gs::tag_word(seq, std::min<unsigned long long>(cap, 1ull << 40));
+    b->cnt = gs::tag_word(seq, (unsigned long long)cd);
+    b->done_seq = gs::tag_word(seq, dseq);
     __atomic_store_n(&b->seq, seq, __ATOMIC_RELEASE);
     const auto t0 = std::chrono::steady_clock::now();
     bool left = false;
@@ -1227,8 +1247,10 @@ static int server_take(gs_handle h, const int64_t* src, const int64_t* dst, size
   }
   h->srv_seq = seq;
   h->srv_windows++;
-  note_exact_count(h, __atomic_load_n(h->h_done + 1, __ATOMIC_ACQUIRE));
-  *count = __atomic_load_n(h->h_done + 2, __ATOMIC_ACQUIRE);
+  uint64_t nv = 0;
+  if (int rc = done_value_read(h, 1, dseq, &nv)) return rc;
+  if (int rc = done_value_read(h, 2, dseq, count)) return rc;
+  note_exact_count(h, nv);
   return check_flags_now(h);
 }
 
@@ -1294,8 +1316,10 @@ int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, siz
   fs.take_seq = &seq;
   if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, true, true, fs)) return rc;
   if (int rc = wait_done(h, seq)) return rc;
-  note_exact_count(h, __atomic_load_n(h->h_done + 1, __ATOMIC_ACQUIRE));
-  *count = __atomic_load_n(h->h_done + 2, __ATOMIC_ACQUIRE);
+  uint64_t nv = 0;
+  if (int rc = done_value_read(h, 1, seq, &nv)) return rc;
+  if (int rc = done_value_read(h, 2, seq, count)) return rc;
+  note_exact_count(h, nv);
   return check_flags_now(h);
 }
 

@@ -313,6 +313,7 @@ struct gs_group {
   uint64_t own_edges = 0;  // own edges folded since create / finish (the ramp's position)
   uint64_t ramp_edges = 1ull << 22, ramp_batch = 1ull << 20;  // gs_group_set_ramp
   uint64_t done = 0;    // exchanges whose data half has been issued
+  uint64_t api_seen = 0;  // h->api_calls at the previous fold call (lane ordering)
   // statistics
   uint64_t exchanges = 0, rows_received = 0, live_received = 0;
   bool hostprof = false;  // GS_GROUP_HOSTPROF=1: host seconds per phase, printed at destroy
@@ -521,11 +522,20 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   // remote folds all run on other streams, so own folds go back to back.
   const bool lanes = !h->profiling && !g->no_lanes;  // (profiling serialises folds on the handle stream)
   if (lanes) {
-    // Every call: the lanes start behind the caller's work on the handle stream (a reset,
-    // edges written there, a buffer reused after a sync through it), as gs_fold_device
-    // is ordered after it -- not only at the first exchange.
-    GS_HIP(hipEventRecord(h->main_ev, h->stream));
-    for (int i = 0; i < kGroupLanes; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], h->main_ev, 0));
+    // The lanes start behind the caller's work on the handle stream (a reset, edges
+    // written there, a buffer reused after a sync through it), as gs_fold_device is
+    // ordered after it: at the first exchange, and whenever any gs_* call was made on
+    // the handle since the previous group call (a caller that queues its own
+    // kernels on gs_get_stream(h) marks them with gs_wait_stream(h, that stream)).
+    // Not at every call: with the box's 4 hardware queues the handle stream shares a
+    // queue with a communication stream, so a marker recorded there waits behind the
+    // collectives of earlier exchanges, and every lane with it (one-rank exchange step
+    // 44.7 -> 74 ms, profiles/r03_exchange_lane_order.txt).
+    if (b == 0 || h->api_calls != g->api_seen) {
+      GS_HIP(hipEventRecord(h->main_ev, h->stream));
+      for (int i = 0; i < kGroupLanes; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], h->main_ev, 0));
+    }
+    g->api_seen = h->api_calls;
     if (b >= (uint64_t)gs::kDeltaSets)
       for (int i = 0; i < kGroupLanes; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], g->staged[d], 0));
   } else if (b >= (uint64_t)gs::kDeltaSets) {

@@ -142,6 +142,7 @@ struct gs_summary {
   // over lane streams so that fold b+1 may start while fold b drains; every other
   // entry point joins the lanes onto `stream` first (join_lanes)
   int pipe_depth = 1;
+  uint64_t api_calls = 0;  // gs_* calls made on the handle (gs_group_fold_device orders its lanes after any)
   int group_lanes = 0;  // own-fold lanes of an exchange group using this summary (0: none)
   static constexpr int kLanes = 4;
   hipStream_t lane[kLanes] = {};
@@ -241,6 +242,7 @@ int wait_stream(gs_summary* h, const uint32_t* vals = nullptr, uint64_t* value =
                 int stride = 0);
 int check_device_flags(gs_summary* h);
 int check_flags_now(gs_summary* h);
+int done_value_read(gs_summary* h, int i, unsigned long long seq, uint64_t* out);  // tagged completion value
 int wait_done(gs_summary* h, unsigned long long seq);  // spin on the completion word (h->stream)  // after a wait: the host-mapped flags only
 int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n, int part = 0,
                        int nparts = 1);

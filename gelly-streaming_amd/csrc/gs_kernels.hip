@@ -132,6 +132,18 @@ __device__ unsigned long long g_blog_cap = 0;
 __device__ unsigned long long g_blog_n = 0;
 #endif
 
+#ifdef GS_SERVER_TRACE
+// Diagnostic build (make -C gelly-streaming_amd variant V=strace VFLAGS=-DGS_SERVER_TRACE;
+// tools/server_trace.py): per window of the resident server, wall-clock stamps (100 MHz)
+// of its phases, in record (seq mod cap):
+//   [0] block 0 sees the window in the mailbox   [1] block 0 has broadcast it
+//   [2] last block to start folding (max)        [3] last block done folding (max)
+//   [4] publishing block enters take_tail        [5] completion word stored
+//   [6] blocks that took part
+__device__ unsigned long long* g_strace = nullptr;
+__device__ unsigned long long g_strace_cap = 0;
+#endif
+
 // Tail of a fused window take (config 5's per-window fold + delta export + completion
 // in ONE launch instead of fold, stage and completion kernels, each a kernel boundary of
 // ~3 us). Each block reserves its rows in the output with one atomic and writes them
@@ -143,7 +155,8 @@ __device__ unsigned long long g_blog_n = 0;
 // and only the rows and the count are read before that (by the host or other streams).
 // A signed summary's count word carries the verdict (| kFailBit once it failed): the
 // take's consumer replays the records AND the verdict (Candidates.merge :79-81).
-__device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, const int64_t* lrec, uint32_t lcnt,
+// Returns true in the one thread that published the window (the last block's thread 0).
+__device__ __forceinline__ bool take_tail(const Table& t, const FoldArgs& a, const int64_t* lrec, uint32_t lcnt,
                                           bool signed_kind, uint32_t blk, uint32_t nblocks) {
   __shared__ unsigned long long base_sh;
   __shared__ uint32_t last_sh;
@@ -151,6 +164,13 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
   // a one-block window owns the whole output: no reservation and no ticket (two
   // dependent atomics of a small window's latency)
   const bool solo = nblocks == 1;
+  // a one-block window's vertex count is final once its own fold is (its inserts were
+  // counted by returning atomics): the count loads go out now, beside the row stores.
+  // (Not the verdict: the fold raises it with no-return atomics, ordered only by the
+  // drain below.)
+  unsigned long long nv = 0;
+  if (solo && threadIdx.x < 64)
+    nv = __hip_atomic_load(t.ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (threadIdx.x == 0)
     base_sh = (nb && !solo) ? atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE)),
                                         (unsigned long long)nb)
@@ -190,22 +210,22 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
     last_sh = last;
   }
   __syncthreads();
-  if (!last_sh || threadIdx.x >= 64) return;
+  if (!last_sh || threadIdx.x >= 64) return false;
   // one round of loads, issued together (each is a dependent memory hop of the window's
   // latency): the 64 shard counts, the take total (lane 0) and, signed, the verdict
   // (lane 1; every block's verdict updates are memory-side atomics that preceded its
   // ticket, so the flag is read at the memory side too, never from a stale line)
   unsigned long long* take = reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE));
-  unsigned long long nv = __hip_atomic_load(t.ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-  unsigned long long tot = threadIdx.x == 0 ? (solo ? (unsigned long long)lcnt
-                                                    : __hip_atomic_load(take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                                            : 0ull;
+  unsigned long long tot = lcnt;
+  if (!solo) {
+    nv = __hip_atomic_load(t.ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tot = threadIdx.x == 0 ? __hip_atomic_load(take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+  }
   const uint32_t fl = (signed_kind && threadIdx.x == 1) ? atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 0u) : 0u;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) nv += __shfl_xor(nv, o, 64);
   const bool failed = __shfl(fl, 1, 64) != 0u;
-  if (threadIdx.x != 0) return;
+  if (threadIdx.x != 0) return false;
   const unsigned long long total = tot;
   const unsigned long long word = total | (failed ? kFailBit : 0ull);
   __hip_atomic_store(a.take_count, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
@@ -219,13 +239,17 @@ __device__ __forceinline__ void take_tail(const Table& t, const FoldArgs& a, con
     for (int k = 0; k < 16; ++k)
       __hip_atomic_store(t.ctr + ctr_index(CTR_TAKE_SHARD + k), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  __hip_atomic_store(a.done + 1, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(a.done + 2, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  // one system release (L2 write-back) for everything above, its wait explicit
-  // (MI355X_MICROARCH.md compiler hazard), then the completion word
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  // Every store above is write-through (agent scope): draining them puts the count word
+  // and the counter resets in memory before the host can see the window complete,
+  // without an L2 write-back (a release fence costs ~1.7 us even on a clean L2,
+  // MI355X_MICROARCH.md). The completion record then goes out undrained: its values
+  // carry the sequence number as a tag, and the host takes them when the tags match
+  // (gsi::done_value_read), whichever of the three host-memory stores lands first.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(a.done + 1, done_value(a.seq, nv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(a.done + 2, done_value(a.seq, word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return true;
 }
 
 template <bool SIGNED, bool TRACK, bool TAKE>
@@ -377,13 +401,17 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
 // does and the window's last block publishes it (take_tail). The table needs no kernel
 // boundary between windows: every access is already correct on stale lines (the
 // concurrency model in gs_device.hpp), as between the blocks of one launch. Hand-offs:
-//   host -> block 0: mailbox in host-mapped memory, seq stored last (x86 release), read
-//     with system-scope loads;
-//   block 0 -> blocks: the descriptor stored with agent-scope (write-through) stores,
-//     each storing lane's `s_waitcnt vmcnt(0)`, then the seq word; polled and read with
-//     agent-scope loads by one lane per block, handed to its block through LDS behind a
-//     barrier (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms);
-//   window -> host: take_tail's rows, count word and completion word.
+//   host -> block 0: a 64-byte mailbox line in host-mapped memory, {seq, 7 descriptor
+//     words}, each descriptor word tagged with seq mod 2^16 in its top 16 bits
+//     (data-tagged granules, MI355X_MICROARCH.md handoff-1to1): 8 lanes of wave 0
+//     poll the whole line with system-scope loads in ONE load round; a window is taken
+//     when seq is new and every tag matches it (a torn read is polled again);
+//   block 0 -> blocks: the same tagged line written to device memory with agent-scope
+//     (write-through) stores and no wait; the other blocks poll it the same way with
+//     agent-scope loads; the line reaches the block through LDS behind a barrier;
+//   window -> host: take_tail's rows, count word and tagged completion record.
+// (Round 3: descriptor loads after the poll and a drained broadcast cost 2.7 us of
+// every window: tools/server_trace.py.)
 // Exit conditions every wave reaches: a stop request, or no window for idle_ticks
 // (block 0 then tells the others and the host), or -- for the other blocks -- twice
 // that without any word from block 0.
@@ -397,51 +425,50 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
   D.lrec = lrec;
   D.lcnt = &lcnt;
   unsigned long long last = seq0;
+#ifdef GS_SERVER_TRACE
+  __shared__ unsigned long long tseen, tbc;
+#endif
   for (;;) {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {  // wave 0: lanes 0..7 hold the line's words (wave-uniform loop)
+      const uint32_t lane = threadIdx.x;
+      const bool b0 = blockIdx.x == 0;
       const unsigned long long t0 = wall_clock64();
-      unsigned long long s = 0;
-      if (blockIdx.x == 0) {
-        for (;;) {
-          s = __hip_atomic_load(&box->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-          if (s != last) break;
-          if (wall_clock64() - t0 > idle_ticks) {
-            s = kServerStop | last;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
+      const unsigned long long limit = b0 ? idle_ticks : 2 * idle_ticks;
+      unsigned long long* line = b0 ? &box->seq : &bc->seq;
+      unsigned long long v = 0, s = 0;
+      for (;;) {
+        if (lane < 8)
+          v = b0 ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                 : __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s = __shfl(v, 0, 64);
+        if (s != last) {
+          if (s & kServerStop) break;
+          const bool ok = lane == 0 || lane >= 8 || (v >> 48) == (s & 0xFFFFull);
+          if (__ballot(!ok) == 0ull) break;  // every tag is this window's
+          continue;                          // a torn line: poll again at once
         }
-        unsigned long long f[8];
-        f[0] = s;
-        if (!(s & kServerStop)) {
-#pragma unroll
-          for (int k = 1; k < 8; ++k)
-            f[k] = __hip_atomic_load(&box->seq + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#pragma unroll
-          for (int k = 1; k < 8; ++k) __hip_atomic_store(&bc->seq + k, f[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wall_clock64() - t0 > limit) {
+          s = kServerStop | last;
+          break;
         }
-        // every descriptor store (write-through, agent scope) acknowledged before the seq word
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&bc->seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (s & kServerStop) __hip_atomic_store(&box->exited, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) w[k] = f[k];
-      } else {
-        for (;;) {
-          s = __hip_atomic_load(&bc->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (s != last) break;
-          if (wall_clock64() - t0 > 2 * idle_ticks) {
-            s = kServerStop | last;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-        w[0] = s;
-        if (!(s & kServerStop)) {
-#pragma unroll
-          for (int k = 1; k < 8; ++k) w[k] = __hip_atomic_load(&bc->seq + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        __builtin_amdgcn_s_sleep(2);
       }
+#ifdef GS_SERVER_TRACE
+      if (b0) tseen = wall_clock64();
+#endif
+      if (b0) {
+        // broadcast the tagged line as it was read (no wait: the other blocks check tags)
+        if (!(s & kServerStop)) {
+          if (lane < 8) __hip_atomic_store(&bc->seq + lane, lane == 0 ? s : v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (lane == 0) {
+          __hip_atomic_store(&bc->seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&box->exited, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+#ifdef GS_SERVER_TRACE
+        tbc = wall_clock64();
+#endif
+      }
+      if (lane < 8) w[lane] = lane == 0 ? s : (v & kServerTagMask);
     }
     __syncthreads();
     const unsigned long long s = w[0];
@@ -470,9 +497,30 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
                                         __hip_atomic_load(&t.ctr[ctr_index(CTR_FAIL)], __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT)) != 0;
       __syncthreads();
+#ifdef GS_SERVER_TRACE
+      const unsigned long long tgo = wall_clock64();
+#endif
       fold_block<SIGNED, true, true>(t, D, a, blockIdx.x, failed, 0ull, nullptr);
       __syncthreads();
+#ifdef GS_SERVER_TRACE
+      const unsigned long long tfold = wall_clock64();
+      unsigned long long* tr = g_strace ? g_strace + (size_t)(s & (g_strace_cap - 1)) * 8 : nullptr;
+      if (tr && threadIdx.x == 0) {
+        atomicMax(tr + 2, tgo);
+        atomicMax(tr + 3, tfold);
+        if (blockIdx.x == 0) {
+          tr[0] = tseen;
+          tr[1] = tbc;
+          tr[6] = active;
+        }
+      }
+      if (take_tail(t, a, lrec, lcnt, SIGNED, blockIdx.x, active) && tr) {
+        tr[4] = tfold;
+        tr[5] = wall_clock64();
+      }
+#else
       take_tail(t, a, lrec, lcnt, SIGNED, blockIdx.x, active);
+#endif
     }
     __syncthreads();  // LDS (lrec, lcnt, w) is reused by the next window
   }
@@ -744,7 +792,9 @@ __global__ __launch_bounds__(64) void k_signal(unsigned long long* out, unsigned
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   if (threadIdx.x != 0) return;
-  if (vals) __hip_atomic_store(out + 1, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // (a system release: the host may read what earlier work of the stream wrote to host
+  // memory once it sees the word; the value is tagged as take_tail's)
+  if (vals) __hip_atomic_store(out + 1, done_value(seq, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(out, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -797,6 +847,17 @@ extern "C" unsigned long long gs_debug_blocklog_count() {
   (void)hipDeviceSynchronize();
   (void)hipMemcpyFromSymbol(&n, HIP_SYMBOL(gs::g_blog_n), sizeof n);
   return n;
+}
+namespace gs {
+#endif
+#ifdef GS_SERVER_TRACE
+}  // namespace gs
+extern "C" int gs_debug_server_trace(void* buf, unsigned long long cap) {  // diagnostic build only (cap: power of 2)
+  unsigned long long* p = static_cast<unsigned long long*>(buf);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(gs::g_strace), &p, sizeof p) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(gs::g_strace_cap), &cap, sizeof cap) != hipSuccess)
+    return -2;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -2;
 }
 namespace gs {
 #endif

@@ -38,13 +38,27 @@ struct FoldLaunch {
 constexpr uint32_t kServerBlocks = 256;                       // one per CU: a 2^16-edge window
 constexpr uint64_t kServerMaxEdges = (uint64_t)kServerBlocks * kFoldBS;
 constexpr unsigned long long kServerStop = 1ull << 63;        // mailbox seq bit: leave
-struct ServerBox {                 // host-mapped; written by the host, read by block 0
+// Mailbox / broadcast descriptor words and completion records carry a 16-bit tag (the
+// sequence number mod 2^16) in bits 48..63 over a 48-bit value (data-tagged granules:
+// a reader takes the line when every tag matches, with no fence on the writer's side).
+constexpr unsigned long long kServerTagMask = (1ull << 48) - 1;
+__host__ __device__ constexpr unsigned long long tag_word(unsigned long long seq, unsigned long long v) {
+  return (seq & 0xFFFFull) << 48 | (v & kServerTagMask);
+}
+// Completion record values: a count word's failed-verdict bit (bit 62) travels as bit 47.
+__host__ __device__ constexpr unsigned long long done_value(unsigned long long seq, unsigned long long v) {
+  return (seq & 0xFFFFull) << 48 | ((v >> 62) & 1ull) << 47 | (v & ((1ull << 47) - 1));
+}
+__host__ __device__ constexpr unsigned long long done_decode(unsigned long long w) {
+  return (w & ((1ull << 47) - 1)) | ((w >> 47) & 1ull) << 62;
+}
+struct alignas(64) ServerBox {      // host-mapped; written by the host, read by block 0 (one 64-B line + exited)
   unsigned long long seq;          // window number (stored last, release) | kServerStop
-  unsigned long long src, dst, n, rec, cap, cnt, done_seq;
+  unsigned long long src, dst, n, rec, cap, cnt, done_seq;  // each gs::tag_word(seq, value)
   unsigned long long exited;       // block 0 stores 1 when the server leaves (stop or idle)
   unsigned long long pad[7];
 };
-struct ServerBcast {               // device memory: block 0 -> the other blocks
+struct alignas(64) ServerBcast {    // device memory: block 0 -> the other blocks (the tagged line)
   unsigned long long seq, src, dst, n, rec, cap, cnt, done_seq;
 };
 void launch_window_server(bool sign, const Table& t, const Delta& D, ServerBox* box, ServerBcast* bc,

@@ -46,7 +46,11 @@ int gs_group_create(gs_group_t* g, gs_handle h, const void* id, int nranks, int 
  * stride 1; n <= batch_edges), stage the delta and all-gather its count, then
  * move and fold the PREVIOUS micro-batch's records (whose counts landed while this
  * fold was queued). Asynchronous. Collective: every rank calls it the same number
- * of times (n may differ, including 0). */
+ * of times (n may differ, including 0). Ordering: the own folds run after the work
+ * queued on the handle's stream at the first call and after any gs_* call on the
+ * handle since the previous group call (a reset, gs_wait_event, gs_wait_stream, a
+ * sync, ...). A caller that queues its own kernels on gs_get_stream(h) between group
+ * calls (edges written there) marks them with gs_wait_stream(h, that stream). */
 int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n);
 
 /* Consecutive gs_group_fold_device calls over src[0..n) in batch-edge micro-batches,

@@ -99,6 +99,36 @@ def test_group_lanes_follow_handle_stream_every_call(gs, oracle_mod, monkeypatch
     assert np.array_equal(v, ov) and np.array_equal(lab, olab)
 
 
+def test_group_lanes_follow_marked_handle_stream(gs, oracle_mod, monkeypatch):
+    """gs_group.h ordering contract: a caller that queues its own kernels on the
+    handle's stream (a cached gs_get_stream) between group calls, with no other call on
+    the handle, marks them with gs_wait_stream(h, that stream); the own folds then run
+    behind them. Every batch is generated into its own buffers behind a GPU sleep."""
+    import torch
+    monkeypatch.setenv("GS_GROUP_SELF_APPLY", "1")
+    n, B, scale = 1 << 16, 1 << 12, 14
+    with gs.Summary("cc", capacity_hint=1 << scale) as s:
+        g = gs.Group(s, gs.group_unique_id(), 1, 0, B)
+        st = s.stream
+        ext = torch.cuda.ExternalStream(st)
+        bufs = []
+        for o in range(0, n, B):
+            bs = torch.empty(B, dtype=torch.int64, device="cuda")
+            bd = torch.empty(B, dtype=torch.int64, device="cuda")
+            bufs.append((bs, bd))
+            with torch.cuda.stream(ext):
+                torch.cuda._sleep(100000)
+            gs.gen_rmat(bs, bd, o, B, scale, 0x5EED0026, True, stream=st)
+            s.wait_stream(st)  # the mark: the group's lanes start behind the generator
+            g.fold_device(bs, bd, B)
+        g.finish()
+        v, lab = s.labels()
+        g.close()
+    src, dst = _rmat(gs, n, scale)
+    ov, olab = oracle_mod.cc_labels(src.cpu().numpy(), dst.cpu().numpy())
+    assert np.array_equal(v, ov) and np.array_equal(lab, olab)
+
+
 def test_reset_config_restores_a_fresh_handle(gs, oracle_mod):
     """a pooled handle that had change tracking (and so delta tracking) on,
     released with gs_reset_config, folds more than 2^22 edges between takes like a
