@@ -489,10 +489,15 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     hipStream_t st = side ? h->side : h->stream;
     if (side) h->side_dirty = true;
     if (pipe) {  // the lane waits for the caller's work on the handle stream, not for the other lane
-      GS_HIP(hipEventRecord(h->main_ev, h->stream));
       st = h->lane[h->lane_next];
       h->lane_next = (h->lane_next + 1) % h->pipe_depth;
-      GS_HIP(hipStreamWaitEvent(st, h->main_ev, 0));
+      // An idle handle stream has nothing to order behind: no marker. (With 4 hardware
+      // queues a lane can share one with the handle stream, and a marker recorded there
+      // waits behind that lane's fold: every fold would then wait for the previous one.)
+      if (hipStreamQuery(h->stream) != hipSuccess) {
+        GS_HIP(hipEventRecord(h->main_ev, h->stream));
+        GS_HIP(hipStreamWaitEvent(st, h->main_ev, 0));
+      }
       h->lanes_dirty = true;
     } else if (on_lane) {  // the caller ordered the lane (a group's own fold)
       st = h->lane[fs.lane];

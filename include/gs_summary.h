@@ -134,7 +134,12 @@ int gs_fold_device_after(gs_handle h, const int64_t* src, const int64_t* dst, co
  * the handle (reads, exports, combine, serialize, sync, gs_get_stream) first orders
  * the handle's stream behind all pending folds. Device buffers passed to a
  * pipelined fold must stay valid until that next call. Applies to plain folds
- * (no delta or change tracking, profiling off); depth 1 (default) = in order. */
+ * (no delta or change tracking, profiling off); depth 1 (default) = in order.
+ * Each lane is a HIP stream, and streams beyond GPU_MAX_HW_QUEUES share hardware
+ * queues (run in submission order): depth 2 fits HIP's default of 4 queues beside the
+ * handle's and the process's null stream in any creation order; depth 3 gains ~1 %
+ * when its lanes land on distinct queues and loses ~15 % when two share one
+ * (DESIGN.md section 7). */
 int gs_set_pipelining(gs_handle h, int depth);
 
 /* Merge summary `src` into `dst` (either may be on any device; `src` is unchanged).

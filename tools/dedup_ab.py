@@ -22,9 +22,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import gsamd as gs  # noqa: E402
 
 
-def run(src, dst, B, hint, dedup, reps):
+def run(src, dst, B, hint, dedup, reps, depth=3):
     s = gs.Summary("cc", capacity_hint=hint)
-    s.set_pipelining(3)
+    s.set_pipelining(depth)
     s.set_batch_dedup(dedup)
     best = 1e9
     E = src.numel()
@@ -43,6 +43,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--only", default="")
+    ap.add_argument("--pipeline", type=int, default=3)
+    ap.add_argument("--off-only", action="store_true", help="time the plain fold only")
     a = ap.parse_args()
     cases = []
     for name, scale, n, B, rep in (("rmat26", 26, 1 << 30, 1 << 20, 1), ("rmat20", 20, 1 << 24, 1 << 20, 1),
@@ -59,8 +61,12 @@ def main():
             dst = dst.repeat_interleave(rep)
         torch.cuda.synchronize()
         hint = 1 << scale
-        s0, t0 = run(src, dst, B, hint, False, a.reps)
-        s1, t1 = run(src, dst, B, hint, True, a.reps)
+        s0, t0 = run(src, dst, B, hint, False, a.reps, a.pipeline)
+        if a.off_only:
+            print("%-9s pipeline %d: plain %.3f ms" % (name, a.pipeline, t0 * 1e3), flush=True)
+            s0.close()
+            continue
+        s1, t1 = run(src, dst, B, hint, True, a.reps, a.pipeline)
         nv = s0.num_vertices()
         v = torch.empty(nv + 1, dtype=torch.int64, device="cuda")
         lab = torch.empty(nv + 1, dtype=torch.int64, device="cuda")
