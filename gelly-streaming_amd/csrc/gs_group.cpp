@@ -6,11 +6,12 @@
 //   exchange b:  own fold b (tracked) -> stage b: records -> send[b%2], count word
 //                -> count all-gather (communicator C, stream xc) -> k_headers: the
 //                   gathered counts in host-mapped memory
-//   then, still inside the call for exchange b, the DATA of exchange b-1:
-//                host reads b-1's counts (already landed: they were gathered while
-//                fold b ran) -> data all-gather of exactly max-count rows per rank
-//                (communicator D, stream xd) -> fold of the other ranks' live rows
-//                on the apply (side) stream, overlapping this rank's next own fold.
+//   then, still inside the call for exchange b, after fold b is queued, the DATA of
+//                exchange b-1 (data lag 1, the default; GS_GROUP_DATA_LAG up to 3):
+//                host reads b-1's counts (they land when fold b-1 is done, while the
+//                GPU works on fold b) -> data all-gather of exactly max-count rows per
+//                rank (communicator D, stream xd) -> fold of the other ranks' live
+//                rows on the apply (side) stream, beside this rank's own fold b.
 //
 // Only live rows move: the collective size is the largest record count of THIS
 // exchange, known before the data collective is issued, so nothing is queued,
@@ -313,6 +314,7 @@ struct gs_group {
   uint64_t own_edges = 0;  // own edges folded since create / finish (the ramp's position)
   uint64_t ramp_edges = 1ull << 22, ramp_batch = 1ull << 20;  // gs_group_set_ramp
   uint64_t done = 0;    // exchanges whose data half has been issued
+  int data_lag = 1;     // exchanges between an exchange's own fold and its data half (GS_GROUP_DATA_LAG: 1..kLag)
   uint64_t api_seen = 0;  // h->api_calls at the previous fold call (lane ordering)
   // statistics
   uint64_t exchanges = 0, rows_received = 0, live_received = 0;
@@ -450,6 +452,7 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   if (const char* m = getenv("GS_GROUP_HOSTPROF")) g->hostprof = atoi(m) != 0;
   if (const char* m = getenv("GS_GROUP_LANES")) g->no_lanes = atoi(m) == 0;
   if (const char* m = getenv("GS_GROUP_SIDE")) g->no_side = atoi(m) == 0;
+  if (const char* m = getenv("GS_GROUP_DATA_LAG")) g->data_lag = std::min(kLag, std::max(1, atoi(m)));
   auto bail = [&](int code) {
     gs_group_destroy(g);
     return code;
@@ -512,9 +515,10 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   const int d = (int)(b % gs::kDeltaSets), k = (int)(b % kLag);  // delta set, buffer set
   g->hp_calls++;
   g->own_edges += n;
-  // the data half of exchange b - kLag (its counts landed long ago): issued first, so
-  // buffer set k is released (events recorded) before this exchange reuses it
-  if (b >= (uint64_t)kLag)
+  // data lag kLag: the data half of exchange b - kLag (its counts landed long ago),
+  // issued first, so buffer set k is released (events recorded) before this exchange
+  // reuses it. A shorter lag issues it at the end of the call (below).
+  if (g->data_lag == kLag && b >= (uint64_t)kLag)
     if (int rc = finish_data(g, b - kLag)) return rc;
   HostTimer ht(g->hostprof ? &g->hp[0] : nullptr);
   // The own fold records into delta set d. The summary stream only waits for the
@@ -585,6 +589,14 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   ht.lap(nullptr);
   g->b++;
   g->exchanges++;
+  // data lag L < kLag: the data half of exchange b - L, after this exchange's own folds
+  // are queued -- the host waits for that exchange's counts (its folds done) while the
+  // GPU already has this exchange's folds, and its remote rows are folded beside them:
+  // every rank learns the others' hooks kLag - L exchanges sooner, so fewer of its own
+  // hooks duplicate theirs. (The stage above reused buffer set k
+  // after the data half of exchange b - kLag, issued in call b - kLag + L < b.)
+  if (g->data_lag < kLag && b >= (uint64_t)g->data_lag)
+    if (int rc = finish_data(g, b - g->data_lag)) return rc;
   return GS_OK;
 }
 

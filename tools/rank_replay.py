@@ -81,6 +81,7 @@ def main():
             summ[r].sync()
             k = int(cnt.item())
             recs[r][b] = scratch[:k].clone()
+        torch.cuda.current_stream().synchronize()  # the clones (torch's stream) before other summaries fold them
         e = b - a.lag
         if e >= 0:
             for r in range(N):
@@ -143,7 +144,8 @@ def main():
             o, m = bounds[b]
             if "own" in parts:
                 fold_own(rep0, 0, o, m)
-                rep0.take_delta_records(scratch, cap, cnt)
+                if "untracked" not in parts:
+                    rep0.take_delta_records(scratch, cap, cnt)
             e = b - a.lag
             if e >= 0 and "remote" in parts:
                 for x in remote[e]:
@@ -159,6 +161,11 @@ def main():
     for parts in (("own",), ("own", "remote")):
         res[parts] = min(run_rank(parts) for _ in range(a.reps))
     t_own, t_all = res[("own",)], res[("own", "remote")]
+    # the same own folds untracked and with no takes, serialised (what tracking costs)
+    rep0.set_delta_tracking(False)
+    t_plain = min(run_rank(("own", "untracked")) for _ in range(a.reps))
+    rep0.set_delta_tracking(True)
+    print("rank 0 alone: own folds untracked, no takes, serialised %.2f ms" % (t_plain * 1e3), flush=True)
     print("rank 0 alone: own tracked folds + takes %.2f ms; + %d remote rows (%.2f per own edge) %.2f ms" % (
         t_own * 1e3, rows, rows / per, t_all * 1e3), flush=True)
     print("collective bytes per rank per pass: sends %.1f MB, receives %.1f MB (16-B rows)" % (
