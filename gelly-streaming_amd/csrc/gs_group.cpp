@@ -7,11 +7,11 @@
 //                -> count all-gather (communicator C, stream xc) -> k_headers: the
 //                   gathered counts in host-mapped memory
 //   then, still inside the call for exchange b, after fold b is queued, the DATA of
-//                exchange b-1 (data lag 1, the default; GS_GROUP_DATA_LAG up to 3):
-//                host reads b-1's counts (they land when fold b-1 is done, while the
-//                GPU works on fold b) -> data all-gather of exactly max-count rows per
-//                rank (communicator D, stream xd) -> fold of the other ranks' live
-//                rows on the apply (side) stream, beside this rank's own fold b.
+//                exchange b-2 (data lag 2, the default; GS_GROUP_DATA_LAG 1..3):
+//                host reads b-2's counts (landed while fold b-1 ran) -> data all-gather
+//                of exactly max-count rows per rank (communicator D, stream xd) -> fold
+//                of the other ranks' live rows on the apply (side) stream, beside this
+//                rank's own folds.
 //
 // Only live rows move: the collective size is the largest record count of THIS
 // exchange, known before the data collective is issued, so nothing is queued,
@@ -314,7 +314,7 @@ struct gs_group {
   uint64_t own_edges = 0;  // own edges folded since create / finish (the ramp's position)
   uint64_t ramp_edges = 1ull << 22, ramp_batch = 1ull << 20;  // gs_group_set_ramp
   uint64_t done = 0;    // exchanges whose data half has been issued
-  int data_lag = 1;     // exchanges between an exchange's own fold and its data half (GS_GROUP_DATA_LAG: 1..kLag)
+  int data_lag = 2;     // exchanges between an exchange's own fold and its data half (GS_GROUP_DATA_LAG: 1..kLag)
   uint64_t api_seen = 0;  // h->api_calls at the previous fold call (lane ordering)
   // statistics
   uint64_t exchanges = 0, rows_received = 0, live_received = 0;
