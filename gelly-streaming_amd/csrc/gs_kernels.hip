@@ -140,6 +140,7 @@ __device__ unsigned long long g_blog_n = 0;
 //   [2] last block to start folding (max)        [3] last block done folding (max)
 //   [4] publishing block enters take_tail        [5] completion word stored
 //   [6] blocks that took part
+// followed by 64 counters: a histogram of every block's fold time in 0.5-us buckets.
 __device__ unsigned long long* g_strace = nullptr;
 __device__ unsigned long long g_strace_cap = 0;
 #endif
@@ -508,6 +509,9 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
       if (tr && threadIdx.x == 0) {
         atomicMax(tr + 2, tgo);
         atomicMax(tr + 3, tfold);
+        // histogram of per-block fold times (0.5 us buckets) after the cap records
+        const unsigned long long bkt = min((tfold - tgo) / 50ull, 63ull);
+        atomicAdd(g_strace + g_strace_cap * 8 + bkt, 1ull);
         if (blockIdx.x == 0) {
           tr[0] = tseen;
           tr[1] = tbc;

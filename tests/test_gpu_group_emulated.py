@@ -110,6 +110,50 @@ def test_bench_exchange_shape_emulated_ranks(gs, oracle_mod, monkeypatch, world,
         assert st["exchanges"] >= per // B
 
 
+@pytest.mark.parametrize("lag", [1, 2, 3])
+@pytest.mark.parametrize("kind", ["cc", "signed"])
+def test_data_lag_emulated_ranks(gs, oracle_mod, monkeypatch, lag, kind):
+    """GS_GROUP_DATA_LAG: the data half of exchange b - L is issued
+    after own fold b is queued (L = 1, 2; the default is 2) or, at L = 3, before it.
+    Every schedule leaves every replica equal to the oracle (CC labels; signed colouring
+    and verdict, with a mid-shard odd cycle in the signed case), with small batches so
+    that many exchanges are in flight."""
+    import torch
+    monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
+    monkeypatch.setenv("GS_GROUP_DATA_LAG", str(lag))
+    world, B = 4, 1 << 11
+    n = 1 << 17
+    src = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int64, device="cuda")
+    if kind == "cc":
+        gs.gen_rmat(src, dst, 0, n, 14, 0x5EED0026, True)
+    else:
+        gs.gen_bip(src, dst, 0, n, 13, 0x5EED0B1B, inject=((5 << 13) + 99,))
+    torch.cuda.synchronize()
+    uid = gs.group_unique_id()
+    per = n // world
+
+    def rank(r):
+        with gs.Summary(kind, capacity_hint=1 << 10) as s:  # small hint: growth during the exchange
+            g = gs.Group(s, uid, world, r, B)
+            g.fold_batches(src[r * per:], dst[r * per:], per, B)
+            g.finish()
+            res = s.labels() if kind == "cc" else s.colouring()
+            g.close()
+        return res
+
+    res = _run_ranks(world, rank)
+    if kind == "cc":
+        ov, olab = oracle_mod.cc_labels(src.cpu().numpy(), dst.cpu().numpy())
+        for r, (v, lab) in enumerate(res):
+            assert np.array_equal(v, ov) and np.array_equal(lab, olab), "rank %d replica" % r
+    else:
+        t = oracle_mod.bip_truth(src.cpu().numpy(), dst.cpu().numpy())
+        assert not t[0]
+        for r, (ok, *_rest) in enumerate(res):
+            assert ok == t[0], "rank %d verdict" % r
+
+
 @pytest.mark.parametrize("inject", [(), (1 << 15,), (5 << 12,), (2 << 15) + 777])
 def test_signed_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, inject):
     """inject (1 << 15) is the first edge of rank 1's shard (its endpoints are new

@@ -44,7 +44,7 @@ def main():
     rec = torch.empty(cap * 3, dtype=torch.int64, device="cuda")
     cnt = torch.empty(1, dtype=torch.int64, device="cuda")
     TC = 1 << 13
-    tr = torch.zeros(TC * 8, dtype=torch.int64, device="cuda")
+    tr = torch.zeros(TC * 8 + 64, dtype=torch.int64, device="cuda")
     s.sync()
     if L.gs_debug_server_trace(tr.data_ptr(), TC):
         raise SystemExit("gs_debug_server_trace failed")
@@ -69,7 +69,8 @@ def main():
                 if rc:
                     raise gs.GSError(rc, L.gs_last_error().decode())
             s.sync()  # stops the server: every stamp is in memory
-        t = tr.view(TC, 8).cpu().numpy().astype(np.float64)
+        hist = tr[TC * 8:].cpu().numpy()
+        t = tr[:TC * 8].view(TC, 8).cpu().numpy().astype(np.float64)
         t = t[t[:, 5] > 0]  # windows published in the measured pass
         t = t[np.argsort(t[:, 0])][-n:]
         ph = {
@@ -86,6 +87,11 @@ def main():
               (lw, n, len(t), int(np.median(t[:, 6])), np.percentile(host, 50), np.percentile(host, 99)))
         for kx, v in ph.items():
             print("   %-13s p50 %6.2f  p90 %6.2f us" % (kx, np.percentile(v, 50), np.percentile(v, 90)))
+        # per-block fold times over all blocks of the measured pass
+        c = np.cumsum(hist)
+        q = lambda f: 0.5 * (int(np.searchsorted(c, f * c[-1])) + 0.5)  # noqa: E731
+        print("   per-block fold time (%d blocks): p10 %.2f  p50 %.2f  p90 %.2f  p99 %.2f us" % (
+            int(c[-1]), q(0.1), q(0.5), q(0.9), q(0.99)))
         sys.stdout.flush()
     s.close()
     return 0
