@@ -51,3 +51,29 @@ def test_fold_parity_components(gs):
         ec, ev, _ = _expect(u, v, colour)
         o = np.argsort(ev)
         assert np.array_equal(vv, ev[o]) and np.array_equal(lab, ec[o])
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_fold_host_pinned_and_pageable(gs, oracle_mod, pinned):
+    """gs_fold from host memory: chunks of every size are copied by DMA straight from a
+    pinned (hipHostMalloc'ed) caller buffer; pageable buffers take the staging path above
+    2^18 edges. Both equal the oracle, and the caller may overwrite its buffer as soon as
+    each call returns (the next call's data is written into the same buffer)."""
+    import torch
+    n, call = (3 << 20) + 12345, (1 << 20) + 777  # calls of more than one chunk, ragged tail
+    src = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int64, device="cuda")
+    gs.gen_rmat(src, dst, 0, n, 20, 0x5EED0026, True)
+    torch.cuda.synchronize()
+    hs_all, hd_all = src.cpu().numpy(), dst.cpu().numpy()
+    bs = torch.empty(call, dtype=torch.int64, pin_memory=pinned)
+    bd = torch.empty(call, dtype=torch.int64, pin_memory=pinned)
+    with gs.Summary("cc", capacity_hint=1 << 16) as s:  # small hint: growth mid-stream
+        for o in range(0, n, call):
+            m = min(call, n - o)
+            bs[:m] = torch.from_numpy(hs_all[o:o + m])  # reuse of the caller's buffer
+            bd[:m] = torch.from_numpy(hd_all[o:o + m])
+            s.fold(bs.numpy()[:m], bd.numpy()[:m])
+        v, lab = s.labels()
+    ov, olab = oracle_mod.cc_labels(hs_all, hd_all)
+    assert np.array_equal(v, ov) and np.array_equal(lab, olab)
