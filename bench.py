@@ -404,7 +404,7 @@ def bench_er_latency(args):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     logn, E, B, seed = 22, 1 << 26, 1 << 16, 0x5EED00E5
-    summ = gs.Summary("cc", device=0, capacity_hint=1 << logn)
+    summ = gs.Summary("cc", device=0, capacity_hint=1 << (args.capacity_log2 or logn))
     src = torch.empty(E, dtype=torch.int64, device=dev)
     dst = torch.empty(E, dtype=torch.int64, device=dev)
     gs.gen_er(src, dst, 0, E, logn, seed, True, stream=summ.stream)
@@ -477,7 +477,8 @@ def bench_er_latency(args):
             "warmup": args.warmup, "ms_per_step": sel["total_ms"], "higher_is_better": False,
             "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
             "config": {"workload": "er-latency-config5", "n": 1 << logn, "edges": E, "micro_batch": B,
-                       "windows": E // B, "mode": args.er_mode, "p50_us": sel["p50_us"], "p99_us": sel["p99_us"],
+                       "windows": E // B, "capacity_hint": 1 << (args.capacity_log2 or logn),
+                       "mode": args.er_mode, "p50_us": sel["p50_us"], "p99_us": sel["p99_us"],
                        "max_us": sel["max_us"], "edges_per_s": sel["edges_per_s"],
                        "delta_records": sel["delta_records"], "modes": res,
                        "modes_agree": agree, "first_%d_windows_oracle_exact" % nchk: prefix_ok,
@@ -519,7 +520,7 @@ def bench_ingest(args):
     ok = n == E and bad == -1 and bool(torch.equal(ps, src)) and bool(torch.equal(pd, dst))
     nbytes = int(text.numel())
     alg = nbytes + 16 * E  # text read once + int64 pair written per edge
-    with gs.Summary("cc", device=0, capacity_hint=1 << 26) as summ:
+    with gs.Summary("cc", device=0, capacity_hint=1 << 24) as summ:
         th = bytes(text_h)
         t1 = time.perf_counter()
         nf = summ.fold_text(th)
@@ -644,7 +645,7 @@ def main():
     start = rank * per
     nbatch = (per + B - 1) // B
 
-    xlog = args.scale
+    xlog = args.scale - 1  # capacity hint: RMAT's distinct endpoints are about half the id space (32.8 M of 2^26)
     summ = gs.Summary("cc", device=local, capacity_hint=1 << (args.capacity_log2 or xlog))
     st = summ.stream
     src = torch.empty(per, dtype=torch.int64, device=dev)

@@ -660,7 +660,7 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   gs_summary* h = new gs_summary();
   h->device = device;
   h->kind = kind;
-  uint64_t cap = next_pow2(std::max<uint64_t>(2 * std::max<uint64_t>(capacity_hint, 1), 1024));
+  uint64_t cap = next_pow2(std::max<uint64_t>(kSlotsPerHintedVertex * std::max<uint64_t>(capacity_hint, 1), 1024));
   if (cap > kMaxCap) cap = kMaxCap;
   auto bail = [&](int code) {
     gs_destroy(h);

@@ -17,7 +17,7 @@
 // Concurrency model (MI355X: per-CU L1 and per-XCD L2 are not coherent inside a
 // launch). Correctness never depends on a plain load being fresh:
 //   * a key changes once, EMPTY -> k, by 64-bit CAS; a stale EMPTY read is settled by
-//     a fresh (agent-scope) re-read before any CAS, and by the CAS itself;
+//     the CAS itself (it returns the key that won the slot);
 //   * links only move "up": every parent pointer points to a strictly smaller key,
 //     so any historical link is still an ancestor and finds terminate;
 //   * only roots are hooked (32-bit CAS expecting `self<<1`); a failed CAS returns
@@ -155,16 +155,10 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
       link = l;
       return h;
     }
-    if (k == kEmpty) {
-      // test-and-test-and-set: an EMPTY read may be a stale line of a hub's slot that
-      // another XCD has filled; a fresh load settles it without queueing a CAS on
-      // that address (all of a hub's occurrences in a batch would otherwise CAS it)
-      k = (int64_t)__hip_atomic_load((unsigned long long*)&t.tab[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (k == key) {
-        link = load_link_fresh(t.tab + h);
-        return h;
-      }
-    }
+    // An EMPTY read may be a stale line of a slot another XCD has filled: the CAS settles
+    // it (it returns the winner's key). Round 3 dropped the agent-scope re-read that
+    // preceded it (test-and-test-and-set): one round trip less per insert (config 5 p99
+    // 27 -> 25 us), RMAT-26 and config 4 unchanged (profiles/r03_insert_ab.txt).
     if (k == kEmpty) {
       const unsigned long long old =
           atomicCAS((unsigned long long*)&t.tab[h].key, (unsigned long long)kEmpty, (unsigned long long)key);
@@ -213,21 +207,35 @@ __device__ __forceinline__ uint32_t lookup_find(const Table& t, int64_t key, uin
 
 // Register fresh inserts: the shard's new-vertex count (capacity tracking) doubles
 // as the append position of the vertex list; change tracking needs nothing more
-// (lookup_resolve marked the slots).
-__device__ __forceinline__ void note_new_vertices(const Table& t, int shard, bool nu, uint32_t su, bool nv,
-                                                  uint32_t sv) {
-  const bool second = nv && sv != su;
-  const uint32_t k = (nu ? 1u : 0u) + (second ? 1u : 0u);
-  if (!k) return;
-  const uint32_t pos = atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], k);
-  if (!t.vlist) return;
-  if (pos + k > t.vshard_cap) {
+// (lookup_resolve marked the slots). The fold reserves the positions right after its
+// probes and writes the ids after its finds and hook, so that the returning atomic
+// overlaps the find loads instead of preceding them (config 5 with the CAS-only
+// insert: p50 13.4 -> 12.5 us, p99 27.2 -> 24.8; profiles/r03_insert_ab.txt).
+struct NewVertices {
+  uint32_t k = 0, pos = 0, su = 0, sv = 0;
+  bool nu = false;
+};
+
+__device__ __forceinline__ NewVertices reserve_new_vertices(const Table& t, int shard, bool nu, uint32_t su, bool nv,
+                                                            uint32_t sv) {
+  NewVertices r;
+  r.k = (nu ? 1u : 0u) + ((nv && sv != su) ? 1u : 0u);
+  r.nu = nu;
+  r.su = su;
+  r.sv = sv;
+  if (r.k) r.pos = atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], r.k);
+  return r;
+}
+
+__device__ __forceinline__ void write_new_vertices(const Table& t, int shard, const NewVertices& r) {
+  if (!r.k || !t.vlist) return;
+  if (r.pos + r.k > t.vshard_cap) {
     raise_flag(t, CTR_VOVF, 2);
     return;
   }
-  uint32_t* vl = t.vlist + (size_t)shard * t.vshard_cap + pos;
-  if (nu) *vl++ = su;
-  if (second) *vl = sv;
+  uint32_t* vl = t.vlist + (size_t)shard * t.vshard_cap + r.pos;
+  if (r.nu) *vl++ = r.su;
+  if (r.k == 2u || !r.nu) *vl = r.sv;
 }
 
 // One step of a find with path splitting. (x, lx, kx): current slot, its link and

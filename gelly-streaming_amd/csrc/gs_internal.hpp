@@ -25,6 +25,11 @@ int fail(int code, const std::string& msg);
 constexpr uint32_t kMaxChunk = 1u << 22;     // edges per k_fold launch
 constexpr uint32_t kStageChunk = 1u << 20;   // edges per pinned staging buffer
 constexpr double kMaxLoad = 0.70;            // grow the table past this load factor
+// Slots per hinted vertex at create (load <= 1/4 at the hinted count). Linear-probe
+// clusters set the tail of a small window: config 5 (ER, 2^16-edge windows) p50
+// 20.5 -> 13.3 us going from load 1/2 to 1/4; a 2^28-slot table for RMAT-26's 32.8 M
+// vertices (load 1/8) was 2 % slower than 2^27 (profiles/r03_capacity_ab.txt).
+constexpr uint64_t kSlotsPerHintedVertex = 4;
 constexpr uint64_t kMaxCap = 1ull << 30;     // link holds slot << 1 in 32 bits
 // A table whose load limit is crossed by pipeline slack alone (the capacity bound
 // charges 2 new vertices per in-flight edge) grows once instead of waiting for

@@ -354,11 +354,12 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   uint32_t ru = 0, rv = 0, lu = 0, lv = 0;
   int64_t kru = 0, krv = 0;
   bool act = false;
+  NewVertices nvx;
   if (valid) {
     bool nu, nv;
     const uint32_t su = lookup_resolve(t, ks, hu, k0u, l0u, lu, nu);
     const uint32_t sv = lookup_resolve(t, kd, hv, k0v, l0v, lv, nv);
-    note_new_vertices(t, shard, nu, su, nv, sv);
+    nvx = reserve_new_vertices(t, shard, nu, su, nv, sv);  // ids written after the hook
     if (dbg) atomicAdd(&dbg[1], (nu ? 1u : 0u) + ((nv && sv != su) ? 1u : 0u));
     // Delta: a new vertex with an edge to another vertex is always named by a hook
     // record (as the hooked root or as the new parent: its singleton tree can only
@@ -390,6 +391,7 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   }
   if (__popcll(__ballot(act)) >= 2) combine_hooks(act, ru, kru, rv, krv, need, kCombineRounds);  // wave-uniform
   if (act) hook<SIGNED, TRACK, TAKE>(t, D, shard, ru, ru << 1, kru, rv, rv << 1, krv, need);
+  write_new_vertices(t, shard, nvx);
   if (dbg) {
     if (valid) atomicAdd(&dbg[0], 1u);
     if (act) atomicAdd(&dbg[2], 1u);

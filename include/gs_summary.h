@@ -56,7 +56,8 @@ const char* gs_last_error(void);
 int gs_version(void);
 
 /* Create an empty summary on HIP device `device`. `capacity_hint` = expected
- * number of distinct vertices (the table grows past it automatically).
+ * number of distinct vertices: the table starts with >= 4 slots per hinted vertex
+ * (load <= 1/4, short probe clusters) and grows past it automatically.
  * Replaces the summary's initial value: `new DisjointSet<>()`
  * (ConnectedComponents.java:52-54) / `new Candidates(true)` (BipartitenessCheck.java:50-52). */
 int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint);

@@ -71,14 +71,14 @@ def test_config3_rmat26_full_stream(gs, oracle_mod):
     dst = torch.empty(E, dtype=torch.int64, device="cuda")
     gs.gen_rmat(src, dst, 0, E, scale, 0x5EED0026, True)
     torch.cuda.synchronize()
-    with gs.Summary("cc", capacity_hint=1 << scale) as s:
+    with gs.Summary("cc", capacity_hint=1 << (scale - 1)) as s:
         s.set_pipelining(3)  # as bench.py at one GPU
         for o in range(0, E, B):
             s.fold_device(src[o:], dst[o:], n=B)
         nv = _check_properties(s, src, dst)
         assert nv == 32802821  # the bench's vertices_labelled for this stream (BENCH_r01.json)
     m = 1 << 24  # the prefix the bench's CPU leg folds: bit-exact against the oracle
-    with gs.Summary("cc", capacity_hint=1 << scale) as s:
+    with gs.Summary("cc", capacity_hint=1 << (scale - 1)) as s:
         s.set_pipelining(3)
         for o in range(0, m, B):
             s.fold_device(src[o:], dst[o:], n=B)

@@ -80,7 +80,7 @@ def test_config3_eight_ranks_full_stream(gs, monkeypatch):
     dst = torch.empty(E, dtype=torch.int64, device="cuda")
     gs.gen_rmat(src, dst, 0, E, scale, 0x5EED0026, True)
     torch.cuda.synchronize()
-    with gs.Summary("cc", capacity_hint=1 << scale) as one:  # the single-GPU summary (bench N=1)
+    with gs.Summary("cc", capacity_hint=1 << (scale - 1)) as one:  # the single-GPU summary (bench N=1)
         one.set_pipelining(3)
         for o in range(0, E, 1 << 20):
             one.fold_device(src[o:], dst[o:], n=1 << 20)
@@ -91,7 +91,7 @@ def test_config3_eight_ranks_full_stream(gs, monkeypatch):
         assert one.export_labels_device(v, lab) == nv
     v, lab = v[:nv], lab[:nv]
     uid = gs.group_unique_id()
-    summ = [gs.Summary("cc", capacity_hint=1 << scale) for _ in range(world)]
+    summ = [gs.Summary("cc", capacity_hint=1 << (scale - 1)) for _ in range(world)]
     try:
         def rank(r):
             g = gs.Group(summ[r], uid, world, r, B)

@@ -16,7 +16,7 @@ if os.environ.get("GS_LIB"):
     gs.LIB_PATH = os.path.join(ROOT, os.environ["GS_LIB"])
 B = 1 << 20
 nb = int(os.environ.get("BATCHES", "8"))
-s = gs.Summary("cc", capacity_hint=1 << 26)
+s = gs.Summary("cc", capacity_hint=1 << 25)
 src = torch.empty(nb * B, dtype=torch.int64, device="cuda")
 dst = torch.empty(nb * B, dtype=torch.int64, device="cuda")
 gs.gen_rmat(src, dst, 0, nb * B, 26, 0x5EED0026, True, stream=s.stream)

@@ -32,7 +32,7 @@ def main():
     hs, hd = src.cpu().numpy(), dst.cpu().numpy()                 # pageable
     ps, pd = src.cpu().pin_memory(), dst.cpu().pin_memory()       # pinned
     del src, dst
-    s = gs.Summary("cc", capacity_hint=1 << 26)
+    s = gs.Summary("cc", capacity_hint=1 << 25)
     L = gs.lib()
     for name, xs, xd in (("pageable", hs.ctypes.data, hd.ctypes.data), ("pinned", ps.data_ptr(), pd.data_ptr())):
         best = 1e9

@@ -24,7 +24,7 @@ torch.cuda.set_device(0)
 dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
 B = 1 << a.log_batch
 E = B * a.batches
-s = gs.Summary("cc", capacity_hint=1 << 26)
+s = gs.Summary("cc", capacity_hint=1 << 25)
 src = torch.empty(E, dtype=torch.int64, device=dev)
 dst = torch.empty(E, dtype=torch.int64, device=dev)
 gs.gen_rmat(src, dst, 0, E, 26, 0x5EED0026, True, stream=s.stream)

@@ -11,7 +11,7 @@ import gsamd as gs  # noqa: E402
 
 B = int(os.environ.get("BATCH", str(1 << 20)))
 nb = int(os.environ.get("BATCHES", "256"))
-s = gs.Summary("cc", capacity_hint=1 << 26)
+s = gs.Summary("cc", capacity_hint=1 << 25)
 src = torch.empty(nb * B, dtype=torch.int64, device="cuda")
 dst = torch.empty(nb * B, dtype=torch.int64, device="cuda")
 gs.gen_rmat(src, dst, 0, nb * B, 26, 0x5EED0026, True, stream=s.stream)
