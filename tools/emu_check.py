@@ -40,7 +40,7 @@ def main():
     print("oracle: %d vertices" % ov.size, flush=True)
     per = E // n
     uid = gs.group_unique_id()
-    summ = [gs.Summary("cc", capacity_hint=1 << (a.hint_log2 or a.scale)) for _ in range(n)]
+    summ = [gs.Summary("cc", capacity_hint=1 << (a.hint_log2 or a.scale - 1)) for _ in range(n)]
     if a.serial:
         for s in summ:
             s.set_profiling(True)

@@ -47,7 +47,7 @@ def main():
     torch.cuda.synchronize()
 
     # baseline: one summary, no exchange, pipelined folds (bench.py at N = 1)
-    s = gs.Summary("cc", capacity_hint=1 << a.scale)
+    s = gs.Summary("cc", capacity_hint=1 << (a.scale - 1))
     s.set_pipelining(3)
     best = 1e9
     for _ in range(a.reps + 1):
@@ -64,7 +64,7 @@ def main():
     for n in [int(x) for x in a.ranks.split(",")]:
         per = E // n
         uid = gs.group_unique_id()
-        summ = [gs.Summary("cc", capacity_hint=1 << (a.hint_log2 or a.scale)) for _ in range(n)]
+        summ = [gs.Summary("cc", capacity_hint=1 << (a.hint_log2 or a.scale - 1)) for _ in range(n)]
         bar = threading.Barrier(n)
         times = [[] for _ in range(n)]
         recs = [None] * n

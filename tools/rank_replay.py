@@ -49,7 +49,7 @@ def main():
     dst = torch.empty(E, dtype=torch.int64, device="cuda")
     gs.gen_rmat(src, dst, 0, E, a.scale, 0x5EED0026, True)
     torch.cuda.synchronize()
-    hint = 1 << a.scale
+    hint = 1 << (a.scale - 1)  # expected distinct vertices (4 slots each)
     # exchange boundaries of one rank's shard (the ramp, then the cadence)
     bounds, o = [], 0
     while o < per:
