@@ -357,8 +357,8 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   NewVertices nvx;
   if (valid) {
     bool nu, nv;
-    const uint32_t su = lookup_resolve<!TAKE>(t, ks, hu, k0u, l0u, lu, nu);
-    const uint32_t sv = lookup_resolve<!TAKE>(t, kd, hv, k0v, l0v, lv, nv);
+    const uint32_t su = lookup_resolve(t, ks, hu, k0u, l0u, lu, nu);
+    const uint32_t sv = lookup_resolve(t, kd, hv, k0v, l0v, lv, nv);
     nvx = reserve_new_vertices(t, shard, nu, su, nv, sv);  // ids written after the hook
     if (dbg) atomicAdd(&dbg[1], (nu ? 1u : 0u) + ((nv && sv != su) ? 1u : 0u));
     // Delta: a new vertex with an edge to another vertex is always named by a hook
