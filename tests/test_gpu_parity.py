@@ -149,6 +149,14 @@ def test_empty_and_self_loops(gs, oracle_mod):
         assert v.tolist() == [3, 4] and lab.tolist() == [3, 4]
 
 
+def test_table_starts_at_four_slots_per_hinted_vertex(gs):
+    """gs_create sizes the table at >= 4 slots per hinted vertex (load <= 1/4: short
+    linear-probe clusters, DESIGN.md §3 "Load factor"), never below 1024 slots."""
+    for hint, want in ((1, 1024), (1000, 4096), (1 << 20, 1 << 22)):
+        with gs.Summary("cc", capacity_hint=hint) as ds:
+            assert ds.table_capacity() == want, (hint, ds.table_capacity())
+
+
 def test_table_growth_from_tiny_hint(gs, oracle_mod):
     s, d = oracle_mod.rmat_edges(99, 16, 0, 1 << 17, True)
     with gs.Summary("cc", capacity_hint=1) as ds:
