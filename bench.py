@@ -90,6 +90,32 @@ def _traffic_fields(pm, launches, step_s):
     return int(pm["fabric_bytes_per_launch"]), out
 
 
+# gs_digest of the single-GPU summary after the whole stream, per (scale, edge factor,
+# seed): the constant every N > 1 replica must reproduce (computed by a one-GPU
+# bench.py run of this build; the N = 1 line recomputes and checks it).
+KNOWN_DIGESTS = {}
+
+
+def _as_i64(u):
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+def replica_digest_checks(digest, world, expected, device):
+    """Self-check of an N-rank line, outside the timed region: every
+    replica's gs_digest (order-independent digest of its full (v, label) set) must be the
+    same -- all-reduce MIN and MAX -- and equal to the single-GPU summary's committed
+    digest for this stream. Returns the check fields."""
+    lo = torch.tensor([_as_i64(digest)], dtype=torch.int64, device=device)
+    hi = lo.clone()
+    if world > 1:
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    out = {"replica_label_digests_equal": int(lo.item()) == int(hi.item()), "digest": "%016x" % digest}
+    out["digest_equals_single_gpu"] = None if expected is None else (
+        out["replica_label_digests_equal"] and digest == expected)
+    return out
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -135,6 +161,10 @@ def parse():
     p.add_argument("--launch-check", action="store_true",
                    help="launcher test (CPU, gloo): form the world exactly as the bench does, print one JSON line "
                         "with the world that formed, touch no GPU")
+    p.add_argument("--launch-check-digest", type=lambda x: int(x, 0), default=None,
+                   help="launcher test: run the N-rank digest self-check on this synthetic digest (rank r "
+                        "reports digest + r * --launch-check-digest-skew)")
+    p.add_argument("--launch-check-digest-skew", type=int, default=0)
     return p.parse_args()
 
 
@@ -183,18 +213,25 @@ def launch_check(args):
     """CPU rehearsal of the multi-rank launch (tests/test_bench_launch.py): gloo process
     group, world counted by an all-reduce, one JSON line on rank 0."""
     world, rank, _ = check_world(args)
+    checks = None
     if world > 1:
         dist.init_process_group("gloo")
         t = torch.ones(1)
         dist.all_reduce(t)
         formed = int(t.item())
+        if args.launch_check_digest is not None:
+            d = (args.launch_check_digest + rank * args.launch_check_digest_skew) % (1 << 64)
+            checks = replica_digest_checks(d, world, args.launch_check_digest, torch.device("cpu"))
         dist.destroy_process_group()
     else:
         formed = 1
     if formed != args.gpus:
         raise SystemExit("--gpus %d but %d rank(s) joined" % (args.gpus, formed))
     if rank == 0:
-        print(json.dumps({"launch_check": True, "n_gpus": formed, "workload": args.workload}), flush=True)
+        line = {"launch_check": True, "n_gpus": formed, "workload": args.workload}
+        if checks is not None:
+            line["self_check"] = checks
+        print(json.dumps(line), flush=True)
 
 
 class NativeExchange:
@@ -241,10 +278,22 @@ def bench_bip(args):
     per = E // world
     start = rank * per
     summ = gs.Summary("signed", device=local, capacity_hint=1 << 20)
-    src = torch.empty(per, dtype=torch.int64, device=dev)
-    dst = torch.empty(per, dtype=torch.int64, device=dev)
-    gs.gen_bip(src, dst, start, per, logside, seed, [], stream=summ.stream)
-    summ.sync()
+
+    def stream(inject):
+        """The whole config-4 stream with ids renamed in first-appearance order (SURVEY.md
+        8(d): the reference's exact regime), every rank the same, before the timed region."""
+        fs = torch.empty(E, dtype=torch.int64, device=dev)
+        fd = torch.empty(E, dtype=torch.int64, device=dev)
+        gs.gen_bip(fs, fd, 0, E, logside, seed, inject)
+        torch.cuda.synchronize(dev)
+        gs.relabel_first_appearance(fs, fd, 2 << logside)
+        torch.cuda.synchronize(dev)
+        return fs, fd
+
+    fs, fd = stream([])
+    src, dst = fs[start:start + per].clone(), fd[start:start + per].clone()
+    del fs, fd
+    torch.cuda.synchronize(dev)
     group = None
     if grouped:
         uid = [gs.group_unique_id() if rank == 0 else None]
@@ -314,10 +363,16 @@ def bench_bip(args):
         if world > 1 or args.exchange:
             dist.destroy_process_group()
         return
+    # the clean stream's colouring, every replica against the single-GPU summary's digest
+    dig = replica_digest_checks(summ.digest(), world, KNOWN_DIGESTS.get("bip-config4-clean"), dev)
     # odd-cycle variant (outside the timed region)
     inject = [E // 8, E // 4, E // 2, 3 * E // 4]
-    gs.gen_bip(src, dst, start, per, logside, seed, [i for i in inject if start <= i < start + per],
-               stream=summ.stream)
+    fs, fd = stream(inject)
+    src.copy_(fs[start:start + per])
+    dst.copy_(fd[start:start + per])
+    torch.cuda.synchronize(dev)
+    if rank != 0:
+        del fs, fd
     summ.reset()
     flip = None
     if group is not None:
@@ -343,16 +398,17 @@ def bench_bip(args):
     line = None
     if rank == 0:
         import oracle  # checker and CPU baseline legs only
-        fs = torch.empty(E, dtype=torch.int64, device=dev)
-        fd = torch.empty(E, dtype=torch.int64, device=dev)
-        gs.gen_bip(fs, fd, 0, E, logside, seed, inject, stream=summ.stream)
-        summ.sync()
         first = oracle.bip_first_failure(fs.cpu().numpy(), fd.cpu().numpy())
         # SURVEY.md 8(a) contract (ii): does the reference's Candidates diverge from the
-        # truth on this stream? Its merge is O(E x components): a capped prefix, one window
+        # truth on this stream? Its merge is O(E x components): a capped prefix, one window.
+        # With first-appearance ids it must not, and the GPU's colouring of the same prefix
+        # must equal the reference's (quirk-exact restatement) string exactly.
         cap = 1 << args.bip_prefix_log2
         ps, pd = fs[:cap].cpu().numpy(), fd[:cap].cpu().numpy()
         div = oracle.bip_quirk_divergence(ps, pd)
+        with gs.Summary("signed", device=local, capacity_hint=cap) as pre:
+            pre.fold_device(fs[:cap], fd[:cap], n=cap)
+            gpu_str = oracle.canonical_candidates_string(*pre.colouring())
         c0 = time.perf_counter()
         oracle.cpu_baseline_bip(ps, pd)
         cpu_secs = time.perf_counter() - c0
@@ -367,12 +423,15 @@ def bench_bip(args):
         else:
             cfg.update({"verdict_parity": agree and oks[0] and oks[1] == (first < 0),
                         "parallelism": "edge-shard x%d, per-batch signed delta all-gather (native group)" % world})
+        cfg["clean_stream_digest"] = dig
+        cfg["ids"] = "first-appearance order (SURVEY.md 8(d) config 4: the reference's exact regime)"
         cfg["reference_quirk_check"] = {
-            "prefix_edges": cap, "diverges": div["diverges"],
-            "note": "quirk-exact Candidates restatement (oracle/gs_oracle.cpp) on the first %d edges of the odd-cycle "
-                    "stream in one window vs the truth; the generator's ids are not in first-appearance order, so "
-                    "the reference's colouring differs from the canonical one (Candidates.java:142-192) when "
-                    "diverges is true" % cap}
+            "prefix_edges": cap, "diverges": div["diverges"], "gpu_equals_reference": gpu_str == div["quirk"],
+            "note": "quirk-exact Candidates restatement (oracle/gs_oracle.cpp, Candidates.java:77-192) on the first "
+                    "%d edges of the odd-cycle stream in one window: diverges = its output differs from the truth; "
+                    "gpu_equals_reference = the GPU summary's (ok,{comp={v=(v,sign),...}}) string of the same prefix "
+                    "equals the reference's string exactly" % cap}
+        cfg["verdict_parity"] = cfg["verdict_parity"] and gpu_str == div["quirk"] and not div["diverges"]
         line = {"metric": "edges/sec for streaming bipartiteness (config 4)", "value": round(E * args.steps / el, 1),
                 "unit": "edges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(el * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "strong",
@@ -711,6 +770,15 @@ def main():
     value = total_edges / elapsed
     labelled = nlabels[0]
     checks = {}
+    # every replica's (v, label) set -- not only its size -- against the single-GPU
+    # summary's committed digest
+    stream_key = "rmat%d-ef%d-seed%#x" % (args.scale, args.edge_factor, args.seed)
+    checks.update(replica_digest_checks(summ.digest(), world, KNOWN_DIGESTS.get(stream_key), dev))
+    checks["digest_stream"] = stream_key
+    if isinstance(xch, NativeExchange):  # the world RCCL formed (ncclCommCount of both communicators)
+        cc, dc = xch.g.comm_ranks()
+        checks["rccl_comm_ranks"] = [cc, dc]
+        checks["rccl_world_ok"] = cc == dc == world
     if world > 1:  # vertices labelled by all ranks' slices (outside the timed region)
         c = torch.tensor([labelled], dtype=torch.int64, device=dev)
         dist.all_reduce(c)
@@ -772,6 +840,31 @@ def main():
         if grouped:
             roof["note"] = ("exchange path: fold launches include the other ranks' gathered rows (side stream); "
                             "achieved assumes 2^20 own edges per launch")
+
+    # Per-phase device time of the exchange protocol, one extra untimed
+    # step with timing events around each phase (gs_group_set_phase_timing): the N > 1
+    # line explains its own scaling. Max over ranks.
+    phases = None
+    if isinstance(xch, NativeExchange) and not args.profile_only:
+        xch.g.set_phase_timing(True)
+        t0p = time.perf_counter()
+        one_step()
+        summ.sync()
+        pstep = time.perf_counter() - t0p
+        ps = xch.g.phase_stats()
+        xch.g.set_phase_timing(False)
+        keys = sorted(k for k in ps if k != "exchanges")
+        vals = torch.tensor([ps[k] for k in keys] + [pstep * 1e3], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+        phases = {k: round(float(v), 3) for k, v in zip(keys + ["step_ms"], vals.tolist())}
+        phases["exchanges_per_rank"] = ps["exchanges"]
+        st_ = xch.g.stats()
+        phases["records_sent_rank0"] = st_["records_sent"]
+        phases["rows_received_rank0"] = st_["rows_received"]
+        phases["note"] = ("max over ranks, one untimed step with HIP timing events around every phase; own-fold "
+                          "time is summed over the 3 pipelining lanes (overlapping), host_wait_counts is the host's "
+                          "poll for gathered counts")
 
     # Secondary, PCIe-inclusive figure: the stream's first 2^27 edges
     # folded from PINNED host memory through gs_fold in 2^20-edge calls (H2D copies by
@@ -845,7 +938,7 @@ def main():
                        "combine": "delta exchange (native RCCL group)" if grouped else "none at 1 GPU (same cadence)",
                        "ids": "sparse 64-bit (scrambled)",
                        "capacity_hint": 1 << (args.capacity_log2 or xlog),
-                       "vertices_labelled": int(labelled), "self_check": checks,
+                       "vertices_labelled": int(labelled), "self_check": checks, "exchange_phases": phases,
                        "pcie_inclusive": pcie,
                        "parallelism": ("edge-shard x%d, per-batch delta all-gather (%s)" % (world, args.exchange_impl))
                        if xch is not None else "single GPU"},

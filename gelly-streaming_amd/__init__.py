@@ -57,9 +57,11 @@ EXPORTED_SYMBOLS = (
     "gs_set_change_tracking", "gs_take_changes_device", "gs_take_changes",
     "gs_fold_records_counted_device", "gs_reset_config", "gs_wait_event", "gs_wait_stream", "gs_fold_device_after",
     "gs_fold_parity", "gs_set_window_server", "gs_window_server_stats", "gs_set_batch_dedup",
+    "gs_digest", "gs_group_comm_ranks", "gs_group_set_phase_timing", "gs_group_phase_stats",
 )
 
 FAIL_BIT = 1 << 62  # count words: a failed signed verdict (GS_FAIL_BIT)
+DIGEST_FAILED = (1 << 64) - 1  # gs_digest of a signed summary whose verdict failed (GS_DIGEST_FAILED)
 
 
 class GSError(RuntimeError):
@@ -156,6 +158,10 @@ def lib():
     L.gs_export_labels_part_device.argtypes = [_vp, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _sz,
                                                ctypes.POINTER(_sz)]
     L.gs_combine_exported_device.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.c_int]
+    L.gs_digest.argtypes = [_vp, ctypes.POINTER(_u64)]
+    L.gs_group_comm_ranks.argtypes = [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    L.gs_group_set_phase_timing.argtypes = [_vp, ctypes.c_int]
+    L.gs_group_phase_stats.argtypes = [_vp, ctypes.POINTER(ctypes.c_double)]
     _lib = L
     return L
 
@@ -319,6 +325,13 @@ class Summary:
         cap = v.numel() if hasattr(v, "numel") else len(v)
         _check(lib().gs_export_labels_device(self._h, _ptr(v), _ptr(label), _ptr(parity), cap, ctypes.byref(got)))
         return got.value
+
+    def digest(self):
+        """gs_digest: order-independent 64-bit digest of the (vertex, label, parity) set
+        (DIGEST_FAILED for a failed signed summary). Synchronises."""
+        d = _u64()
+        _check(lib().gs_digest(self._h, ctypes.byref(d)))
+        return d.value
 
     def ok(self):
         o = ctypes.c_int()
@@ -553,6 +566,22 @@ class Group:
         _check(lib().gs_group_stats(self._g, ctypes.byref(e), ctypes.byref(s), ctypes.byref(c)))
         return {"exchanges": e.value, "records_sent": s.value, "rows_received": c.value}
 
+    def comm_ranks(self):
+        """(ranks of the count communicator, ranks of the data communicator): ncclCommCount."""
+        c, d = ctypes.c_int(), ctypes.c_int()
+        _check(lib().gs_group_comm_ranks(self._g, ctypes.byref(c), ctypes.byref(d)))
+        return c.value, d.value
+
+    def set_phase_timing(self, on=True):
+        _check(lib().gs_group_set_phase_timing(self._g, 1 if on else 0))
+
+    def phase_stats(self):
+        """Per-phase device milliseconds since set_phase_timing (gs_group_phase_stats)."""
+        out = (ctypes.c_double * 6)()
+        _check(lib().gs_group_phase_stats(self._g, out))
+        return {"own_fold_lane_ms": out[0], "remote_fold_ms": out[1], "stage_count_collective_ms": out[2],
+                "data_collective_ms": out[3], "host_wait_counts_ms": out[4], "exchanges": int(out[5])}
+
     def close(self):
         if getattr(self, "_g", None):
             lib().gs_group_destroy(self._g)
@@ -599,3 +628,26 @@ def gen_bip(src, dst, start, count, logside, seed, inject=(), stream=None):
                           inj.ctypes.data if len(inj) else None, len(inj))
     if rc:
         raise GSError(rc, "gs_gen_bip failed")
+
+
+def relabel_first_appearance(src, dst, id_bound):
+    """Rename the vertices of a device edge stream (torch int64 tensors, ids in
+    [0, id_bound)) in place to 1, 2, 3, ... in order of first appearance (edge by edge,
+    src before dst): SURVEY.md 8(d) config 4's ids, the reference's exact regime
+    (with such ids and one window, Candidates.merge -- Candidates.java:
+    77-192 -- returns the canonical colouring). A renaming is a graph isomorphism, so
+    verdicts and the window where one flips are unchanged. Stream preparation (bench and
+    tests), outside any timed region; torch ops on the current stream."""
+    import torch
+    n = src.numel()
+    occ = torch.stack([src, dst], 1).reshape(-1)  # occurrence order: s0, d0, s1, d1, ...
+    pos = torch.arange(2 * n, dtype=torch.int64, device=src.device)
+    first = torch.full((id_bound,), 2 * n, dtype=torch.int64, device=src.device)
+    first.scatter_reduce_(0, occ, pos, reduce="amin")
+    del pos
+    flag = torch.zeros(2 * n + 1, dtype=torch.int64, device=src.device)
+    flag[first] = 1  # first occurrence of every vertex (unseen ids mark the sentinel slot 2n)
+    rank = torch.cumsum(flag[:2 * n], 0)  # 1-based rank of each first occurrence
+    new = rank[first[occ]]
+    src.copy_(new[0::2])
+    dst.copy_(new[1::2])

@@ -353,8 +353,8 @@ int server_start(gs_summary* h) {
   gs::ServerBox* b = h->srv_box;
   memset(b, 0, sizeof(gs::ServerBox));
   b->seq = h->srv_seq;
-  b->pad[0] = h->srv_seq;
-  GS_HIP(hipMemcpyAsync(&h->srv_bc->seq, &b->pad[0], 8, hipMemcpyHostToDevice, h->stream));
+  b->bc_init = h->srv_seq;
+  GS_HIP(hipMemcpyAsync(&h->srv_bc->seq, &b->bc_init, 8, hipMemcpyHostToDevice, h->stream));
   // ~250 ms without a window: the launch leaves on its own (wall clock 100 MHz)
   gs::launch_window_server(h->kind == GS_KIND_SIGNED, h->table(), h->delta(), h->srv_box, h->srv_bc, h->done_dev,
                            h->srv_seq, 25000000ull, h->stream);
@@ -891,10 +891,15 @@ int gs_fold_device(gs_handle h, const int64_t* src, const int64_t* dst, const ui
 // stream, on pipelining lanes that wait for an event recorded on the handle stream at
 // each fold, or on a group's own-fold lanes that do the same at each call -- so one
 // wait on the handle stream orders all of them.
+//
+// A running window server folds every posted window at once, whatever is queued on the
+// handle stream: a wait stops it first, so the next window starts a new
+// server launch queued behind the wait.
 int gs_wait_event(gs_handle h, void* event) {
   if (int rc = check(h)) return rc;
   if (!event) return fail(GS_ERR_INVALID, "null event");
   DeviceGuard g(h->device);
+  if (int rc = server_stop(h)) return rc;
   GS_HIP(hipStreamWaitEvent(h->stream, static_cast<hipEvent_t>(event), 0));
   return GS_OK;
 }
@@ -904,6 +909,7 @@ int gs_wait_stream(gs_handle h, void* stream) {
   DeviceGuard g(h->device);
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (st == h->stream) return GS_OK;
+  if (int rc = server_stop(h)) return rc;
   GS_HIP(hipEventRecord(h->ext_ev, st));  // (stream 0 = the device's null stream)
   GS_HIP(hipStreamWaitEvent(h->stream, h->ext_ev, 0));
   return GS_OK;
@@ -984,6 +990,25 @@ int gs_find_labels_device(gs_handle h, const int64_t* v, size_t n, int64_t* labe
   if (!n) return GS_OK;
   gs::launch_find_batch(h->table(), v, n, label, found, nullptr, h->stream);
   GS_HIP(hipGetLastError());
+  return GS_OK;
+}
+
+int gs_digest(gs_handle h, uint64_t* digest) {
+  if (int rc = check(h)) return rc;
+  if (!digest) return fail(GS_ERR_INVALID, "digest is null");
+  DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
+  unsigned long long* d = reinterpret_cast<unsigned long long*>(h->d_scratch);
+  uint32_t failed = 0;
+  GS_HIP(hipMemsetAsync(d, 0, 8, h->stream));
+  gs::launch_digest(h->table(), d, std::min<uint64_t>(h->nv_ub, h->cap + 1), h->stream);
+  GS_HIP(hipGetLastError());
+  unsigned long long out = 0;
+  GS_HIP(hipMemcpyAsync(&out, d, 8, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipMemcpyAsync(&failed, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  if (int rc = check_flags_now(h)) return rc;
+  *digest = (h->kind == GS_KIND_SIGNED && failed) ? GS_DIGEST_FAILED : out;
   return GS_OK;
 }
 
@@ -1262,8 +1287,20 @@ static int server_take(gs_handle h, const int64_t* src, const int64_t* dst, size
       __builtin_ia32_pause();
     }
     if (!left) break;
-    h->srv_running = false;  // it left before this window: join it, start again
-    GS_HIP(hipStreamSynchronize(h->stream));
+    h->srv_running = false;
+    GS_HIP(hipStreamSynchronize(h->stream));  // join the launch that left
+    if (__atomic_load_n(&b->taken, __ATOMIC_ACQUIRE) == seq && __atomic_load_n(h->h_done, __ATOMIC_ACQUIRE) < dseq) {
+      // It left INSIDE this window (a workgroup never became resident within ~2 s): some
+      // of the window's edges are folded and their rows written, the count word is not.
+      // Replaying it would lose those hooks' records, so the window fails; the take
+      // counters are cleared so that the handle's next take starts clean.
+      GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_TAKE), 0,
+                            (size_t)(gs::CTR_COUNT - gs::CTR_TAKE) * gs::kCtrStride * 4, h->stream));
+      GS_HIP(hipStreamSynchronize(h->stream));
+      return fail(GS_ERR_HIP, "window server left inside window " + std::to_string(seq) +
+                                  " (workgroups not co-resident): the summary holds part of it; reset or restore it");
+    }
+    // it left before this window: start again and post it again
     if (attempt >= 3) return fail(GS_ERR_HIP, "window server: left before the window three times");
   }
   h->srv_seq = seq;
@@ -1313,8 +1350,12 @@ int gs_fold_take_device(gs_handle h, const int64_t* src, const int64_t* dst, siz
   DeviceGuard g(h->device);
   auto* cd = reinterpret_cast<unsigned long long*>(count_dev);
   // the resident server takes a window of at most one launch's worth of edges when
-  // nothing else is pending on the handle
-  if (h->srv_on && n > 0 && n <= gs::kServerMaxEdges && h->delta_fill_ub[h->dset] == 0 && !h->changes &&
+  // nothing else is pending on the handle, on a device where all its workgroups can be
+  // resident at once (checked once per handle: a window completes only when every
+  // workgroup runs; otherwise the fused launch below)
+  if (h->srv_on && h->srv_fits < 0)
+    h->srv_fits = gs::window_server_resident_blocks(h->kind == GS_KIND_SIGNED, h->device) >= (int)gs::kServerBlocks;
+  if (h->srv_on && h->srv_fits > 0 && n > 0 && n <= gs::kServerMaxEdges && h->delta_fill_ub[h->dset] == 0 && !h->changes &&
       !h->profiling && !h->dedup && !h->lanes_dirty && !h->side_dirty)
     return server_take(h, src, dst, n, rec, cap, cd, count);
   if (int rc_ = join_lanes(h)) return rc_;

@@ -139,7 +139,9 @@ __device__ __forceinline__ int64_t settle_key(const Table& t, uint32_t s, int64_
 // Insert-or-find of one id. Its first probe (slot h, loaded into k, l) was issued by
 // the caller (callers issue both endpoints' first loads back to back so they
 // overlap). Returns the slot (dense id), its observed link and whether this call
-// inserted it.
+// inserted it. TTAS: re-read an EMPTY-looking slot with an agent-scope load before the
+// key CAS (throughput folds; the window takes CAS at once, below).
+template <bool TTAS = true>
 __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, uint32_t h, int64_t k, uint32_t l,
                                                    uint32_t& link, bool& fresh) {
   fresh = false;
@@ -155,10 +157,19 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
       link = l;
       return h;
     }
-    // An EMPTY read may be a stale line of a slot another XCD has filled: the CAS settles
-    // it (it returns the winner's key). Round 3 dropped the agent-scope re-read that
-    // preceded it (test-and-test-and-set): one round trip less per insert (config 5 p99
-    // 27 -> 25 us), RMAT-26 and config 4 unchanged (profiles/r03_insert_ab.txt).
+    // An EMPTY read may be a stale line of a slot another XCD has filled; the CAS settles
+    // it (it returns the winner's key). Throughput folds first re-read the slot with an
+    // agent-scope load (test-and-test-and-set): all of a hub's occurrences in a young
+    // table's batch would otherwise queue CASes on its slot (RMAT-20: 0.656 vs 0.690
+    // ms/step without). The window takes (TAKE) skip the re-read: one round trip less per
+    // insert (config 5 p50 13.6 -> 12.9 us, p99 27.1 -> 25.5; profiles/r03_insert_ab.txt).
+    if (TTAS && k == kEmpty) {
+      k = (int64_t)__hip_atomic_load((unsigned long long*)&t.tab[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (k == key) {
+        link = load_link_fresh(t.tab + h);
+        return h;
+      }
+    }
     if (k == kEmpty) {
       const unsigned long long old =
           atomicCAS((unsigned long long*)&t.tab[h].key, (unsigned long long)kEmpty, (unsigned long long)key);

@@ -70,6 +70,7 @@ struct RcclApi {
   int (*groupStart)() = nullptr;
   int (*groupEnd)() = nullptr;
   const char* (*getErrorString)(int) = nullptr;
+  int (*commCount)(void*, int*) = nullptr;  // ncclCommCount: ranks of a communicator
   void* initRankSym = nullptr;  // ncclCommInitRank takes ncclUniqueId (128 B) by value: see Id128
 };
 
@@ -93,6 +94,7 @@ int rccl_load() {
   g_rccl.recv = (int (*)(void*, size_t, int, int, void*, hipStream_t))dlsym(l, "ncclRecv");
   g_rccl.groupStart = (int (*)())dlsym(l, "ncclGroupStart");
   g_rccl.groupEnd = (int (*)())dlsym(l, "ncclGroupEnd");
+  g_rccl.commCount = (int (*)(void*, int*))dlsym(l, "ncclCommCount");
   if (!g_rccl.getUniqueId || !g_rccl.initRankSym || !g_rccl.allGather || !g_rccl.commDestroy)
     return fail(GS_ERR_HIP, "RCCL is missing ncclGetUniqueId/ncclCommInitRank/ncclAllGather/ncclCommDestroy");
   g_rccl.lib = l;
@@ -255,6 +257,10 @@ int fake_recv(void* buf, size_t count, int dtype, int peer, void* comm, hipStrea
   s->cv.notify_all();
   return r;
 }
+int fake_count(void* comm, int* n) {
+  *n = ((FakeComm*)comm)->s->n;
+  return 0;
+}
 int fake_noop() { return 0; }
 const char* fake_error(int) { return "in-process comm emulation error"; }
 
@@ -269,6 +275,7 @@ RcclApi make_fake_api() {
   a.groupStart = fake_noop;
   a.groupEnd = fake_noop;
   a.getErrorString = fake_error;
+  a.commCount = fake_count;
   a.initRankSym = (void*)&fake_init;
   return a;
 }
@@ -323,6 +330,20 @@ struct gs_group {
   bool no_side = false;   // GS_GROUP_SIDE=0 (diagnostic): remote folds on the handle stream
   double hp[4] = {};      // own fold, stage + count collective, wait for counts, data collective + apply
   uint64_t hp_calls = 0;
+  // per-phase timing (gs_group_set_phase_timing): HIP timing events around each phase's
+  // device work; [0] own folds (lane time, summed over lanes), [1] remote-row folds,
+  // [2] stage + count collective + headers, [3] data collective. Host wait for gathered
+  // counts is always timed (wait_s).
+  bool phases = false;
+  struct PhaseEv {
+    int ph;
+    hipEvent_t a, b;
+  };
+  std::vector<PhaseEv> ph_pending;
+  std::vector<hipEvent_t> ph_pool;
+  double ph_ms[4] = {};
+  uint64_t ph_exchanges = 0;
+  double wait_s = 0;
 
   unsigned long long* cnt_send(int k) const { return cnt + k; }
   unsigned long long* cnt_recv(int k) const { return cnt + kLag + (size_t)k * nranks; }
@@ -344,6 +365,40 @@ struct HostTimer {
   ~HostTimer() { lap(nullptr); }
 };
 
+hipEvent_t ph_event(gs_group* g) {
+  if (!g->ph_pool.empty()) {
+    hipEvent_t e = g->ph_pool.back();
+    g->ph_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+// phase timing: an event on st now (the phase's start), or nullptr when timing is off
+hipEvent_t ph_begin(gs_group* g, hipStream_t st) {
+  if (!g->phases) return nullptr;
+  hipEvent_t a = ph_event(g);
+  (void)hipEventRecord(a, st);
+  return a;
+}
+void ph_end(gs_group* g, int ph, hipEvent_t a, hipStream_t st) {
+  if (!a) return;
+  hipEvent_t b = ph_event(g);
+  (void)hipEventRecord(b, st);
+  g->ph_pending.push_back({ph, a, b});
+}
+void ph_drain(gs_group* g) {
+  for (auto& p : g->ph_pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess)
+      g->ph_ms[p.ph] += ms;
+    g->ph_pool.push_back(p.a);
+    g->ph_pool.push_back(p.b);
+  }
+  g->ph_pending.clear();
+}
+
 // The data half of exchange e: wait for its gathered counts (host-mapped), gather
 // exactly max-count rows per rank, fold the other ranks' live rows on the apply
 // stream. No host synchronisation beyond the count poll.
@@ -361,6 +416,7 @@ int finish_data(gs_group* g, uint64_t e) {
       break;
     }
   }
+  g->wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   uint64_t maxc = 0, live = 0;
   for (int r = 0; r < g->nranks; ++r) {
     const uint64_t c = (uint64_t)hd[r] & (gs::kFailBit - 1);
@@ -372,8 +428,10 @@ int finish_data(gs_group* g, uint64_t e) {
   ht.lap(g->hostprof ? &g->hp[3] : nullptr);
   GS_HIP(hipStreamWaitEvent(g->xd, g->counted[k], 0));  // behind the stage (and the count collective)
   if (e >= (uint64_t)kLag) GS_HIP(hipStreamWaitEvent(g->xd, g->applied[k], 0));  // recv[k]: fold of e - kLag done
+  hipEvent_t pa = ph_begin(g, g->xd);
   const int r = g->api->allGather(g->send[k], g->recv[k], rows * g->width, kNcclInt64, g->comm_d, g->xd);
   if (r != 0) return rccl_fail(g->api, "ncclAllGather(data)", r);
+  ph_end(g, 3, pa, g->xd);
   GS_HIP(hipEventRecord(g->gathered[k], g->xd));
   const bool use_side = side_ok(h) && !g->no_side;
   hipStream_t s = use_side ? h->side : h->stream;
@@ -386,9 +444,11 @@ int finish_data(gs_group* g, uint64_t e) {
     fs.units = live;
     fs.on_side = use_side;
     const uint8_t* w = g->width == 3 ? reinterpret_cast<const uint8_t*>(g->recv[k] + 2) : nullptr;
+    hipEvent_t pf = ph_begin(g, s);
     if (int rc = fold_device_impl(h, g->recv[k], g->recv[k] + 1, w, (size_t)g->nranks * rows, g->width,
                                   8 * g->width, /*track=*/false, true, fs))
       return rc;
+    ph_end(g, 1, pf, s);
   }
   GS_HIP(hipEventRecord(g->applied[k], s));
   g->rows_received += rows * (uint64_t)(g->nranks - 1);
@@ -548,6 +608,9 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   h->dset = d;
   int frc = GS_OK;
   bool used_lane[kGroupLanes] = {};
+  hipEvent_t po[kGroupLanes] = {};
+  if (g->phases)
+    for (int i = 0; i < kGroupLanes; ++i) po[i] = ph_begin(g, lanes ? h->lane[i] : h->stream);
   for (size_t off = 0; off < n && !frc; off += kMicro) {
     FoldSource fs;
     if (lanes) {
@@ -562,6 +625,11 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   // the stage waits for every micro-batch of this exchange (one event per lane used)
   int nev = 0;
   hipEvent_t evs[kGroupLanes];
+  for (int i = 0; i < kGroupLanes; ++i) {
+    if (!po[i]) continue;
+    if (lanes ? used_lane[i] : i == 0) ph_end(g, 0, po[i], lanes ? h->lane[i] : h->stream);
+    else g->ph_pool.push_back(po[i]);  // (recorded, never timed)
+  }
   if (!lanes) {
     GS_HIP(hipEventRecord(g->folded[d][0], h->stream));
     evs[nev++] = g->folded[d][0];
@@ -578,6 +646,7 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   // read send[k] / cnt_send[k])
   for (int i = 0; i < nev; ++i) GS_HIP(hipStreamWaitEvent(g->xc, evs[i], 0));
   if (b >= (uint64_t)kLag) GS_HIP(hipStreamWaitEvent(g->xc, g->applied[k], 0));
+  hipEvent_t pc = ph_begin(g, g->xc);
   if (int rc = stage_delta(h, g->send[k], g->rows_cap, g->width, g->cnt_send(k), h->kind == GS_KIND_SIGNED, g->xc, d))
     return rc;
   GS_HIP(hipEventRecord(g->staged[d], g->xc));
@@ -585,10 +654,12 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   if (r != 0) return rccl_fail(g->api, "ncclAllGather(counts)", r);
   gs::launch_headers(g->cnt_recv(k), g->nranks, g->hdr_dev + (size_t)k * (g->nranks + 1), (long long)b, g->xc);
   GS_HIP(hipGetLastError());
+  ph_end(g, 2, pc, g->xc);
   GS_HIP(hipEventRecord(g->counted[k], g->xc));
   ht.lap(nullptr);
   g->b++;
   g->exchanges++;
+  if (g->phases) g->ph_exchanges++;
   // data lag L < kLag: the data half of exchange b - L, after this exchange's own folds
   // are queued -- the host waits for that exchange's counts (its folds done) while the
   // GPU already has this exchange's folds, and its remote rows are folded beside them:
@@ -767,6 +838,45 @@ int gs_group_stats(gs_group_t g, uint64_t* exchanges, uint64_t* records_sent, ui
   return GS_OK;
 }
 
+int gs_group_comm_ranks(gs_group_t g, int* count_comm, int* data_comm) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  if (!g->api->commCount) return fail(GS_ERR_HIP, "RCCL is missing ncclCommCount");
+  int c = 0, d = 0;
+  if (g->comm_c) {
+    const int r = g->api->commCount(g->comm_c, &c);
+    if (r) return rccl_fail(g->api, "ncclCommCount(counts)", r);
+  }
+  if (g->comm_d) {
+    const int r = g->api->commCount(g->comm_d, &d);
+    if (r) return rccl_fail(g->api, "ncclCommCount(data)", r);
+  }
+  if (count_comm) *count_comm = c;
+  if (data_comm) *data_comm = d;
+  return GS_OK;
+}
+
+int gs_group_set_phase_timing(gs_group_t g, int on) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  DeviceGuard dg(g->h->device);
+  ph_drain(g);
+  g->phases = on != 0;
+  for (double& x : g->ph_ms) x = 0;
+  g->ph_exchanges = 0;
+  g->wait_s = 0;
+  return GS_OK;
+}
+
+int gs_group_phase_stats(gs_group_t g, double* out6) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  if (!out6) return fail(GS_ERR_INVALID, "out is null");
+  DeviceGuard dg(g->h->device);
+  ph_drain(g);  // (synchronises the phases' end events)
+  for (int i = 0; i < 4; ++i) out6[i] = g->ph_ms[i];
+  out6[4] = g->wait_s * 1e3;
+  out6[5] = (double)g->ph_exchanges;
+  return GS_OK;
+}
+
 int gs_group_destroy(gs_group_t g) {
   if (!g) return GS_OK;
   if (g->hostprof && g->hp_calls) {
@@ -807,6 +917,8 @@ int gs_group_destroy(gs_group_t g) {
     (void)hipFree(g->send[k]);
     (void)hipFree(g->recv[k]);
   }
+  ph_drain(g);
+  for (hipEvent_t e : g->ph_pool) (void)hipEventDestroy(e);
   (void)hipFree(g->cnt);
   if (g->xc) (void)hipStreamDestroy(g->xc);
   if (g->xd) (void)hipStreamDestroy(g->xd);

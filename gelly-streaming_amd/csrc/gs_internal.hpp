@@ -173,6 +173,7 @@ struct gs_summary {
   // resident window server (gs_set_window_server): one persistent launch serves the
   // latency path's windows; every other entry point stops it first (join_lanes)
   bool srv_on = false, srv_running = false;
+  int srv_fits = -1;                     // all kServerBlocks workgroups co-resident (-1: not yet checked)
   gs::ServerBox* srv_box = nullptr;      // host-mapped mailbox
   gs::ServerBcast* srv_bc = nullptr;     // device: block 0 -> other blocks
   unsigned long long srv_seq = 0;        // last window posted and completed

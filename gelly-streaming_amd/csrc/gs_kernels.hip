@@ -357,8 +357,8 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   NewVertices nvx;
   if (valid) {
     bool nu, nv;
-    const uint32_t su = lookup_resolve(t, ks, hu, k0u, l0u, lu, nu);
-    const uint32_t sv = lookup_resolve(t, kd, hv, k0v, l0v, lv, nv);
+    const uint32_t su = lookup_resolve<!TAKE>(t, ks, hu, k0u, l0u, lu, nu);
+    const uint32_t sv = lookup_resolve<!TAKE>(t, kd, hv, k0v, l0v, lv, nv);
     nvx = reserve_new_vertices(t, shard, nu, su, nv, sv);  // ids written after the hook
     if (dbg) atomicAdd(&dbg[1], (nu ? 1u : 0u) + ((nv && sv != su) ? 1u : 0u));
     // Delta: a new vertex with an edge to another vertex is always named by a hook
@@ -417,7 +417,11 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
 // every window: tools/server_trace.py.)
 // Exit conditions every wave reaches: a stop request, or no window for idle_ticks
 // (block 0 then tells the others and the host), or -- for the other blocks -- twice
-// that without any word from block 0.
+// that without any word from block 0. Block 0 does not leave idle while the last window
+// it handed out is incomplete (a workgroup that was not yet resident still has to fold
+// its edges: leaving would cut the window in half), except after 8 x idle_ticks; it
+// stores the seq of every window it takes in box->taken, so the host tells "left
+// before the window" (post it again) from "left inside it" (an error).
 template <bool SIGNED>
 __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, ServerBox* box, ServerBcast* bc,
                                                            unsigned long long* done, unsigned long long seq0,
@@ -428,6 +432,7 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
   D.lrec = lrec;
   D.lcnt = &lcnt;
   unsigned long long last = seq0;
+  unsigned long long last_done = 0;  // block 0: completion number of the last window it took
 #ifdef GS_SERVER_TRACE
   __shared__ unsigned long long tseen, tbc;
 #endif
@@ -451,6 +456,12 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
           continue;                          // a torn line: poll again at once
         }
         if (wall_clock64() - t0 > limit) {
+          if (b0 && last_done &&
+              __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < last_done &&
+              wall_clock64() - t0 < 8 * limit) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;  // the last window is still being folded
+          }
           s = kServerStop | last;
           break;
         }
@@ -462,7 +473,9 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
       if (b0) {
         // broadcast the tagged line as it was read (no wait: the other blocks check tags)
         if (!(s & kServerStop)) {
+          if (lane == 0) __hip_atomic_store(&box->taken, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if (lane < 8) __hip_atomic_store(&bc->seq + lane, lane == 0 ? s : v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          last_done = __shfl(v, 7, 64) & kServerTagMask;
         } else if (lane == 0) {
           __hip_atomic_store(&bc->seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&box->exited, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -694,6 +707,50 @@ __global__ __launch_bounds__(256) void k_export_list(Table t, int64_t* __restric
   for (uint64_t g = g0; g < total && g < cap_out; g += stride) export_one(t, vlist_at(t, pre, g), ov, ol, op, g, cap_out);
 }
 
+// Order-independent 64-bit digest of the summary's (vertex, canonical label, parity)
+// set (gs_digest): out += sum over vertices of mix64(v) * mix64(label + parity * K),
+// mod 2^64. Replicas of one summary (a group's ranks, a replay) agree exactly when their
+// partitions (and colourings) do, with no export to compare.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ unsigned long long digest_term(const Table& t, uint32_t s) {
+  int64_t k;
+  uint32_t l, acc;
+  load_slot(t.tab + s, k, l);
+  const int64_t v = settle_key(t, s, k);
+  int64_t kx = v;
+  find_ro(t, s, l, kx, acc);
+  return mix64((unsigned long long)v ^ 0x243F6A8885A308D3ull) *
+         mix64((unsigned long long)kx + (acc ? 0x13198A2E03707344ull : 0ull));
+}
+
+__global__ __launch_bounds__(256) void k_digest(Table t, unsigned long long* out) {
+  __shared__ uint32_t cnt[kShards];
+  __shared__ uint64_t pre[kShards + 1];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long sum = 0;
+  if (t.ctr[ctr_index(CTR_VOVF)]) {  // rare: the list is incomplete -- scan the table
+    for (uint64_t s = g0; s <= t.r0; s += stride) {
+      int64_t k;
+      uint32_t l;
+      load_slot(t.tab + s, k, l);
+      const bool present = (s == t.r0) ? ((t.tab[s].aux & kAuxPresent) != 0) : (k != kEmpty);
+      if (present) sum += digest_term(t, (uint32_t)s);
+    }
+  } else {
+    const uint64_t total = vlist_prefix(t, cnt, pre);
+    for (uint64_t g = g0; g < total; g += stride) sum += digest_term(t, vlist_at(t, pre, g));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if ((threadIdx.x & 63u) == 0 && sum) atomicAdd(out, sum);
+}
+
 // Stage the sharded delta list as contiguous records. grid = kShards blocks: block s
 // copies shard s to its prefix position (deterministic, no append atomics); rows
 // past `cap` are dropped (the count says how many there were). Block 0 writes the
@@ -910,6 +967,15 @@ void launch_window_server(bool sign, const Table& t, const Delta& D, ServerBox* 
                        idle_ticks);
 }
 
+int window_server_resident_blocks(bool sign, int device) {
+  int per_cu = 0, cus = 0;
+  const hipError_t e = sign ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_window_server<true>, kFoldBS, 0)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_window_server<false>, kFoldBS, 0);
+  if (e != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return 0;
+  return per_cu * cus;
+}
+
 void launch_export(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, hipStream_t st, int part,
                    int nparts) {
   const uint64_t all = (uint64_t)t.r0 + 1;
@@ -924,6 +990,10 @@ void launch_export(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64
 void launch_export_list(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, uint64_t bound,
                         hipStream_t st) {
   hipLaunchKernelGGL(k_export_list, dim3(list_grid(bound)), dim3(256), 0, st, t, ov, ol, op, cap_out);
+}
+
+void launch_digest(const Table& t, unsigned long long* out, uint64_t bound, hipStream_t st) {
+  hipLaunchKernelGGL(k_digest, dim3(list_grid(bound)), dim3(256), 0, st, t, out);
 }
 
 void launch_stage(const Table& t, const Delta& D, int64_t* out, uint64_t cap, int width,

@@ -56,7 +56,9 @@ struct alignas(64) ServerBox {      // host-mapped; written by the host, read by
   unsigned long long seq;          // window number (stored last, release) | kServerStop
   unsigned long long src, dst, n, rec, cap, cnt, done_seq;  // each gs::tag_word(seq, value)
   unsigned long long exited;       // block 0 stores 1 when the server leaves (stop or idle)
-  unsigned long long pad[7];
+  unsigned long long taken;        // block 0 stores the seq of every window it takes (before its broadcast)
+  unsigned long long bc_init;      // host: the broadcast word's first value (copied to the device at start)
+  unsigned long long pad[5];
 };
 struct alignas(64) ServerBcast {    // device memory: block 0 -> the other blocks (the tagged line)
   unsigned long long seq, src, dst, n, rec, cap, cnt, done_seq;
@@ -64,6 +66,9 @@ struct alignas(64) ServerBcast {    // device memory: block 0 -> the other block
 void launch_window_server(bool sign, const Table& t, const Delta& D, ServerBox* box, ServerBcast* bc,
                           unsigned long long* done, unsigned long long seq0, unsigned long long idle_ticks,
                           hipStream_t st);
+// Workgroups of k_window_server that can be resident on the device at once (occupancy x
+// CUs): a window completes only when all kServerBlocks of them run together.
+int window_server_resident_blocks(bool sign, int device);
 
 void launch_init(Slot* tab, uint64_t nslots, hipStream_t st);
 // micro-batch dedup: w[i] = 1 (keep) or 0x81 (skip: a repeat of an earlier pair of the batch)
@@ -75,6 +80,8 @@ void launch_export(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64
                    int part = 0, int nparts = 1);
 void launch_export_list(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, uint64_t bound,
                         hipStream_t st);
+// order-independent digest of the (vertex, label, parity) set, added into *out
+void launch_digest(const Table& t, unsigned long long* out, uint64_t bound, hipStream_t st);
 void launch_stage(const Table& t, const Delta& D, int64_t* out, uint64_t cap, int width,
                   unsigned long long* count_out, bool with_fail, hipStream_t st);
 void launch_report(uint32_t* ctr, uint64_t n, unsigned long long* out, unsigned epoch, hipStream_t st);

@@ -86,6 +86,19 @@ int gs_group_tree_combine(gs_group_t g);
  * has received (max-count rows from each other rank per exchange; synchronises). */
 int gs_group_stats(gs_group_t g, uint64_t* exchanges, uint64_t* records_sent, uint64_t* rows_received);
 
+/* Ranks of the group's two communicators (ncclCommCount): the world that actually
+ * formed, checked by bench.py's N > 1 line beside torch.distributed's world size. */
+int gs_group_comm_ranks(gs_group_t g, int* count_comm, int* data_comm);
+
+/* Per-phase timing of the exchange protocol (diagnostic; HIP timing events around each
+ * phase's device work while on). gs_group_phase_stats (synchronises) returns, since the
+ * last gs_group_set_phase_timing: out[0] own-fold lane milliseconds (summed over the
+ * pipelining lanes), out[1] remote-row fold ms, out[2] stage + count collective + headers
+ * ms, out[3] data collective ms, out[4] host ms spent waiting for gathered counts (timed
+ * whether or not phase timing is on), out[5] exchanges timed. */
+int gs_group_set_phase_timing(gs_group_t g, int on);
+int gs_group_phase_stats(gs_group_t g, double* out6);
+
 int gs_group_destroy(gs_group_t g);
 
 #ifdef __cplusplus

@@ -177,6 +177,17 @@ int gs_find(gs_handle h, int64_t v, int64_t* label, int* found);
  * Asynchronous on the handle's stream (DisjointSet.find, :66-80, for many ids). */
 int gs_find_labels_device(gs_handle h, const int64_t* v, size_t n, int64_t* label, uint8_t* found);
 
+/* Order-independent 64-bit digest of the summary (synchronises): the sum, mod 2^64, over
+ * every vertex v of mix64(v ^ C1) * mix64(label(v) + parity(v) * C2) (splitmix64
+ * finaliser; parity = 0 for GS_KIND_CC). Two summaries with the same partition (and
+ * colouring) have the same digest whatever their fold order, windows, devices or ranks,
+ * so replicas are compared without an export -- what the reference's tests compare as
+ * sorted strings (ConnectedComponentsTest.java:54-63, DisjointSet.toString :134-150).
+ * A GS_KIND_SIGNED summary whose verdict failed digests to GS_DIGEST_FAILED, as its
+ * output is (false,{}) (Candidates.java:194-196). Not part of the reference API. */
+#define GS_DIGEST_FAILED (~0ull)
+int gs_digest(gs_handle h, uint64_t* digest);
+
 /* Export every (vertex, canonical label) pair to HOST arrays of capacity `cap`,
  * unordered. *n = number of vertices (GS_ERR_TRUNCATED if cap < *n; nothing
  * written). Replaces getMatches()/find()/toString() sinks (DisjointSet.java:44-46,

@@ -209,6 +209,25 @@ def bip_quirk_divergence(src, dst, win=None, part=None):
     return {"quirk": quirk, "truth": truth, "diverges": quirk != truth}
 
 
+def _mix64(z):
+    z = np.asarray(z, dtype=np.uint64)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def label_digest(v, lab, parity=None):
+    """Restatement of gs_digest (include/gs_summary.h) over exported (v, label, parity)
+    rows: sum mod 2^64 of mix64(v ^ C1) * mix64(label + parity * C2). Checker only."""
+    v = np.asarray(v, dtype=np.int64).view(np.uint64)
+    lab = np.asarray(lab, dtype=np.int64).view(np.uint64)
+    p = np.zeros(len(v), np.uint64) if parity is None else np.asarray(parity).astype(np.uint64)
+    with np.errstate(over="ignore"):
+        a = _mix64(v ^ np.uint64(0x243F6A8885A308D3))
+        b = _mix64(lab + np.where(p != 0, np.uint64(0x13198A2E03707344), np.uint64(0)))
+        return int(np.sum(a * b, dtype=np.uint64))
+
+
 # ---------------- canonical formatting shared by tests ----------------
 def canonical_cc_string(v, lab):
     """'{min=[members ascending], ...}' -- DisjointSet.toString() shape."""

@@ -66,3 +66,21 @@ def test_no_gpu_visible_refuses_before_launch():
                        text=True, timeout=300)
     assert r.returncode != 0 and "GPU(s) visible" in r.stderr
     assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
+
+
+def test_digest_self_check_two_ranks_gloo():
+    """the N-rank line's label self-check (replica_digest_checks: MIN
+    and MAX all-reduce of every replica's gs_digest, compared with the single-GPU digest)
+    over 2 gloo ranks: equal replicas pass, one diverging replica fails both checks."""
+    d = "0x8000000000000001"  # above 2^63: the signed all-reduce round trip
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check", "--launch-check-digest", d],
+                       env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    chk = _last_json(r.stdout)["self_check"]
+    assert chk["replica_label_digests_equal"] and chk["digest_equals_single_gpu"]
+    assert chk["digest"] == "8000000000000001"
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check", "--launch-check-digest", d,
+                        "--launch-check-digest-skew", "7"], env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    chk = _last_json(r.stdout)["self_check"]
+    assert not chk["replica_label_digests_equal"] and not chk["digest_equals_single_gpu"]

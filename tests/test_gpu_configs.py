@@ -121,26 +121,35 @@ def test_config5_er_windows_with_delta_records(gs, oracle_mod):
         _check_properties(s, src, dst)
 
 
-def test_config4_bipartite_full_stream(gs, oracle_mod):
-    """Config 4 at full size: sides of 2^19, E = 2^24 in 2^20-edge windows. Odd-cycle
-    variant (same-side edges injected at E/8, E/4, E/2, 3E/4): the verdict flips in
-    exactly the window of the first conflicting edge (truth: the oracle's parity
-    union-find). Clean variant: bipartite, colouring equal to the truth."""
+def _bip_first_appearance(gs, E, logside, inject):
+    """Config 4's stream as SURVEY.md 8(d) specifies it: ids in first-appearance order."""
     import torch
-    logside, E, B = 19, 1 << 24, 1 << 20
-    inject = [E // 8, E // 4, E // 2, 3 * E // 4]
     src = torch.empty(E, dtype=torch.int64, device="cuda")
     dst = torch.empty(E, dtype=torch.int64, device="cuda")
     gs.gen_bip(src, dst, 0, E, logside, 0x5EED0B1B, inject)
     torch.cuda.synchronize()
+    gs.relabel_first_appearance(src, dst, 2 << logside)
+    torch.cuda.synchronize()
+    return src, dst
+
+
+def test_config4_bipartite_full_stream(gs, oracle_mod):
+    """Config 4 at full size: sides of 2^19, E = 2^24 in 2^20-edge windows, ids in
+    first-appearance order. Odd-cycle variant (same-side edges injected at E/8, E/4, E/2,
+    3E/4): the verdict flips in exactly the window of the first conflicting edge (truth:
+    the oracle's parity union-find). Clean variant: bipartite, colouring equal to the
+    truth."""
+    import torch
+    logside, E, B = 19, 1 << 24, 1 << 20
+    inject = [E // 8, E // 4, E // 2, 3 * E // 4]
+    src, dst = _bip_first_appearance(gs, E, logside, inject)
     first = oracle_mod.bip_first_failure(src.cpu().numpy(), dst.cpu().numpy())
     assert first >= 0
     with gs.Summary("signed", capacity_hint=1 << 20) as c:
         for o in range(0, E, B):
             c.fold_device(src[o:], dst[o:], n=B)
             assert c.ok() == (first >= o + B), (o, first)
-    gs.gen_bip(src, dst, 0, E, logside, 0x5EED0B1B, [])
-    torch.cuda.synchronize()
+    src, dst = _bip_first_appearance(gs, E, logside, [])
     with gs.Summary("signed", capacity_hint=1 << 20) as c:
         c.set_pipelining(3)
         for o in range(0, E, B):
@@ -149,3 +158,22 @@ def test_config4_bipartite_full_stream(gs, oracle_mod):
     tok, tcomp, tv, tsign = oracle_mod.bip_truth(src.cpu().numpy(), dst.cpu().numpy())
     assert ok and tok
     assert np.array_equal(comp, tcomp) and np.array_equal(v, tv) and np.array_equal(sign, tsign)
+
+
+@pytest.mark.parametrize("variant", ["odd_cycle", "clean"])
+def test_config4_prefix_equals_reference_candidates(gs, oracle_mod, variant):
+    """on the first 2^15 edges of config 4's stream (first-appearance
+    ids, one window, p = 1 -- the reference's exact regime) the GPU's
+    output string equals the REFERENCE's: the quirk-exact restatement of
+    Candidates.merge (Candidates.java:77-192, BipartitenessCheck.java:54-61), whose result
+    must not diverge from the truth there."""
+    logside, E, m = 19, 1 << 24, 1 << 15
+    inject = [E // 8, E // 4, E // 2, 3 * E // 4] if variant == "odd_cycle" else []
+    src, dst = _bip_first_appearance(gs, E, logside, inject)
+    ps, pd = src[:m].cpu().numpy(), dst[:m].cpu().numpy()
+    div = oracle_mod.bip_quirk_divergence(ps, pd)
+    assert not div["diverges"]
+    with gs.Summary("signed", capacity_hint=m) as c:
+        c.fold_device(src[:m], dst[:m], n=m)
+        got = oracle_mod.canonical_candidates_string(*c.colouring())
+    assert got == div["quirk"]

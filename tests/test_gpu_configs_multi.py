@@ -18,8 +18,9 @@ fold of the other ranks' rows on the side stream -- is the code bench.py runs at
   own forest, which no hook record names: the verdict travels in the count word's
   fail bit (Candidates.merge :79-81). Every replica's verdict equals the truth; on the
   clean stream every replica's colouring equals the truth.
-* Config 5: gs_fold_take_device (the bench's fused window) over all 1024 windows of
-  G(2^22, 2^26); the records replayed on the device (gs_fold_records_counted_device,
+* Config 5: gs_fold_take_device over all 1024 windows of G(2^22, 2^26), as one fused
+  launch per window and through the resident window server (bench.py's default);
+  the records replayed on the device (gs_fold_records_counted_device,
   the replica's stream ordered with gs_wait_stream, no host synchronisation) rebuild
   the summary; oracle-exact at windows 1, 8 and 64, replay-exact at 1, 8, 64 and 1024.
 Reference: S/SummaryBulkAggregation.java:76-83 (partitions, combine),
@@ -155,6 +156,8 @@ def test_config4_eight_ranks_full_stream(gs, oracle_mod, monkeypatch, variant):
     dst = torch.empty(E, dtype=torch.int64, device="cuda")
     gs.gen_bip(src, dst, 0, E, logside, seed, inject)
     torch.cuda.synchronize()
+    gs.relabel_first_appearance(src, dst, 2 << logside)  # SURVEY.md 8(d) config 4 ids (an isomorphism)
+    torch.cuda.synchronize()
     hs, hd = src.cpu().numpy(), dst.cpu().numpy()
     tok, tcomp, tv, tsign = oracle_mod.bip_truth(hs, hd)
     if variant == "mid_shard":
@@ -185,7 +188,13 @@ def test_config4_eight_ranks_full_stream(gs, oracle_mod, monkeypatch, variant):
             assert v.size == 0  # (false,{}) -- Candidates.fail(), Candidates.java:194-196
 
 
-def test_config5_fused_window_take_all_windows(gs, oracle_mod):
+@pytest.mark.parametrize("mode", ["launch", "server"])
+def test_config5_window_take_all_windows(gs, oracle_mod, mode):
+    """Config 5 as bench.py times it, over all 1024 windows: `launch` = one fused launch
+    per window, `server` = the resident window server (bench.py's default er mode,
+    VERDICT r3 item 1). The server is never stopped by a wait here: each window's records
+    go to their own slot of a ring of 64 buffers, and the replica is synchronised every 32
+    windows, so a slot is rewritten only after the replay that read it has completed."""
     import torch
     logn, E, B = 22, 1 << 26, 1 << 16
     nwin = E // B
@@ -194,21 +203,27 @@ def test_config5_fused_window_take_all_windows(gs, oracle_mod):
     gs.gen_er(src, dst, 0, E, logn, 0x5EED00E5, True)
     torch.cuda.synchronize()
     cap = B + 16
-    recs = [torch.empty((cap, 3), dtype=torch.int64, device="cuda") for _ in range(2)]
-    cnts = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(2)]
+    nbuf = 2 if mode == "launch" else 64
+    recs = [torch.empty((cap, 3), dtype=torch.int64, device="cuda") for _ in range(nbuf)]
+    cnts = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(nbuf)]
     torch.cuda.synchronize()
     ps, pd = src.data_ptr(), dst.data_ptr()
     checkpoints = {1, 8, 64, nwin}
     total = 0
     with gs.Summary("cc", capacity_hint=1 << logn) as s, gs.Summary("cc", capacity_hint=1 << logn) as rep:
         s.set_delta_tracking(True)
+        if mode == "server":
+            s.set_window_server(True)
         rep_stream = rep.stream
         for w in range(nwin):
             o = w * B
-            k = w & 1
-            # the take overwrites recs[k], which the replay of window w - 2 read: order
-            # the summary behind the replica's queued work on the device
-            s.wait_stream(rep_stream)
+            k = w % nbuf
+            if mode == "launch":
+                # the take overwrites recs[k], which the replay of window w - 2 read: order
+                # the summary behind the replica's queued work on the device
+                s.wait_stream(rep_stream)
+            elif w % 32 == 0:
+                rep.sync()  # every replay of a slot about to be reused has completed
             got = s.fold_take(ps + 8 * o, pd + 8 * o, B, recs[k], cap, cnts[k])
             assert got <= B  # at most one record per folded edge
             total += got
@@ -221,3 +236,7 @@ def test_config5_fused_window_take_all_windows(gs, oracle_mod):
                     ov, olab = oracle_mod.cc_labels(src[:o + B].cpu().numpy(), dst[:o + B].cpu().numpy())
                     assert np.array_equal(v1, ov) and np.array_equal(l1, olab), "oracle differs at window %d" % (w + 1)
         assert total >= s.num_vertices() - len(set(s.labels()[1].tolist()))
+        if mode == "server":
+            st = s.window_server_stats()
+            # only the checkpoint reads stopped it (and, rarely, an idle exit)
+            assert st["windows"] >= nwin - len(checkpoints) - 4 and st["launches"] <= len(checkpoints) + 4, st

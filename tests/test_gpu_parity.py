@@ -624,3 +624,45 @@ def test_delta_list_full_error_leaves_capacity_tracking_intact(gs, oracle_mod):
         v, lab = s.labels()
     ov, olab = oracle_mod.cc_labels(src.cpu().numpy(), dst.cpu().numpy())
     assert np.array_equal(v, ov) and np.array_equal(lab, olab)
+
+
+def test_digest_matches_restatement_and_is_order_free(gs, oracle_mod):
+    """gs_digest (the N > 1 bench line's label self-check) equals the
+    checker's restatement over the oracle's labels, is independent of fold order,
+    windowing and pipelining, differs when one edge is missing, and is GS_DIGEST_FAILED for
+    a signed summary whose verdict failed."""
+    s, d = oracle_mod.rmat_edges(0x5EED0020, 14, 0, 1 << 16, True)
+    ov, olab = oracle_mod.cc_labels(s, d)
+    want = oracle_mod.label_digest(ov, olab)
+    rng = np.random.default_rng(5)
+    perm = rng.permutation(len(s))
+    digests = []
+    for order, chunk, pipe in ((None, 1 << 16, 1), (perm, 1 << 12, 3), (perm[::-1].copy(), 777, 2)):
+        ss, dd = (s, d) if order is None else (s[order], d[order])
+        with gs.Summary("cc", capacity_hint=1 << 12) as c:
+            c.set_pipelining(pipe)
+            for o in range(0, len(ss), chunk):
+                c.fold(ss[o:o + chunk], dd[o:o + chunk])
+            digests.append(c.digest())
+    assert digests == [want] * 3
+    with gs.Summary("cc", capacity_hint=1 << 12) as c:
+        c.fold(s[1:], d[1:])
+        v2, l2 = oracle_mod.cc_labels(s[1:], d[1:])
+        assert c.digest() == oracle_mod.label_digest(v2, l2)
+        if not (np.array_equal(v2, ov) and np.array_equal(l2, olab)):
+            assert c.digest() != want
+    bs, bd = oracle_mod.bip_edges(0x5EED0B1B, 10, 0, 3000)
+    ok, comp, v, sign = oracle_mod.bip_truth(bs, bd)
+    with gs.Summary("signed", capacity_hint=1 << 11) as c:
+        c.fold(bs, bd)
+        assert ok and c.ok()
+        # parity(v) xor parity(label) = 1 - sign
+        assert c.digest() == oracle_mod.label_digest(v, comp, 1 - np.asarray(sign, np.int64))
+        c.fold(np.array([bs[0]], np.int64), np.array([bd[0]], np.int64))  # same edge again: still bipartite
+        assert c.ok()
+        # an odd cycle: a vertex and its component's minimum, required on the sides they are not on
+        i = int(np.nonzero(np.asarray(v) != np.asarray(comp))[0][0])
+        w = np.array([1 if sign[i] else 0], np.uint8)
+        c.fold_parity(np.array([v[i]], np.int64), np.array([comp[i]], np.int64), w)
+        assert not c.ok()
+        assert c.digest() == gs.DIGEST_FAILED

@@ -268,3 +268,47 @@ def test_window_server_equals_fused_launch(gs, oracle_mod, kind):
         else:
             tok = oracle_mod.bip_truth(hs, hd)[0]
             assert srv.ok() == ref.ok() == rep.ok() == tok
+
+
+@pytest.mark.parametrize("how", ["stream", "event"])
+def test_window_server_stops_for_a_wait(gs, oracle_mod, how):
+    """a wait (gs_wait_stream / gs_wait_event) must order the next window
+    behind the producer even while the resident server runs. Each window is copied into
+    ONE reused buffer on a torch stream behind a GPU sleep and ordered by a wait only (no
+    host synchronisation): the wait stops the server, and the window starts a new server
+    launch queued behind it. Without that, the running server would fold the buffer
+    before (or while) the producer writes it."""
+    import torch
+    E, B = 1 << 16, 1 << 12
+    src = torch.empty(E, dtype=torch.int64, device="cuda")
+    dst = torch.empty(E, dtype=torch.int64, device="cuda")
+    gs.gen_er(src, dst, 0, E, 14, 0x5EED00E5, True)
+    torch.cuda.synchronize()
+    bs = torch.zeros(B, dtype=torch.int64, device="cuda")
+    bd = torch.zeros(B, dtype=torch.int64, device="cuda")
+    rec = torch.empty((B, 3), dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    prod = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with gs.Summary("cc", capacity_hint=1 << 14) as s:
+        s.set_delta_tracking(True)
+        s.set_window_server(True)
+        s.fold_take(src, dst, 1, rec, B, cnt)  # the server is running now
+        for w in range(E // B):
+            o = w * B
+            with torch.cuda.stream(prod):
+                torch.cuda._sleep(300000)  # the writer is still busy when the window is posted
+                bs.copy_(src[o:o + B])
+                bd.copy_(dst[o:o + B])
+                ev = torch.cuda.Event()
+                ev.record(prod)
+            if how == "stream":
+                s.wait_stream(prod)
+            else:
+                s.wait_event(ev)
+            s.fold_take(bs, bd, B, rec, B, cnt)  # returns when the window is complete
+        st = s.window_server_stats()
+        assert st["launches"] >= E // B, st  # every wait stopped the server
+        v, lab = s.labels()
+    ov, olab = oracle_mod.cc_labels(src.cpu().numpy(), dst.cpu().numpy())
+    assert np.array_equal(v, ov) and np.array_equal(lab, olab)

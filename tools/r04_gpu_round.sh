@@ -1,0 +1,17 @@
+#!/bin/bash
+# r04 GPU pass: the round-end evidence (tools/final_round.sh) plus a per-dispatch kernel
+# trace of the config-4 (bipartiteness) step.
+# Usage (repo root on the GPU box): bash tools/r04_gpu_round.sh <tag>
+set -u
+TAG=${1:-r04a}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+bash tools/final_round.sh $TAG || exit 1
+O=$R/gpurun_out/final_$TAG
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 240 rocprofv3 --kernel-trace -d /tmp/bip_$TAG -o run -- python3 $R/bench.py --workload bip --steps 3 --warmup 1 --profile-only --no-profile-pass > $O/bip_trace.log 2>&1 || { echo "bip trace failed rc=$?"; exit 1; }
+DB=$(find /tmp/bip_$TAG -name "*.db" | head -1)
+python3 $R/tools/step_dispatches.py "$DB" 1.2 > $O/bip_dispatches.txt
+python3 $R/tools/timeline.py "$DB" 0 > $O/bip_timeline.txt
+rm -rf /tmp/bip_$TAG
+echo "bip trace ok"
