@@ -93,7 +93,10 @@ def _traffic_fields(pm, launches, step_s):
 # gs_digest of the single-GPU summary after the whole stream, per (scale, edge factor,
 # seed): the constant every N > 1 replica must reproduce (computed by a one-GPU
 # bench.py run of this build; the N = 1 line recomputes and checks it).
-KNOWN_DIGESTS = {}
+KNOWN_DIGESTS = {
+    "rmat26-ef16-seed0x5eed0026": 0x961EBDC5F302C813,  # config 3 (r04a: N = 1 and the 1-rank exchange path)
+    "bip-config4-clean": 0x5648FC1682105E51,           # config 4, clean stream, first-appearance ids (r04a)
+}
 
 
 def _as_i64(u):
@@ -129,7 +132,8 @@ def parse():
     p.add_argument("--scale", type=int, default=26)
     p.add_argument("--edge-factor", type=int, default=16)
     p.add_argument("--log-batch", type=int, default=20)
-    p.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED0026)
+    p.add_argument("--seed", type=lambda x: int(x, 0), default=None,
+                   help="RMAT seed (default: SURVEY.md 8(d)'s, 0x5EED0020 for --scale 20 = config 2, else 0x5EED0026)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--bip-prefix-log2", type=int, default=15,
                    help="bip: edges of the prefix the quirk-exact Candidates oracle folds (O(E x components))")
@@ -278,6 +282,12 @@ def bench_bip(args):
     per = E // world
     start = rank * per
     summ = gs.Summary("signed", device=local, capacity_hint=1 << 20)
+    group = None
+    if not grouped and args.pipeline > 1:
+        # lanes first: every HIP stream maps onto one of GPU_MAX_HW_QUEUES (4) queues, and
+        # lanes created after torch's null stream share one (effective depth 2: the r04a
+        # trace of this step, profiles/r04_bip_dispatches.txt)
+        summ.set_pipelining(args.pipeline)
 
     def stream(inject):
         """The whole config-4 stream with ids renamed in first-appearance order (SURVEY.md
@@ -294,13 +304,10 @@ def bench_bip(args):
     src, dst = fs[start:start + per].clone(), fd[start:start + per].clone()
     del fs, fd
     torch.cuda.synchronize(dev)
-    group = None
     if grouped:
         uid = [gs.group_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         group = gs.Group(summ, uid[0], world, rank, B)
-    elif args.pipeline > 1:
-        summ.set_pipelining(args.pipeline)
     ok = [True]
 
     def one_step():
@@ -479,6 +486,7 @@ def bench_er_latency(args):
     k_host = ctypes.c_uint64()
     k_ref = ctypes.byref(k_host)
     res = {}
+    lat_of = {}
     for mode in ("launch", "server"):
         summ.set_window_server(mode == "server")
         for step in range(args.warmup + 1):
@@ -494,6 +502,7 @@ def bench_er_latency(args):
                     raise gs.GSError(rc, gs.lib().gs_last_error().decode())
                 nrec += k_host.value
         lat = np.array(lat) * 1e6
+        lat_of[mode] = lat
         res[mode] = {"p50_us": round(float(np.percentile(lat, 50)), 2), "p99_us": round(float(np.percentile(lat, 99)), 2),
                      "max_us": round(float(lat.max()), 2), "total_ms": round(lat.sum() * 1e-3, 3),
                      "edges_per_s": round(E / (lat.sum() * 1e-6), 1), "delta_records": nrec}
@@ -515,6 +524,39 @@ def bench_er_latency(args):
     for m in res.values():
         for k in ("_v", "_lab", "_nv"):
             m.pop(k)
+    # Latency floors of a window, the p50 is read against them:
+    #  * hand-off floor: the same mode with 64-edge windows (one workgroup's dependent chain
+    #    + the post/poll hand-off), 1024 windows from the stream's start, a fresh summary;
+    #  * request floor: the window's fabric requests at the calibrated ceiling (>= one per
+    #    endpoint probe: 2 x 2^16 requests at 53.5 G/s).
+    summ.set_window_server(args.er_mode == "server")
+    summ.reset()
+    tiny = []
+    for w in range(E // B):
+        o = w * B
+        t0 = time.perf_counter()
+        take(summ._h, ps + 8 * o, pd + 8 * o, 64, prec, cap, pcnt, k_ref)
+        tiny.append(time.perf_counter() - t0)
+    handoff_us = float(np.percentile(np.array(tiny) * 1e6, 50))
+    request_us = 2.0 * B / REQUEST_CEILING_PER_S * 1e6
+    sel_lat = lat_of[args.er_mode]
+    p99v = float(np.percentile(sel_lat, 99))
+    slow = np.nonzero(sel_lat >= p99v)[0]
+    tail = {"p50_us_first_64_windows": round(float(np.percentile(sel_lat[:64], 50)), 2),
+            "p50_us_windows_64_on": round(float(np.percentile(sel_lat[64:], 50)), 2),
+            "p99_windows_index_median": int(np.median(slow)) if len(slow) else None,
+            "p99_windows_in_first_64": int((slow < 64).sum()), "p99_windows": int(len(slow)),
+            "note": "where the slowest 1% of windows sit in the stream: the young table's windows insert most "
+                    "of their endpoints (CAS + vertex-list append per new vertex)"}
+    floor_us = max(handoff_us, request_us)
+    roof = {"kernel": "k_window_server" if args.er_mode == "server" else "k_fold<false, true, true>",
+            "bound": "latency", "achieved": None, "peak": None, "unit": "us", "frac": None, "traffic": None,
+            "achieved_p50_us": res[args.er_mode]["p50_us"], "floor_us": round(floor_us, 2),
+            "frac_floor_over_p50": round(floor_us / res[args.er_mode]["p50_us"], 3),
+            "handoff_floor_us": round(handoff_us, 2), "request_floor_us": round(request_us, 2),
+            "note": "latency path: the bound is the larger of the measured 64-edge-window latency of the same mode "
+                    "(dependent chain + hand-off) and the window's request floor (2 requests per edge at the "
+                    "calibrated 53.5 G/s); frac_floor_over_p50 = floor / p50"}
     import oracle  # checker and CPU baseline legs only
     nchk = 8
     summ.set_window_server(args.er_mode == "server")
@@ -540,10 +582,11 @@ def bench_er_latency(args):
                        "mode": args.er_mode, "p50_us": sel["p50_us"], "p99_us": sel["p99_us"],
                        "max_us": sel["max_us"], "edges_per_s": sel["edges_per_s"],
                        "delta_records": sel["delta_records"], "modes": res,
-                       "modes_agree": agree, "first_%d_windows_oracle_exact" % nchk: prefix_ok,
+                       "modes_agree": agree, "first_%d_windows_oracle_exact" % nchk: prefix_ok, "tail": tail,
                        "per_window": "fold + delta export to device + completion (host steady clock; "
                                      "gs_fold_take_device; launch = one fused launch per window, server = the "
                                      "resident window server)"},
+            "roofline": roof,
             "cpu_baseline": cpu}
     print(json.dumps(line), flush=True)
     summ.close()
@@ -668,6 +711,8 @@ def bench_dropin(args):
 
 def main():
     args = parse()
+    if args.seed is None:
+        args.seed = 0x5EED0020 if args.scale == 20 else 0x5EED0026
     rc = self_launch(args)
     if rc is not None:  # this process only launched the ranks
         sys.exit(rc)
@@ -824,8 +869,8 @@ def main():
         edges_per_launch = per / max(nf, 1) if not grouped else 1 << 20  # own micro-batches dominate
         achieved = BYTES_PER_EDGE_SPARSE * edges_per_launch / (fold_avg_ms * 1e-3) / 1e9
         step_gbs = BYTES_PER_EDGE_SPARSE * per / (elapsed / args.steps) / 1e9
-        pm, extra = _matching_pmc("pmc_fold_traffic.json", {"workload": "rmat%d-cc-stream" % args.scale,
-                                                              "batch": B, "pipeline": args.pipeline})
+        pm, extra = _matching_pmc("pmc_r20_traffic.json" if args.scale == 20 else "pmc_fold_traffic.json",
+                                  {"workload": "rmat%d-cc-stream" % args.scale, "batch": B, "pipeline": args.pipeline})
         traffic = None
         if pm is not None and not grouped:  # fabric request bytes (PMC, per launch) over the pipelined step
             traffic, extra = _traffic_fields(pm, nf, elapsed / args.steps)

@@ -451,8 +451,16 @@ int read_nv(gs_summary* h, uint64_t* nv) {
   return GS_OK;
 }
 
-// Sparse tables export / reset over the vertex list; dense ones scan the table.
-bool use_vertex_list(gs_summary* h, uint64_t nv_bound) { return h->vlist_ok && nv_bound * 4 < h->cap; }
+// Sparse tables export / reset over the vertex list; dense ones scan the table. A listed
+// slot costs a random 16-B access (~50 G/s, the request ceiling), a scanned one a share
+// of a streaming pass (~375 G slots/s at 6 TB/s): the list wins below ~1/8 load. The
+// bound is tightened with the landed capacity reports (a reset right after a pass of
+// folds would otherwise see 2 vertices per folded edge: config 4 re-initialised its
+// whole 2^24-slot table, 41 us of every step, for 2^20 vertices).
+bool use_vertex_list(gs_summary* h, uint64_t nv_bound) {
+  nv_bound = std::min<uint64_t>(nv_bound, capacity_bound(h, nullptr));
+  return h->vlist_ok && nv_bound * 8 < h->cap;
+}
 
 int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
                      size_t stride, size_t w_stride, bool track, bool check_cap, const FoldSource& fs) {

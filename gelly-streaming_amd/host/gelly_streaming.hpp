@@ -136,15 +136,20 @@ class HandlePool {
 // --------------------------------------------------------------------------
 // GPU-resident summaries
 // --------------------------------------------------------------------------
+//
+// The handle is taken from the pool at first use, not at construction: a summary built
+// where no GPU work happens (the Flink job client builds the operator's initial value,
+// ConnectedComponents.java:52-54, then ships it to the TaskManagers by Java
+// serialization) holds no device state. writeObject / readObject model that Java
+// serialization (GpuDisjointSet / GpuCandidates writeObject + readObject): a summary that
+// was never used travels as a one-byte marker, any other as its gs_serialize image, which
+// the copy applies on its own first use (SummaryAggregation.Merger's initialVal and
+// summary fields, SummaryAggregation.java:95-103).
 class GpuSummary {
  public:
   GpuSummary(int kind, int device, uint64_t capacity_hint, size_t flush_edges)
-      : kind_(kind), device_(device), hint_(capacity_hint), flush_edges_(flush_edges) {
-    h_ = HandlePool::instance().acquire(kind, device, capacity_hint);
-  }
-  virtual ~GpuSummary() {
-    if (h_) HandlePool::instance().release(h_, kind_, device_, hint_);
-  }
+      : kind_(kind), device_(device), hint_(capacity_hint), flush_edges_(flush_edges) {}
+  virtual ~GpuSummary() { release(); }
   GpuSummary(const GpuSummary&) = delete;
   GpuSummary& operator=(const GpuSummary&) = delete;
 
@@ -161,10 +166,55 @@ class GpuSummary {
   }
   void flush() {
     if (n_ == 0) return;
+    gs_handle h = ensure();
     const auto t0 = std::chrono::steady_clock::now();
-    gs_check(gs_fold(h_, src_.get(), dst_.get(), n_));
+    gs_check(gs_fold(h, src_.get(), dst_.get(), n_));
     flush_seconds() += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     n_ = 0;
+  }
+  // the device handle, taken at first use; a pending image (readObject) or an initial
+  // failed verdict (Candidates(false)) is applied to it then
+  gs_handle ensure() {
+    if (h_) return h_;
+    h_ = HandlePool::instance().acquire(kind_, device_, hint_);
+    if (!image_.empty()) {
+      std::vector<uint8_t> img;
+      img.swap(image_);
+      gs_check(gs_deserialize(h_, img.data(), img.size()));
+    } else if (failed_initially_) {
+      // :194-196 fail() == new Candidates(false): the image of a failed, empty summary
+      // (header only: magic 'GSS1', kind, ok = 0, n = 0)
+      std::vector<uint8_t> img(24, 0);
+      const uint32_t hdr[4] = {0x31535347u, (uint32_t)kind_, 0u, 0u};
+      std::memcpy(img.data(), hdr, 16);
+      gs_check(gs_deserialize(h_, img.data(), img.size()));
+    }
+    return h_;
+  }
+  bool acquired() const { return h_ != nullptr; }
+  // back to the pool (the glue's explicit release of a summary the combine dropped); the
+  // object reads as a fresh initial value afterwards
+  void release() {
+    n_ = 0;
+    image_.clear();
+    if (h_) HandlePool::instance().release(h_, kind_, device_, hint_);
+    h_ = nullptr;
+  }
+  // Java serialization of the summary object: [0] 1 = an image follows, [1] failed
+  // initially (Candidates(false)), then the gs_serialize image
+  std::vector<uint8_t> writeObject() {
+    std::vector<uint8_t> out = {0, (uint8_t)(failed_initially_ ? 1 : 0)};
+    if (!h_ && image_.empty() && n_ == 0) return out;  // never used: no device state to ship
+    const std::vector<uint8_t> img = h_ || n_ ? serialize() : image_;
+    out[0] = 1;
+    out.insert(out.end(), img.begin(), img.end());
+    return out;
+  }
+  void readObjectInto(const std::vector<uint8_t>& bytes) {  // (on a fresh object)
+    if (bytes.size() < 2) throw GsException(GS_ERR_INVALID, "readObject: truncated stream");
+    release();
+    failed_initially_ = bytes[1] != 0;
+    if (bytes[0]) image_.assign(bytes.begin() + 2, bytes.end());
   }
   // host seconds spent in gs_fold (micro-batch flushes), process-wide (dropin_bench)
   static double& flush_seconds() {
@@ -173,7 +223,7 @@ class GpuSummary {
   }
   gs_handle handle() {
     flush();
-    return h_;
+    return ensure();
   }
   size_t size() {
     uint64_t n = 0;
@@ -182,7 +232,8 @@ class GpuSummary {
   }
   void reset() {
     n_ = 0;
-    gs_check(gs_reset(h_));
+    image_.clear();
+    gs_check(gs_reset(ensure()));
   }
   // all (vertex, canonical label, parity) rows, sorted by vertex
   struct Row {
@@ -219,7 +270,8 @@ class GpuSummary {
   }
   void deserialize(const std::vector<uint8_t>& buf) {
     n_ = 0;
-    gs_check(gs_deserialize(h_, buf.data(), buf.size()));
+    image_.clear();
+    gs_check(gs_deserialize(ensure(), buf.data(), buf.size()));
   }
   int device() const { return device_; }
 
@@ -231,6 +283,8 @@ class GpuSummary {
   gs_handle h_ = nullptr;
   std::unique_ptr<int64_t[]> src_, dst_;  // [flush_edges_] each, allocated on first push
   size_t n_ = 0;                          // buffered edges
+  std::vector<uint8_t> image_;            // readObject: applied at first use
+  bool failed_initially_ = false;         // Candidates(false), applied at first use
 };
 
 // DisjointSet<Long> (DisjointSet.java:25-151) over the GPU forest. find() returns
@@ -254,6 +308,12 @@ class DisjointSet : public GpuSummary {
   void merge(DisjointSet& other) {  // :127-131
     if (&other == this) return;
     gs_check(gs_combine(handle(), other.handle()));
+  }
+  static std::shared_ptr<DisjointSet> readObject(const std::vector<uint8_t>& bytes, int device = 0,
+                                                 uint64_t capacity_hint = 1 << 16) {
+    auto d = std::make_shared<DisjointSet>(device, capacity_hint);
+    d->readObjectInto(bytes);
+    return d;
   }
   // getMatches() (:44-46) as (vertex, representative) pairs
   std::vector<std::pair<int64_t, int64_t>> getMatches() {
@@ -290,7 +350,13 @@ class Candidates : public GpuSummary {
   explicit Candidates(bool success = true, int device = 0, uint64_t capacity_hint = 1 << 16,
                       size_t flush_edges = 1 << 20)
       : GpuSummary(GS_KIND_SIGNED, device, capacity_hint, flush_edges) {
-    if (!success) fail();
+    failed_initially_ = !success;  // applied when the handle is taken
+  }
+  static std::shared_ptr<Candidates> readObject(const std::vector<uint8_t>& bytes, int device = 0,
+                                                uint64_t capacity_hint = 1 << 16) {
+    auto c = std::make_shared<Candidates>(true, device, capacity_hint);
+    c->readObjectInto(bytes);
+    return c;
   }
   bool getSuccess() {  // :44-46
     int ok = 1;
@@ -333,16 +399,6 @@ class Candidates : public GpuSummary {
       }
     }
     return s + "})";
-  }
-
- private:
-  // :194-196 fail() == new Candidates(false): load the serialized image of a failed,
-  // empty summary (header only: magic 'GSS1', kind, ok = 0, n = 0).
-  void fail() {
-    std::vector<uint8_t> img(24, 0);
-    const uint32_t hdr[4] = {0x31535347u, (uint32_t)GS_KIND_SIGNED, 0u, 0u};
-    std::memcpy(img.data(), hdr, 16);
-    deserialize(img);
   }
 };
 

@@ -18,22 +18,32 @@
  * same side as that minimum), which equals the reference's exactly in its exact
  * regime and the mathematical truth everywhere (DESIGN.md section 2); the reference's
  * order-dependent quirks are not reproduced.
+ *
+ * Java serialization as GpuDisjointSet's: the handle is taken at the first use (the job
+ * client builds the initial value without a GPU), writeObject ships the gs_serialize
+ * image (verdict included) and the copy applies it at its first use; a
+ * `new GpuCandidates(false)` that was never used ships its failed verdict as a field.
  */
 package org.apache.flink.graph.streaming.summaries;
 
+import java.io.IOException;
+import java.io.ObjectInputStream;
+import java.io.ObjectOutputStream;
 import java.util.Map;
 import java.util.TreeMap;
 
 import org.apache.flink.graph.streaming.util.SignedVertex;
 
 public class GpuCandidates extends Candidates implements GpuSummary {
-	private static final long serialVersionUID = 1L;
+	private static final long serialVersionUID = 2L;
 	static final int BATCH = GpuDisjointSet.BATCH;
 
-	private transient long handle;
-	private transient long[] src = new long[BATCH];
-	private transient long[] dst = new long[BATCH];
-	private transient byte[] par = new byte[BATCH];
+	private final boolean failedInitially;  // new GpuCandidates(false): applied at the first use
+	private transient long handle;          // 0 until the first use
+	private transient byte[] image;         // read by readObject, applied at the first use
+	private transient long[] src;           // edge buffers, allocated at the first edge
+	private transient long[] dst;
+	private transient byte[] par;
 	private transient int n;
 	private transient boolean plain = true;  // every buffered edge has parity 1 (a stream edge)
 
@@ -43,10 +53,7 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 
 	public GpuCandidates(boolean success) {
 		super(success);
-		handle = HandlePool.SIGNED.acquire();
-		if (!success) {
-			GsNative.markFailed(handle);
-		}
+		failedInitially = !success;
 	}
 
 	public GpuCandidates(boolean success, Candidates input) throws Exception {  // :36-42
@@ -55,6 +62,11 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 	}
 
 	private void buffer(long a, long b, boolean differentSides) {
+		if (src == null) {
+			src = new long[BATCH];
+			dst = new long[BATCH];
+			par = new byte[BATCH];
+		}
 		src[n] = a;
 		dst[n] = b;
 		par[n] = (byte) (differentSides ? 1 : 0);
@@ -86,12 +98,12 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 			GpuCandidates o = (GpuCandidates) input;
 			flush();
 			o.flush();
-			GsNative.combine(handle, o.handle);  // rows + verdict, ordered behind both handles
+			GsNative.combine(handle(), o.handle());  // rows + verdict, ordered behind both handles
 			return this;
 		}
 		if (!input.getSuccess()) {  // :79-81
 			flush();
-			GsNative.markFailed(handle);
+			GsNative.markFailed(handle());
 			return this;
 		}
 		for (Map.Entry<Long, Map<Long, SignedVertex>> comp : input.getMap().entrySet()) {
@@ -116,7 +128,7 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 	@Override
 	public boolean getSuccess() {
 		flush();
-		f0 = GsNative.bipStatus(handle);
+		f0 = GsNative.bipStatus(handle());
 		return f0;
 	}
 
@@ -124,11 +136,11 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 	public TreeMap<Long, Map<Long, SignedVertex>> getMap() {
 		flush();
 		TreeMap<Long, Map<Long, SignedVertex>> map = new TreeMap<>();
-		int c = (int) GsNative.numVertices(handle);
+		int c = (int) GsNative.numVertices(handle());
 		long[] comp = new long[c];
 		long[] v = new long[c];
 		byte[] sign = new byte[c];
-		int got = GsNative.exportColouring(handle, comp, v, sign);  // 0 rows once the verdict failed
+		int got = GsNative.exportColouring(handle(), comp, v, sign);  // 0 rows once the verdict failed
 		for (int i = 0; i < got; i++) {
 			map.computeIfAbsent(comp[i], k -> new TreeMap<>()).put(v[i], new SignedVertex(v[i], sign[i] != 0));
 		}
@@ -149,31 +161,71 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 	public void flush() {
 		if (n > 0) {
 			if (plain) {
-				GsNative.fold(handle, src, dst, n);  // every edge: different sides
+				GsNative.fold(handle(), src, dst, n);  // every edge: different sides
 			} else {
-				GsNative.foldParity(handle, src, dst, par, n);
+				GsNative.foldParity(handle(), src, dst, par, n);
 			}
 			n = 0;
 			plain = true;
 		}
 	}
 
+	/** The gs_handle, taken from the pool at the first use (a deserialised image or the
+	 *  initial failed verdict applied). */
 	@Override
 	public long handle() {
+		if (handle == 0) {
+			long h = HandlePool.SIGNED.acquire();
+			try {
+				if (image != null) {
+					GsNative.deserialize(h, image);  // rows and verdict
+				} else if (failedInitially) {
+					GsNative.markFailed(h);
+				}
+			} catch (RuntimeException e) {
+				HandlePool.SIGNED.release(h);
+				throw e;
+			}
+			image = null;
+			handle = h;
+		}
 		return handle;
 	}
 
+	/** Back to the pool (the combine dropped this summary, GpuBipartitenessCheck); it reads
+	 *  as a fresh initial value afterwards. */
 	@Override
 	public void release() {
+		n = 0;
+		plain = true;
+		image = null;
 		if (handle != 0) {
-			n = 0;
 			HandlePool.SIGNED.release(handle);
 			handle = 0;
 		}
 	}
 
+	// ---- Java serialization (the Merger's fields, SummaryAggregation.java:95-103)
+	private void writeObject(ObjectOutputStream out) throws IOException {
+		out.defaultWriteObject();
+		byte[] img = image;
+		if (img == null && (handle != 0 || n > 0)) {
+			flush();
+			img = GsNative.serialize(handle);
+		}
+		out.writeObject(img);  // null: never used (failedInitially travels as a field)
+	}
+
+	private void readObject(ObjectInputStream in) throws IOException, ClassNotFoundException {
+		in.defaultReadObject();
+		image = (byte[]) in.readObject();
+		handle = 0;
+		n = 0;
+		plain = true;
+	}
+
 	@Override
-	protected void finalize() {
+	protected void finalize() {  // backstop (Java 8) for summaries nobody released
 		release();
 	}
 }

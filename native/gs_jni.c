@@ -9,9 +9,12 @@
  *
  * Every ABI failure is rethrown as java.lang.RuntimeException(gs_last_error()), the
  * reference's `throws Exception` on EdgesFold.foldEdges / ReduceFunction.reduce
- * (S/EdgesFold.java:47). Host arrays are pinned with Get*ArrayCritical only around
- * calls that copy them before returning (gs_fold, gs_fold_parity); output arrays use
- * Get/Release*ArrayElements so that the rows are written back.
+ * (S/EdgesFold.java:47). Edge arrays are copied with Get<T>ArrayRegion into a
+ * per-thread native buffer before gs_fold / gs_fold_parity run: a fold of more than 2^18
+ * edges does host copies, HIP copies and an event wait, which JNI forbids inside a
+ * Get*ArrayCritical region (and which would stall the JVM's garbage collector for the
+ * whole fold). Output arrays use Get/Release*ArrayElements so that the rows are written
+ * back.
  */
 #include <jni.h>
 #include <stdint.h>
@@ -72,18 +75,44 @@ JNIEXPORT void JNICALL FN(resetConfig)(JNIEnv* env, jclass c, jlong h) {
 
 /* ---- fold / combine ------------------------------------------------------- */
 
+/* Per-thread native copy of a flush (one Flink subtask thread per summary): grown once
+ * to the summaries' flush size, reused by every later flush of the thread. */
+typedef struct {
+  int64_t *s, *d;
+  uint8_t* w;
+  size_t cap;
+} EdgeStage;
+static _Thread_local EdgeStage t_stage;
+
+static int stage_reserve(JNIEnv* env, size_t n) {
+  if (n <= t_stage.cap) return 1;
+  int64_t* s = realloc(t_stage.s, n * 8);
+  if (s) t_stage.s = s;
+  int64_t* d = s ? realloc(t_stage.d, n * 8) : NULL;
+  if (d) t_stage.d = d;
+  uint8_t* w = d ? realloc(t_stage.w, n) : NULL;
+  if (w) t_stage.w = w;
+  if (!w) {
+    jclass ex = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+    if (ex) (*env)->ThrowNew(env, ex, "gs_jni: edge staging buffer");
+    return 0;
+  }
+  t_stage.cap = n;
+  return 1;
+}
+
 JNIEXPORT void JNICALL FN(fold)(JNIEnv* env, jclass c, jlong h, jlongArray src, jlongArray dst, jint n) {
   (void)c;
   if (n < 0 || (*env)->GetArrayLength(env, src) < n || (*env)->GetArrayLength(env, dst) < n) {
     throw_msg(env, "fold: n outside the arrays");
     return;
   }
-  jlong* s = (*env)->GetPrimitiveArrayCritical(env, src, NULL); /* no copy on HotSpot */
-  jlong* d = (*env)->GetPrimitiveArrayCritical(env, dst, NULL);
-  const int rc = (s && d) ? gs_fold(H(h), (const int64_t*)s, (const int64_t*)d, (size_t)n) : GS_ERR_INVALID;
-  if (d) (*env)->ReleasePrimitiveArrayCritical(env, dst, d, JNI_ABORT); /* read only */
-  if (s) (*env)->ReleasePrimitiveArrayCritical(env, src, s, JNI_ABORT);
-  if (rc != GS_OK) throw_gs(env); /* gs_fold copied the edges before returning */
+  if (!stage_reserve(env, (size_t)n)) return;
+  (*env)->GetLongArrayRegion(env, src, 0, n, (jlong*)t_stage.s);
+  (*env)->GetLongArrayRegion(env, dst, 0, n, (jlong*)t_stage.d);
+  if ((*env)->ExceptionCheck(env)) return;
+  /* outside any critical region: gs_fold may copy, launch and wait */
+  if (gs_fold(H(h), t_stage.s, t_stage.d, (size_t)n) != GS_OK) throw_gs(env);
 }
 
 JNIEXPORT void JNICALL FN(foldParity)(JNIEnv* env, jclass c, jlong h, jlongArray src, jlongArray dst,
@@ -94,16 +123,12 @@ JNIEXPORT void JNICALL FN(foldParity)(JNIEnv* env, jclass c, jlong h, jlongArray
     throw_msg(env, "foldParity: n outside the arrays");
     return;
   }
-  jlong* s = (*env)->GetPrimitiveArrayCritical(env, src, NULL);
-  jlong* d = (*env)->GetPrimitiveArrayCritical(env, dst, NULL);
-  jbyte* w = (*env)->GetPrimitiveArrayCritical(env, par, NULL);
-  const int rc = (s && d && w) ? gs_fold_parity(H(h), (const int64_t*)s, (const int64_t*)d, (const uint8_t*)w,
-                                                (size_t)n)
-                               : GS_ERR_INVALID;
-  if (w) (*env)->ReleasePrimitiveArrayCritical(env, par, w, JNI_ABORT);
-  if (d) (*env)->ReleasePrimitiveArrayCritical(env, dst, d, JNI_ABORT);
-  if (s) (*env)->ReleasePrimitiveArrayCritical(env, src, s, JNI_ABORT);
-  if (rc != GS_OK) throw_gs(env);
+  if (!stage_reserve(env, (size_t)n)) return;
+  (*env)->GetLongArrayRegion(env, src, 0, n, (jlong*)t_stage.s);
+  (*env)->GetLongArrayRegion(env, dst, 0, n, (jlong*)t_stage.d);
+  (*env)->GetByteArrayRegion(env, par, 0, n, (jbyte*)t_stage.w);
+  if ((*env)->ExceptionCheck(env)) return;
+  if (gs_fold_parity(H(h), t_stage.s, t_stage.d, t_stage.w, (size_t)n) != GS_OK) throw_gs(env);
 }
 
 JNIEXPORT void JNICALL FN(combine)(JNIEnv* env, jclass c, jlong dst, jlong src) {

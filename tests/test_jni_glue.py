@@ -61,3 +61,28 @@ def test_java_sources_are_complete():
         assert text.count("{") == text.count("}"), fn
     for cls in ("GpuDisjointSet", "GpuCandidates", "LazyMatches", "HandlePool", "GpuSummarySerializer", "GsNative"):
         assert os.path.exists(os.path.join(PKG, cls + ".java")), cls
+
+
+def test_summaries_survive_java_serialization_by_construction():
+    """the handle is taken at the first use (no HandlePool.acquire in
+    a constructor: the job client needs no GPU), both summaries carry writeObject /
+    readObject, and the operators release the input their combine drops. The behaviour
+    itself is modelled and tested on the C++ host mirror (test_java_serialization)."""
+    for cls, pool in (("GpuDisjointSet", "CC"), ("GpuCandidates", "SIGNED")):
+        text = _read(os.path.join(PKG, cls + ".java"))
+        assert "private void writeObject(ObjectOutputStream out)" in text, cls
+        assert "private void readObject(ObjectInputStream in)" in text, cls
+        ctors = re.findall(r"public %s\([^)]*\)[^{]*\{(.*?)\n\t\}" % cls, text, flags=re.S)
+        assert ctors and not any("acquire" in c for c in ctors), cls
+        assert text.count("HandlePool.%s.acquire()" % pool) == 1, cls  # in handle() only
+    for op in ("GpuConnectedComponents", "GpuBipartitenessCheck"):
+        text = _read(os.path.join(PKG, op + ".java"))
+        assert ".release();" in text and "extends SummaryBulkAggregation" in text, op
+
+
+def test_jni_fold_outside_critical_regions():
+    """gs_fold may copy, launch and wait; JNI forbids that inside a
+    Get*ArrayCritical region. The glue copies with Get<T>ArrayRegion instead."""
+    c = re.sub(r"/\*.*?\*/", "", _read(JNI), flags=re.S)
+    assert "GetPrimitiveArrayCritical" not in c
+    assert "GetLongArrayRegion" in c and "GetByteArrayRegion" in c

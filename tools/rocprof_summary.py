@@ -10,7 +10,7 @@ tallies each 128-B request at 64 B (MI355X_MICROARCH.md HBM section: x2), and th
 counters count Infinity-Cache hits too -- so the figure is what the L2 asks of the
 fabric, an upper bound of HBM bytes, not HBM bytes.
 For ingest, the SQ pass gives VALU and LDS activity and LDS bank conflicts.
-Usage: python tools/rocprof_summary.py <dir> <tag> <pipeline> [batch] [--workload rmat-cc|bip|ingest]
+Usage: python tools/rocprof_summary.py <dir> <tag> <pipeline> [batch] [--workload rmat-cc|rmat20|bip|ingest]
 """
 import glob
 import json
@@ -28,7 +28,7 @@ if "--workload" in argv:
 d, tag = argv[0], argv[1]
 pipeline = int(argv[2]) if len(argv) > 2 else 3
 batch = int(argv[3]) if len(argv) > 3 else 1 << 20
-DOMINANT = {"rmat-cc": "k_fold", "bip": "k_fold", "ingest": "k_parse"}[workload]
+DOMINANT = {"rmat-cc": "k_fold", "rmat20": "k_fold", "bip": "k_fold", "ingest": "k_parse"}[workload]
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out = {"tag": tag, "pipeline": pipeline, "kernels": {}}
 
@@ -118,6 +118,7 @@ with open(os.path.join(root, "profiles", "%s_rocprof_summary.json" % tag), "w") 
     json.dump(out, f, indent=1)
 # per-launch traffic of the workload's dominant kernel, read by bench.py (roofline.traffic)
 TARGET = {"rmat-cc": ("k_fold<false, false, false>", "rmat26-cc-stream", "pmc_fold_traffic.json"),  # <SIGNED, TRACK, TAKE>
+          "rmat20": ("k_fold<false, false, false>", "rmat20-cc-stream", "pmc_r20_traffic.json"),  # config 2
           "bip": ("k_fold<true, false, false>", "bip-config4", "pmc_bip_traffic.json"),
           "ingest": ("k_parse", "ingest-rmat26-text", "pmc_ingest_traffic.json")}[workload]
 kname, wname, fname = TARGET
@@ -145,7 +146,7 @@ if "derived" in r and r["derived"].get("read_requests"):
                   "(MI355X_MICROARCH.md HBM section: x2); writes = WRITE_SIZE (KiB)",
         "source": "profiles/%s_rocprof_summary.json" % tag,
     }
-    if workload in ("rmat-cc", "bip"):
+    if workload in ("rmat-cc", "rmat20", "bip"):
         traffic["read_requests_per_edge"] = round(dv["read_requests"] / batch, 3)
     if "derived_sq" in r:
         traffic["sq"] = r["derived_sq"]
