@@ -96,6 +96,7 @@ def _traffic_fields(pm, launches, step_s):
 KNOWN_DIGESTS = {
     "rmat26-ef16-seed0x5eed0026": 0x961EBDC5F302C813,  # config 3 (r04a: N = 1 and the 1-rank exchange path)
     "bip-config4-clean": 0x5648FC1682105E51,           # config 4, clean stream, first-appearance ids (r04a)
+    "rmat20-ef16-seed0x5eed0020": 0xDF58644480272C13,  # config 2 (r04b)
 }
 
 
@@ -811,6 +812,13 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if args.profile_only:  # profiling / tracing run: the timed steps only
+        if isinstance(xch, NativeExchange):
+            xch.g.close()
+        summ.close()
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return
     total_edges = E * args.steps
     value = total_edges / elapsed
     labelled = nlabels[0]

@@ -580,7 +580,11 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       h->rep_pending_edges += cu;
       // off the handle stream a report is not a gap between folds: report every chunk
       // while the bound is near the load limit (small tables), so no fold has to wait
-      const bool tight = rs != 0 && (double)(h->nv_ub + 4ull * gs_summary::kRepEvery * c) > kMaxLoad * (double)h->cap;
+      // A counted replay (the row count lives on the device) charges its full capacity:
+      // it reports at once, so the bound drops to the real count as soon as it lands
+      // instead of carrying kRepEvery replays' worth of phantom vertices.
+      const bool tight = (rs != 0 && (double)(h->nv_ub + 4ull * gs_summary::kRepEvery * c) > kMaxLoad * (double)h->cap) ||
+                         fs.n_dev != nullptr;
       // (a fused take is waited for: its caller takes the exact count instead)
       if (!fs.take_out && (++h->rep_skip[rs] >= gs_summary::kRepEvery || tight)) {
         const uint64_t claim = h->rep_pending[rs];
@@ -1069,9 +1073,10 @@ int gs_bip_status(gs_handle h, int* ok) {
   if (!ok) return fail(GS_ERR_INVALID, "ok is null");
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
-  uint32_t f = 0;
-  GS_HIP(hipMemcpyAsync(&f, h->ctr + gs::ctr_index(gs::CTR_FAIL), 4, hipMemcpyDeviceToHost, h->stream));
-  GS_HIP(hipStreamSynchronize(h->stream));
+  // the verdict handed to the host with the completion word (k_signal): no device-to-host
+  // copy and no hipStreamSynchronize wake-up (config 4 reads it at the end of every step)
+  uint64_t f = 0;
+  if (int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_FAIL), &f, 1, 0)) return rc;
   *ok = f ? 0 : 1;
   return GS_OK;
 }

@@ -45,6 +45,14 @@ constexpr uint64_t kFailBit = 1ull << 62;  // exchange count word: the sender's 
 #define GS_DELTA_SETS 4
 #endif
 constexpr int kDeltaSets = GS_DELTA_SETS;
+// experiment switches (make variant VFLAGS=...): hook's first CAS on a root the thread
+// just inserted skips the re-read; throughput folds re-read an EMPTY slot before the key CAS
+#ifndef GS_FRESH_HOOK_SKIP
+#define GS_FRESH_HOOK_SKIP 1
+#endif
+#ifndef GS_INSERT_TTAS
+#define GS_INSERT_TTAS 1
+#endif
 enum CounterBlock : int {
   CTR_NV = 0,                    // [kShards] new-vertex counts (= vertex-list fill per shard)
   CTR_DELTA = kShards,           // [kDeltaSets][kShards] delta-record counts
@@ -397,10 +405,16 @@ __device__ __forceinline__ void append_record(const Table& t, const Delta& D, in
 // agent-scope loads; before its CAS the loop re-reads the target root's link
 // (test-and-test-and-set): a root a concurrent hook already moved -- the hub root
 // while a giant component forms -- is followed without queueing a CAS on its address.
+// fresh0 / fresh1: slots this thread has just inserted (kNoSlot: none). A root this
+// thread created itself is not a hub other lanes queue on: its first CAS goes out without
+// the re-read (one dependent round trip less for every edge that hooks a new vertex --
+// the young table's windows of config 5 and the first micro-batches of configs 2 and 4).
 template <bool SIGNED, bool TRACK, bool TAKE = false>
 __device__ __forceinline__ void hook(const Table& t, const Delta& D, int shard, uint32_t a, uint32_t la, int64_t ka,
-                                     uint32_t b, uint32_t lb, int64_t kb, uint32_t need) {
+                                     uint32_t b, uint32_t lb, int64_t kb, uint32_t need, uint32_t fresh0 = kNoSlot,
+                                     uint32_t fresh1 = kNoSlot) {
   GS_DBG(CTR_DBG_HOOKS);
+  bool first = true;
   while (true) {
     GS_DBG(CTR_DBG_ITERS);
     uint32_t pa = 0, pb = 0;
@@ -417,7 +431,9 @@ __device__ __forceinline__ void hook(const Table& t, const Delta& D, int shard, 
     const uint32_t lo = a_lo ? a : b;
     const uint32_t expect = hi << 1;
     const uint32_t desired = (lo << 1) | (SIGNED ? (need & 1u) : 0u);
-    const uint32_t seen = load_link_fresh(t.tab + hi);
+    const bool own = GS_FRESH_HOOK_SKIP && first && (hi == fresh0 || hi == fresh1);
+    first = false;
+    const uint32_t seen = own ? expect : load_link_fresh(t.tab + hi);
     const uint32_t old = seen == expect ? atomicCAS(&t.tab[hi].link, expect, desired) : seen;
     if (old == expect) {
       if (TRACK) append_record<TAKE>(t, D, shard, a_lo ? kb : ka, a_lo ? ka : kb, (int64_t)(SIGNED ? (need & 1u) : 0u));

@@ -355,11 +355,14 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   int64_t kru = 0, krv = 0;
   bool act = false;
   NewVertices nvx;
+  uint32_t fresh0 = kNoSlot, fresh1 = kNoSlot;  // slots this thread inserted
   if (valid) {
     bool nu, nv;
-    const uint32_t su = lookup_resolve<!TAKE>(t, ks, hu, k0u, l0u, lu, nu);
-    const uint32_t sv = lookup_resolve<!TAKE>(t, kd, hv, k0v, l0v, lv, nv);
+    const uint32_t su = lookup_resolve<!TAKE && GS_INSERT_TTAS>(t, ks, hu, k0u, l0u, lu, nu);
+    const uint32_t sv = lookup_resolve<!TAKE && GS_INSERT_TTAS>(t, kd, hv, k0v, l0v, lv, nv);
     nvx = reserve_new_vertices(t, shard, nu, su, nv, sv);  // ids written after the hook
+    if (nu) fresh0 = su;
+    if (nv) fresh1 = sv;
     if (dbg) atomicAdd(&dbg[1], (nu ? 1u : 0u) + ((nv && sv != su) ? 1u : 0u));
     // Delta: a new vertex with an edge to another vertex is always named by a hook
     // record (as the hooked root or as the new parent: its singleton tree can only
@@ -390,7 +393,7 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
     }
   }
   if (__popcll(__ballot(act)) >= 2) combine_hooks(act, ru, kru, rv, krv, need, kCombineRounds);  // wave-uniform
-  if (act) hook<SIGNED, TRACK, TAKE>(t, D, shard, ru, ru << 1, kru, rv, rv << 1, krv, need);
+  if (act) hook<SIGNED, TRACK, TAKE>(t, D, shard, ru, ru << 1, kru, rv, rv << 1, krv, need, fresh0, fresh1);
   write_new_vertices(t, shard, nvx);
   if (dbg) {
     if (valid) atomicAdd(&dbg[0], 1u);

@@ -13,7 +13,7 @@ mkdir -p $O
 cd $R
 bash tools/rocprof_round.sh $TAG || exit 1
 python3 tools/rocprof_summary.py gpurun_out/rocprof_$TAG $TAG 3 || exit 1
-bash tools/rocprof_round.sh ${TAG}_r20 --scale 20 || exit 1
+bash tools/rocprof_round.sh ${TAG}_r20 --scale 20 --warmup 1 || exit 1
 python3 tools/rocprof_summary.py gpurun_out/rocprof_${TAG}_r20 ${TAG}_r20 3 --workload rmat20 || exit 1
 bash tools/pmc_workload.sh ${TAG}_bip bip || exit 1
 python3 tools/rocprof_summary.py gpurun_out/rocprof_${TAG}_bip ${TAG}_bip 3 --workload bip || exit 1

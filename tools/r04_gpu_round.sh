@@ -15,3 +15,8 @@ python3 $R/tools/step_dispatches.py "$DB" 1.2 > $O/bip_dispatches.txt
 python3 $R/tools/timeline.py "$DB" 0 > $O/bip_timeline.txt
 rm -rf /tmp/bip_$TAG
 echo "bip trace ok"
+timeout -k 10 240 rocprofv3 --kernel-trace -d /tmp/r20_$TAG -o run -- python3 $R/bench.py --scale 20 --steps 3 --warmup 1 --profile-only --no-profile-pass --no-cpu-baseline > $O/r20_trace.log 2>&1 || { echo "r20 trace failed rc=$?"; exit 1; }
+DB=$(find /tmp/r20_$TAG -name "*.db" | head -1)
+python3 $R/tools/step_dispatches.py "$DB" 0.8 > $O/r20_dispatches.txt
+rm -rf /tmp/r20_$TAG
+echo "r20 trace ok"

@@ -9,7 +9,7 @@ TAG=${1:-r02}; shift || true
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/rocprof_$TAG
 mkdir -p $OUT
-ARGS="--steps 1 --warmup 0 --no-cpu-baseline --no-profile-pass $*"
+ARGS="--steps 1 --warmup 0 --no-cpu-baseline --no-profile-pass --profile-only $*"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- python3 $R/bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
 echo "trace ok"

@@ -87,6 +87,12 @@ def main():
               (lw, n, len(t), int(np.median(t[:, 6])), np.percentile(host, 50), np.percentile(host, 99)))
         for kx, v in ph.items():
             print("   %-13s p50 %6.2f  p90 %6.2f us" % (kx, np.percentile(v, 50), np.percentile(v, 90)))
+        if len(t) > 128:  # young table (the first 64 windows insert most endpoints) vs the rest
+            for nm, sl in (("windows 0-63", slice(0, 64)), ("windows 64-", slice(64, None))):
+                print("   %s: host p50 %.2f p99 %.2f | " % (nm, np.percentile(host[-m:][sl], 50),
+                                                         np.percentile(host[-m:][sl], 99)) +
+                      "  ".join("%s %.2f" % (kx, np.percentile(v[-m:][sl], 50)) for kx, v in ph.items()
+                                if kx != "host-device"))
         # per-block fold times over all blocks of the measured pass
         c = np.cumsum(hist)
         q = lambda f: 0.5 * (int(np.searchsorted(c, f * c[-1])) + 0.5)  # noqa: E731
