@@ -21,12 +21,18 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
+#include <cstring>
 
 #include "gs_ingest.h"
 #include "gs_ingest.hpp"
 
 namespace gs {
+
+#ifndef GS_PARSE_BRANCHLESS
+#define GS_PARSE_BRANCHLESS 1
+#endif
 
 constexpr uint32_t kTile = 16384;  // bytes per parse block (64 per thread in the start scan)
 constexpr uint32_t kOver = 512;    // bytes of the next tile staged for lines crossing the end
@@ -37,9 +43,10 @@ __device__ __forceinline__ bool is_sep(uint8_t c, int sep) {
 }
 
 __global__ __launch_bounds__(256) void k_count_lines(const uint8_t* __restrict__ text, uint64_t len,
-                                                     uint64_t* __restrict__ tile_cnt, bool aligned) {
+                                                     uint64_t* __restrict__ tile_cnt, bool aligned, uint64_t tile0) {
   __shared__ uint32_t wsum[4];
-  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  const uint64_t tile = tile0 + blockIdx.x;
+  const uint64_t t0 = tile * kTile;
   uint32_t c = 0;
 #pragma unroll
   for (uint32_t h = 0; h < kTile / 4096; ++h) {  // 16 B per thread per 4 KiB slice: coalesced
@@ -60,8 +67,9 @@ __global__ __launch_bounds__(256) void k_count_lines(const uint8_t* __restrict__
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
   __syncthreads();
-  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = (uint64_t)wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  if (threadIdx.x == 0) tile_cnt[tile] = (uint64_t)wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
+
 
 constexpr uint32_t kLds0 = 32;  // LDS offset of byte t0 (byte t0 - 1 sits at kLds0 - 1; the SWAR
                                 // windows of a line may read up to 27 bytes before it)
@@ -168,6 +176,52 @@ __device__ __forceinline__ bool sep_byte(uint32_t c) {
   return SEP == GS_SEP_TAB ? c == '\t' : (c == ' ' || (c - 9u) <= 4u);
 }
 
+// Branch-free form of digits_value and parse_line_swar (GS_PARSE_BRANCHLESS): every
+// window and both values are computed and the verdict selected at the end, so a wave
+// runs one straight path per line instead of exec-mask juggling around early returns
+// (k_parse issued ~270 scalar instructions per wave; profiles/r04_ingest_stalls.txt).
+// Out-of-range windows stay inside the staged LDS (fields clamped to 1..23 digits).
+__device__ __forceinline__ bool digits_value_bf(const uint8_t* L, int end, int n, bool neg, int64_t& out) {
+  uint32_t w[6];
+  lds_win24(L, end - 24, w);
+  uint32_t g[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int v = 24 - n - 4 * k;
+    const uint32_t keep = v <= 0 ? 0xFFFFFFFFu : (v >= 4 ? 0u : (0xFFFFFFFFu << (8 * v)));
+    const uint32_t x = ((w[k] & keep) | (0x30303030u & ~keep)) - 0x30303030u;
+    const uint32_t t = (x << 3) + (x << 1) + (x >> 8);
+    g[k] = (t & 0xFFu) * 100u + ((t >> 16) & 0xFFu);
+  }
+  const uint32_t hi = g[0] * 10000u + g[1];
+  const uint64_t v = (uint64_t)hi * 10000000000000000ull + ((uint64_t)(g[2] * 10000u + g[3]) * 100000000ull +
+                                                            (uint64_t)(g[4] * 10000u + g[5]));
+  out = neg ? (int64_t)(0ull - v) : (int64_t)v;
+  return hi <= 922u && v <= (neg ? (1ull << 63) : (1ull << 63) - 1);
+}
+
+template <int SEP>
+__device__ __forceinline__ int parse_line_swar_bf(const uint8_t* L, int s, int e, int64_t& a, int64_t& b) {
+  e = (e > s && L[e - 1] == '\r') ? e - 1 : e;  // a '\r' right before the line end is dropped
+  uint32_t w[6];
+  lds_win24(L, s, w);
+  const uint32_t c0 = w[0] & 0xFFu;
+  const bool sg0 = c0 == '+' || c0 == '-';
+  const int f0 = first_nondigit(w, sg0);
+  const int p1 = s + min(f0, 23), n0 = f0 - (sg0 ? 1 : 0);
+  const bool ok0 = n0 > 0 && p1 < e && sep_byte<SEP>(L[p1]);
+  const int q = p1 + 1;
+  lds_win24(L, q, w);
+  const uint32_t c1 = w[0] & 0xFFu;
+  const bool sg1 = q < e && (c1 == '+' || c1 == '-');
+  const int f1 = first_nondigit(w, sg1);
+  const int p2 = max(q + 1, min(q + f1, e)), n1 = min(q + f1, e) - q - (sg1 ? 1 : 0);
+  const bool ok1 = n1 > 0 && (q + f1 >= e || sep_byte<SEP>(L[q + min(f1, 23)]));
+  const bool va = digits_value_bf(L, p1, min(max(n0, 1), 23), c0 == '-', a);
+  const bool vb = digits_value_bf(L, p2, min(max(n1, 1), 23), sg1 && c1 == '-', b);
+  return f0 >= 24 ? -1 : (!ok0 ? 0 : (f1 >= 24 ? -1 : ((ok1 && va && vb) ? 1 : 0)));
+}
+
 template <int SEP>
 __device__ __forceinline__ int parse_line_swar(const uint8_t* L, int s, int e, int64_t& a, int64_t& b) {
   if (e > s && L[e - 1] == '\r') --e;  // a '\r' right before the line end is dropped
@@ -228,17 +282,99 @@ __device__ __forceinline__ uint32_t chunk_nl_mask(const uint8_t* L, uint32_t c, 
   return nl;
 }
 
+template <bool FUSED>
 __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                            const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                            int64_t* __restrict__ dst, uint64_t cap,
-                                           unsigned long long* __restrict__ bad, bool aligned, uint64_t tile);
+                                           unsigned long long* __restrict__ bad, bool aligned, uint64_t tile,
+                                           unsigned long long* __restrict__ status);
+
+// Single pass (GS_PARSE_FUSED, default): no k_count_lines pass and no scan. Every block
+// counts its tile's '\n' from the masks it builds anyway and finds the count before its
+// tile by a decoupled look-back over per-tile status words (status[t]: bit 63 = the
+// inclusive count through tile t is final, bit 62 = tile t's own count is, value in bits
+// 0..61): wave 0 reads the 64 nearest predecessors' words in one round, sums own counts
+// back to the nearest final prefix, publishes its own. A block only waits for lower
+// tiles, which are dispatched before it on their XCD; should a wait ever outlast ~50 ms,
+// the block counts the '\n' before its tile itself (no deadlock either way). The text
+// is read once instead of twice (the count pass was 126 us of a 684 MB parse).
+
+constexpr unsigned long long kStP = 1ull << 63, kStA = 1ull << 62, kStVal = (1ull << 62) - 1;
+
+// Wave 0 of tile `tile`: '\n' before the tile (decoupled look-back over 64 predecessors
+// per round); publishes the tile's inclusive count. agg = the tile's own '\n' count.
+// Between unsuccessful rounds the wave backs off (s_sleep 8 -> 64): every waiting wave
+// re-reading 64 status words at once slowed the other blocks' staging loads.
+__device__ __forceinline__ unsigned long long look_back(const uint8_t* __restrict__ text, unsigned long long* status,
+                                                        uint64_t tile, unsigned long long agg) {
+  const int lane = threadIdx.x & 63;
+  if (tile == 0) {
+    if (lane == 0) __hip_atomic_store(status, kStP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0) __hip_atomic_store(status + tile, kStA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long excl = 0;
+  int64_t base = (int64_t)tile - 1;
+  const unsigned long long t_start = wall_clock64();
+  int backoff = 0;
+  for (;;) {
+    const int64_t ti = base - lane;  // lane 0: the nearest predecessor
+    const unsigned long long w =
+        ti >= 0 ? __hip_atomic_load(status + ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kStP;
+    const unsigned long long pm = __ballot((w & kStP) != 0), am = __ballot((w & (kStP | kStA)) != 0);
+    const int j = pm ? __ffsll((long long)pm) - 1 : 64;  // nearest final prefix in this window
+    const unsigned long long need = j >= 64 ? ~0ull : ((2ull << j) - 1ull);  // lanes 0..j
+    if ((am & need) == need) {
+      unsigned long long v = lane <= j ? (w & kStVal) : 0ull;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+      excl += v;
+      if (j < 64) break;
+      base -= 64;  // the whole window was own counts: continue further back
+      continue;
+    }
+    if (wall_clock64() - t_start > 5000000ull) {  // ~50 ms (100 MHz clock): count it directly
+      unsigned long long c = 0;
+      const uint64_t end = tile * kTile;
+      for (uint64_t q = (uint64_t)lane; q < end; q += 64) c += text[q] == '\n';
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+      excl = c;
+      break;
+    }
+    if (backoff < 3) {
+      __builtin_amdgcn_s_sleep(8);
+    } else {
+      __builtin_amdgcn_s_sleep(64);
+    }
+    ++backoff;
+  }
+  if (lane == 0) __hip_atomic_store(status + tile, kStP | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
+__global__ __launch_bounds__(256) void k_parse_fused(const uint8_t* __restrict__ text, uint64_t len, int sep,
+                                                     int64_t* __restrict__ src, int64_t* __restrict__ dst, uint64_t cap,
+                                                     unsigned long long* __restrict__ bad, bool aligned,
+                                                     unsigned long long* __restrict__ status, uint64_t tiles,
+                                                     bool ticket) {
+  // ticket: tiles are numbered in the order blocks START (status[tiles] counts them), so
+  // every predecessor of a tile is already running when it looks back; blockIdx order
+  // lets a tile wait on a predecessor its XCD has not dispatched yet
+  __shared__ uint64_t tile_sh;
+  if (ticket) {
+    if (threadIdx.x == 0) tile_sh = atomicAdd(reinterpret_cast<unsigned long long*>(status + tiles), 1ull);
+    __syncthreads();
+  }
+  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, ticket ? tile_sh : blockIdx.x, status);
+}
 
 // One tile per block (44 VGPRs, 8 blocks per CU).
 __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                                const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                                int64_t* __restrict__ dst, uint64_t cap,
-                                               unsigned long long* __restrict__ bad, bool aligned) {
-  parse_tile(text, len, sep, tile_pre, src, dst, cap, bad, aligned, blockIdx.x);
+                                               unsigned long long* __restrict__ bad, bool aligned, uint64_t tile0) {
+  parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile0 + blockIdx.x, nullptr);
 }
 
 // Experiment (GS_PARSE_TPB > 1): each block parses `tpb` consecutive tiles, one after
@@ -252,15 +388,17 @@ __global__ __launch_bounds__(256) void k_parse_multi(const uint8_t* __restrict__
   const uint64_t first = (uint64_t)blockIdx.x * tpb;
   const uint64_t last = min(tiles, first + tpb);
   for (uint64_t tile = first; tile < last; ++tile) {
-    parse_tile(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile);
+    parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile, nullptr);
     __syncthreads();  // the next tile restages the LDS
   }
 }
 
+template <bool FUSED>
 __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                            const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                            int64_t* __restrict__ dst, uint64_t cap,
-                                           unsigned long long* __restrict__ bad, bool aligned, uint64_t tile) {
+                                           unsigned long long* __restrict__ bad, bool aligned, uint64_t tile,
+                                           unsigned long long* __restrict__ status) {
   constexpr uint32_t kSeg = kTile / 256;  // bytes per thread in the line-start scan
   constexpr uint32_t kExtra = 2;          // '\n' masks past the tile: lines that cross its end
   constexpr uint32_t kSlots = (kTile + kOver + 4095) / 4096;
@@ -269,6 +407,7 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
   __shared__ __align__(16) uint8_t lds[kLds0 + kTile + kOver];
   __shared__ uint64_t nlm[256 + kExtra];
   __shared__ uint32_t wsum[4];
+  __shared__ uint32_t wnl[4];
   const uint64_t t0 = tile * kTile;
   const uint64_t staged_end = min(len, t0 + kTile + kOver);
   // stage [t0, staged_end) at lds[kLds0..] with 16-B stores; lds[kLds0 - 1] = byte t0 - 1.
@@ -327,22 +466,34 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
     if (lane >= o) x += y;
   }
   if (lane == 63) wsum[wid] = x;
+  if (FUSED) {  // the tile's own '\n' (its bytes only): the look-back's aggregate
+    uint32_t cn = __popcll(valid >= 64 ? nl : (nl & ((1ull << valid) - 1ull)));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) cn += __shfl_xor(cn, o, 64);
+    if (lane == 0) wnl[wid] = cn;
+  }
   __syncthreads();
   uint32_t wbase = 0;
   for (int q = 0; q < 4; ++q)
     if (q < wid) wbase += wsum[q];
   // (2) each thread parses the lines that start in its segment; the k-th start of the
   //     tile follows k '\n' of the tile if a line starts at t0, else k + 1
-  uint64_t line = tile_pre[tile] + (L[-1] == '\n' ? 0u : 1u) + wbase + (x - c);
+  const uint64_t line_off = (L[-1] == '\n' ? 0u : 1u) + wbase + (x - c);  // within the text after the tile's prefix
   const LineBuf b{lds, text, t0, len, staged_end};
-  while (mine) {
-    const uint32_t j = __ffsll((unsigned long long)mine) - 1;
-    mine &= mine - 1;
+#if GS_PARSE_BRANCHLESS
+  const uint64_t nx1 = nlm[threadIdx.x + 1], nx2 = nlm[threadIdx.x + 2];  // the next two segments' '\n' masks
+#endif
+  // one line starting at segment byte j: (a, d) and whether it is well formed
+  auto parse_at = [&](uint32_t j, int64_t& a, int64_t& d) -> bool {
     const int so = (int)(seg + j);
     // the line's '\n': the first one at or after its start, within this segment or
     // the next two (longer lines take the per-character path)
     int e = -1;
     const uint64_t own = nl & (~0ull << j);
+#if GS_PARSE_BRANCHLESS
+    e = own ? (int)seg + __builtin_ctzll(own)
+            : (nx1 ? (int)seg + 64 + __builtin_ctzll(nx1) : (nx2 ? (int)seg + 128 + __builtin_ctzll(nx2) : -1));
+#else
     if (own) {
       e = (int)seg + __builtin_ctzll(own);
     } else {
@@ -354,12 +505,21 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
         if (n2) e = (int)seg + 128 + __builtin_ctzll(n2);
       }
     }
+#endif
     uint64_t q = t0 + (uint64_t)so;
-    int64_t a = 0, d = 0;
+    a = 0;
+    d = 0;
     int r = -1;
+#if GS_PARSE_BRANCHLESS
+    const int ee = e >= 0 ? e : so + 1;  // (no '\n' in reach: the result is discarded, r = -1)
+    r = sep == GS_SEP_TAB ? parse_line_swar_bf<GS_SEP_TAB>(L, so, ee, a, d)
+                          : parse_line_swar_bf<GS_SEP_WHITESPACE>(L, so, ee, a, d);
+    if (e < 0) r = -1;
+#else
     if (e >= 0)
       r = sep == GS_SEP_TAB ? parse_line_swar<GS_SEP_TAB>(L, so, e, a, d)
                             : parse_line_swar<GS_SEP_WHITESPACE>(L, so, e, a, d);
+#endif
     bool ok = r == 1;
     if (r < 0) {  // a long line or field: one byte per step
       // two fields: the first must end at a separator (else fields[1] does not exist)
@@ -369,33 +529,104 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
         ok = parse_long(b, q, sep, d) != kFieldBad;
       }
     }
+    return ok;
+  };
+  auto emit = [&](uint64_t line, bool ok, int64_t a, int64_t d) {
     if (!ok) {
       atomicMin(bad, (unsigned long long)line);
     } else if (line < cap) {
       src[line] = a;
       dst[line] = d;
     }
+  };
+  uint64_t line;
+  if (FUSED) {
+    // a thread's first two lines (nearly always all of them) are parsed into registers
+    // BEFORE the look-back, so that the predecessors' counts are published by the time
+    // wave 0 reads them, and only the stores wait for the tile's line numbers
+    int64_t a0 = 0, d0 = 0, a1 = 0, d1 = 0;
+    bool ok0 = true, ok1 = true;
+    uint32_t k = 0;
+    if (mine) {
+      const uint32_t j = __ffsll((unsigned long long)mine) - 1;
+      mine &= mine - 1;
+      ok0 = parse_at(j, a0, d0);
+      k = 1;
+    }
+    if (mine) {
+      const uint32_t j = __ffsll((unsigned long long)mine) - 1;
+      mine &= mine - 1;
+      ok1 = parse_at(j, a1, d1);
+      k = 2;
+    }
+    __shared__ unsigned long long pre_sh;
+    if (wid == 0) {
+      const unsigned long long e = look_back(text, status, tile, (unsigned long long)wnl[0] + wnl[1] + wnl[2] + wnl[3]);
+      if (lane == 0) pre_sh = e;
+    }
+    __syncthreads();
+    line = pre_sh + line_off;
+    if (k >= 1) emit(line, ok0, a0, d0);
+    if (k >= 2) emit(line + 1, ok1, a1, d1);
+    line += k;
+  } else {
+    line = tile_pre[tile] + line_off;
+  }
+  while (mine) {
+    const uint32_t j = __ffsll((unsigned long long)mine) - 1;
+    mine &= mine - 1;
+    int64_t a, d;
+    const bool ok = parse_at(j, a, d);
+    emit(line, ok, a, d);
     ++line;
   }
 }
 
-// {line count, first malformed line (~0: none)} of a parsed text
+// {line count, first malformed line (~0: none)} of a parsed text; with `host` (mapped
+// memory) also host[1..2] = the same two words and then host[0] = seq (system-scope
+// release): the caller spins on that word instead of a copy and a stream synchronisation
 __global__ void k_parse_result(const uint64_t* tile_pre, const uint64_t* tile_cnt, uint64_t tiles,
-                               const uint8_t* text, uint64_t len, const unsigned long long* bad, uint64_t* res) {
+                               const uint8_t* text, uint64_t len, const unsigned long long* bad, uint64_t* res,
+                               unsigned long long* host, unsigned long long seq, const unsigned long long* status) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  res[0] = tile_pre[tiles - 1] + tile_cnt[tiles - 1] + (text[len - 1] != '\n' ? 1u : 0u);  // a last line may lack '\n'
-  res[1] = *bad;
+  // '\n' through the last tile (fused: its status word), + 1: a last line may lack '\n'
+  const uint64_t nl = status ? (status[tiles - 1] & kStVal) : tile_pre[tiles - 1] + tile_cnt[tiles - 1];
+  const uint64_t lines = nl + (text[len - 1] != '\n' ? 1u : 0u);
+  const uint64_t b = *bad;
+  res[0] = lines;
+  res[1] = b;
+  if (host) {
+    __hip_atomic_store(host + 1, (unsigned long long)lines, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host + 2, (unsigned long long)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, int64_t* src, int64_t* dst, size_t cap,
-                       ParseScratch& s) {
+                       ParseScratch& s, unsigned long long* host_res, unsigned long long seq, bool fused) {
   if (len == 0) return hipMemsetAsync(s.res, 0xFF, 16, st) == hipSuccess &&
                         hipMemsetAsync(s.res, 0, 8, st) == hipSuccess ? 0 : -1;
   const uint64_t tiles = (len + kTile - 1) / kTile;
   if (tiles > s.tiles_cap) return -1;
   const bool aligned = ((uintptr_t)text & 15u) == 0;
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
-  hipLaunchKernelGGL(k_count_lines, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, s.tile_cnt, aligned);
+  if (fused) {  // status words (s.tile_cnt) zeroed, then one pass
+    if (tiles + 1 > s.tiles_cap) return -1;
+    if (hipMemsetAsync(s.tile_cnt, 0, (tiles + 1) * 8, st) != hipSuccess ||
+        hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess)
+      return -1;
+    static const bool ticket = [] {
+      const char* e = getenv("GS_PARSE_TICKET");  // experiment knob: 0 = tiles in blockIdx order
+      return !(e && atoi(e) == 0);
+    }();
+    hipLaunchKernelGGL(k_parse_fused, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, src, dst,
+                       (uint64_t)cap, s.bad, aligned, reinterpret_cast<unsigned long long*>(s.tile_cnt), tiles, ticket);
+    hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
+                       s.bad, s.res, host_res, seq, reinterpret_cast<const unsigned long long*>(s.tile_cnt));
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+  hipLaunchKernelGGL(k_count_lines, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, s.tile_cnt, aligned,
+                     (uint64_t)0);
   size_t tmp = s.cub_bytes;
   if (hipcub::DeviceScan::ExclusiveSum(s.cub_tmp, tmp, s.tile_cnt, s.tile_pre, (int)tiles, st) != hipSuccess)
     return -1;
@@ -409,9 +640,9 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
                        sep, s.tile_pre, src, dst, (uint64_t)cap, s.bad, aligned, tiles, tpb);
   else
     hipLaunchKernelGGL(k_parse, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, s.tile_pre, src, dst,
-                       (uint64_t)cap, s.bad, aligned);
+                       (uint64_t)cap, s.bad, aligned, (uint64_t)0);
   hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
-                     s.bad, s.res);
+                     s.bad, s.res, host_res, seq, nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -419,7 +650,7 @@ int parse_text(hipStream_t st, const char* text, size_t len, int sep, int64_t* s
                ParseScratch& s, uint64_t* n_lines, int64_t* bad_line) {
   *n_lines = 0;
   *bad_line = -1;
-  if (parse_text_enqueue(st, text, len, sep, src, dst, cap, s)) return -1;
+  if (parse_text_enqueue(st, text, len, sep, src, dst, cap, s, nullptr, 0)) return -1;
   uint64_t res[2];
   if (hipMemcpyAsync(res, s.res, 16, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
   if (hipStreamSynchronize(st) != hipSuccess) return -1;
@@ -453,21 +684,81 @@ int parse_scratch_init(ParseScratch& s, void* mem, size_t max_len) {
 
 }  // namespace gs
 
+namespace {
+// Scratch of gs_parse_edges_device kept per thread and device (grown, never shrunk), and
+// a host-mapped result record: a call costs the parse's launches and one spin on host
+// memory, not an allocation, a device-to-host copy and two stream synchronisations
+// (~40 us of a 2^24-line parse; profiles/r04_ingest_ab.txt).
+struct ParseCache {
+  int device = -1;
+  size_t len_cap = 0;
+  void* mem = nullptr;
+  gs::ParseScratch s;
+  unsigned long long* host = nullptr;  // mapped {seq, lines, bad}
+  unsigned long long* host_dev = nullptr;
+  unsigned long long seq = 0;
+};
+thread_local ParseCache t_parse;
+
+int parse_cache_ready(hipStream_t st, size_t len) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  ParseCache& c = t_parse;
+  if (c.device != dev) {  // (a thread moved to another device: the old scratch stays allocated there)
+    c = ParseCache();
+    c.device = dev;
+    if (hipHostMalloc(&c.host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&c.host_dev), c.host, 0) != hipSuccess)
+      return -1;
+    memset(c.host, 0, 64);
+  }
+  if (c.len_cap < len || !c.mem) {
+    if (c.mem) {
+      if (hipStreamSynchronize(st) != hipSuccess) return -1;  // the old scratch's last user
+      (void)hipFree(c.mem);
+      c.mem = nullptr;
+    }
+    const size_t want = std::max<size_t>(len + len / 4, 1u << 20);
+    size_t cub = 0;
+    if (hipMalloc(&c.mem, gs::parse_scratch_bytes(want, &cub)) != hipSuccess) return -1;
+    gs::parse_scratch_init(c.s, c.mem, want);
+    c.len_cap = want;
+  }
+  return 0;
+}
+}  // namespace
+
 extern "C" int gs_parse_edges_device(void* stream, const char* text, size_t len, int sep, int64_t* src, int64_t* dst,
                                      size_t cap, uint64_t* n_lines, int64_t* bad_line) {
   if (!n_lines || !bad_line || (len && !text)) return GS_ERR_INVALID;
   if (sep != GS_SEP_WHITESPACE && sep != GS_SEP_TAB) return GS_ERR_INVALID;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  size_t cub = 0;
-  const size_t bytes = gs::parse_scratch_bytes(len, &cub);
-  void* mem = nullptr;
-  if (hipMallocAsync(&mem, bytes, st) != hipSuccess) return GS_ERR_HIP;
-  gs::ParseScratch s;
-  gs::parse_scratch_init(s, mem, len);
-  const int rc = gs::parse_text(st, text, len, sep, src, dst, cap, s, n_lines, bad_line);
-  (void)hipFreeAsync(mem, st);
-  (void)hipStreamSynchronize(st);
+  *n_lines = 0;
+  *bad_line = -1;
+  if (len == 0) return GS_OK;
+  if (parse_cache_ready(st, len)) return GS_ERR_HIP;
+  ParseCache& c = t_parse;
+  const unsigned long long seq = ++c.seq;
+  static const bool one_pass = [] {  // experiment knob: GS_PARSE_MODE=0 = count pass + scan + parse pass
+    const char* e = getenv("GS_PARSE_MODE");
+    return !(e && atoi(e) == 0);
+  }();
+  const int rc = gs::parse_text_enqueue(st, text, len, sep, src, dst, cap, c.s, c.host_dev, seq, one_pass);
   if (rc) return GS_ERR_HIP;
+  // spin on the mapped record; a long parse hands over to the stream synchronisation
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1; __atomic_load_n(c.host, __ATOMIC_ACQUIRE) != seq; ++i) {
+    if ((i & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) {
+      if (hipStreamSynchronize(st) != hipSuccess) return GS_ERR_HIP;
+      if (__atomic_load_n(c.host, __ATOMIC_ACQUIRE) != seq) return GS_ERR_HIP;
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  if (hipGetLastError() != hipSuccess) return GS_ERR_HIP;
+  *n_lines = __atomic_load_n(c.host + 1, __ATOMIC_ACQUIRE);
+  const unsigned long long b = __atomic_load_n(c.host + 2, __ATOMIC_ACQUIRE);
+  *bad_line = b == ~0ull ? -1 : (int64_t)b;
   if (*bad_line >= 0) return GS_ERR_PARSE;
   if (*n_lines > cap) return GS_ERR_TRUNCATED;
   return GS_OK;

@@ -20,9 +20,12 @@ struct ParseScratch {
 size_t parse_scratch_bytes(size_t max_len, size_t* cub_bytes);
 int parse_scratch_init(ParseScratch& s, void* mem, size_t max_len);
 // Enqueue the parse of device text on st; the result {lines, bad or ~0} lands in s.res
-// (device). Returns 0 or -1 (HIP failure).
+// (device) and, with host_res (mapped), in host_res[1..2] behind host_res[0] = seq.
+// fused: one pass (k_parse_fused, decoupled look-back) instead of count + scan + parse.
+// Returns 0 or -1 (HIP failure).
 int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, int64_t* src, int64_t* dst, size_t cap,
-                       ParseScratch& s);
+                       ParseScratch& s,
+                       unsigned long long* host_res = nullptr, unsigned long long seq = 0, bool fused = false);
 // Parse device text; synchronises st. Returns 0 or -1 (HIP failure).
 int parse_text(hipStream_t st, const char* text, size_t len, int sep, int64_t* src, int64_t* dst, size_t cap,
                ParseScratch& s, uint64_t* n_lines, int64_t* bad_line);
