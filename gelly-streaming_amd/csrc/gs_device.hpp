@@ -50,6 +50,9 @@ constexpr int kDeltaSets = GS_DELTA_SETS;
 #ifndef GS_FRESH_HOOK_SKIP
 #define GS_FRESH_HOOK_SKIP 1
 #endif
+#ifndef GS_WAVE_APPEND
+#define GS_WAVE_APPEND 1  // 0: one append atomic per record (experiment switch)
+#endif
 #ifndef GS_INSERT_TTAS
 #define GS_INSERT_TTAS 1
 #endif
@@ -399,6 +402,31 @@ __device__ __forceinline__ void append_record(const Table& t, const Delta& D, in
   }
 }
 
+// Wave-aggregated append (the tracked folds of a group's exchange): the lanes of a wave
+// holding a record take one range of the shard with ONE atomic and write their rows
+// contiguously (coalesced 24-B rows), instead of one same-address atomic and a scattered
+// row per record. Call in wave-uniform control flow.
+__device__ __forceinline__ void append_record_wave(const Table& t, const Delta& D, int shard, bool has, int64_t a,
+                                                   int64_t b, int64_t w) {
+  const unsigned long long m = __ballot(has);
+  if (!m) return;
+  const int lane = (int)(threadIdx.x & 63u);
+  const int leader = __ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(&t.ctr[ctr_index(D.dctr + shard)], (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (!has) return;
+  const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  if (pos < D.shard_cap) {
+    int64_t* r = D.drec + ((size_t)shard * D.shard_cap + pos) * 3;
+    r[0] = a;
+    r[1] = b;
+    r[2] = w;
+  } else {
+    raise_flag(t, CTR_OVF, 1);
+  }
+}
+
 // Hook loop: make a and b one set with colour(a) ^ colour(b) == need (SIGNED).
 // The larger-key root is hooked under the smaller key, so every root is the
 // minimum id of its tree (the canonical label) at all times. Finds read links with
@@ -409,10 +437,11 @@ __device__ __forceinline__ void append_record(const Table& t, const Delta& D, in
 // thread created itself is not a hub other lanes queue on: its first CAS goes out without
 // the re-read (one dependent round trip less for every edge that hooks a new vertex --
 // the young table's windows of config 5 and the first micro-batches of configs 2 and 4).
-template <bool SIGNED, bool TRACK, bool TAKE = false>
-__device__ __forceinline__ void hook(const Table& t, const Delta& D, int shard, uint32_t a, uint32_t la, int64_t ka,
-                                     uint32_t b, uint32_t lb, int64_t kb, uint32_t need, uint32_t fresh0 = kNoSlot,
-                                     uint32_t fresh1 = kNoSlot) {
+// Returns whether this call's CAS joined two trees; with TRACK the join's record
+// {hi key, lo key, parity} goes to rec (appended by the caller).
+template <bool SIGNED, bool TRACK>
+__device__ __forceinline__ bool hook(const Table& t, uint32_t a, uint32_t la, int64_t ka, uint32_t b, uint32_t lb,
+                                     int64_t kb, uint32_t need, uint32_t fresh0, uint32_t fresh1, int64_t* rec) {
   GS_DBG(CTR_DBG_HOOKS);
   bool first = true;
   while (true) {
@@ -424,7 +453,7 @@ __device__ __forceinline__ void hook(const Table& t, const Delta& D, int shard, 
     need ^= pa ^ pb;
     if (a == b) {
       if (SIGNED && (need & 1u)) atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);
-      return;
+      return false;
     }
     const bool a_lo = ka < kb;
     const uint32_t hi = a_lo ? b : a;
@@ -436,8 +465,12 @@ __device__ __forceinline__ void hook(const Table& t, const Delta& D, int shard, 
     const uint32_t seen = own ? expect : load_link_fresh(t.tab + hi);
     const uint32_t old = seen == expect ? atomicCAS(&t.tab[hi].link, expect, desired) : seen;
     if (old == expect) {
-      if (TRACK) append_record<TAKE>(t, D, shard, a_lo ? kb : ka, a_lo ? ka : kb, (int64_t)(SIGNED ? (need & 1u) : 0u));
-      return;
+      if (TRACK) {
+        rec[0] = a_lo ? kb : ka;
+        rec[1] = a_lo ? ka : kb;
+        rec[2] = (int64_t)(SIGNED ? (need & 1u) : 0u);
+      }
+      return true;
     }
     // hi was hooked meanwhile: continue that side from its live link
     GS_DBG(CTR_DBG_CASFAIL);

@@ -377,22 +377,6 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
   parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile0 + blockIdx.x, nullptr);
 }
 
-// Experiment (GS_PARSE_TPB > 1): each block parses `tpb` consecutive tiles, one after
-// another (LDS reused, no prefetch across tiles). The loop costs registers (88 VGPRs,
-// 5 blocks per CU).
-__global__ __launch_bounds__(256) void k_parse_multi(const uint8_t* __restrict__ text, uint64_t len, int sep,
-                                                     const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
-                                                     int64_t* __restrict__ dst, uint64_t cap,
-                                                     unsigned long long* __restrict__ bad, bool aligned,
-                                                     uint64_t tiles, uint32_t tpb) {
-  const uint64_t first = (uint64_t)blockIdx.x * tpb;
-  const uint64_t last = min(tiles, first + tpb);
-  for (uint64_t tile = first; tile < last; ++tile) {
-    parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile, nullptr);
-    __syncthreads();  // the next tile restages the LDS
-  }
-}
-
 template <bool FUSED>
 __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                            const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
@@ -631,16 +615,8 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
   if (hipcub::DeviceScan::ExclusiveSum(s.cub_tmp, tmp, s.tile_cnt, s.tile_pre, (int)tiles, st) != hipSuccess)
     return -1;
   if (hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess) return -1;
-  static const uint32_t tpb = [] {
-    const char* e = getenv("GS_PARSE_TPB");  // experiment knob: tiles per k_parse block
-    return (uint32_t)(e ? std::max(1, atoi(e)) : 1);
-  }();
-  if (tpb > 1)
-    hipLaunchKernelGGL(k_parse_multi, dim3((unsigned)((tiles + tpb - 1) / tpb)), dim3(256), 0, st, t, (uint64_t)len,
-                       sep, s.tile_pre, src, dst, (uint64_t)cap, s.bad, aligned, tiles, tpb);
-  else
-    hipLaunchKernelGGL(k_parse, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, s.tile_pre, src, dst,
-                       (uint64_t)cap, s.bad, aligned, (uint64_t)0);
+  hipLaunchKernelGGL(k_parse, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, s.tile_pre, src, dst,
+                     (uint64_t)cap, s.bad, aligned, (uint64_t)0);
   hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
                      s.bad, s.res, host_res, seq, nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -1;

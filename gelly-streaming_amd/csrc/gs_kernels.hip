@@ -356,6 +356,8 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   bool act = false;
   NewVertices nvx;
   uint32_t fresh0 = kNoSlot, fresh1 = kNoSlot;  // slots this thread inserted
+  bool has_rec = false;  // TRACK: this edge's record (a self-loop's new vertex, or its hook)
+  int64_t rec[3] = {0, 0, 0};
   if (valid) {
     bool nu, nv;
     const uint32_t su = lookup_resolve<!TAKE && GS_INSERT_TTAS>(t, ks, hu, k0u, l0u, lu, nu);
@@ -368,7 +370,12 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
     // record (as the hooked root or as the new parent: its singleton tree can only
     // change through a CAS on it or onto it), so only a new vertex seen through a
     // self-loop needs a record of its own.
-    if (TRACK && nu && su == sv) append_record<TAKE>(t, D, shard, ks, ks, 0);
+    if (TRACK && nu && su == sv) {
+      has_rec = true;
+      rec[0] = ks;
+      rec[1] = ks;
+      rec[2] = 0;
+    }
     ru = su;
     rv = sv;
     if (su != kNoSlot && sv != kNoSlot && su != sv) {  // a self-loop adds its vertex, never a conflict
@@ -393,7 +400,13 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
     }
   }
   if (__popcll(__ballot(act)) >= 2) combine_hooks(act, ru, kru, rv, krv, need, kCombineRounds);  // wave-uniform
-  if (act) hook<SIGNED, TRACK, TAKE>(t, D, shard, ru, ru << 1, kru, rv, rv << 1, krv, need, fresh0, fresh1);
+  if (act) has_rec = hook<SIGNED, TRACK>(t, ru, ru << 1, kru, rv, rv << 1, krv, need, fresh0, fresh1, rec);
+  if (TRACK) {  // a self-loop is never `act`: at most one record per edge
+    if (!TAKE && GS_WAVE_APPEND)
+      append_record_wave(t, D, shard, has_rec, rec[0], rec[1], rec[2]);
+    else if (has_rec)
+      append_record<TAKE>(t, D, shard, rec[0], rec[1], rec[2]);
+  }
   write_new_vertices(t, shard, nvx);
   if (dbg) {
     if (valid) atomicAdd(&dbg[0], 1u);
