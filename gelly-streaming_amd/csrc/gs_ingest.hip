@@ -356,17 +356,8 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
 __global__ __launch_bounds__(256) void k_parse_fused(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                                      int64_t* __restrict__ src, int64_t* __restrict__ dst, uint64_t cap,
                                                      unsigned long long* __restrict__ bad, bool aligned,
-                                                     unsigned long long* __restrict__ status, uint64_t tiles,
-                                                     bool ticket) {
-  // ticket: tiles are numbered in the order blocks START (status[tiles] counts them), so
-  // every predecessor of a tile is already running when it looks back; blockIdx order
-  // lets a tile wait on a predecessor its XCD has not dispatched yet
-  __shared__ uint64_t tile_sh;
-  if (ticket) {
-    if (threadIdx.x == 0) tile_sh = atomicAdd(reinterpret_cast<unsigned long long*>(status + tiles), 1ull);
-    __syncthreads();
-  }
-  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, ticket ? tile_sh : blockIdx.x, status);
+                                                     unsigned long long* __restrict__ status) {
+  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, blockIdx.x, status);
 }
 
 // One tile per block (44 VGPRs, 8 blocks per CU).
@@ -595,16 +586,10 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
   const bool aligned = ((uintptr_t)text & 15u) == 0;
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
   if (fused) {  // status words (s.tile_cnt) zeroed, then one pass
-    if (tiles + 1 > s.tiles_cap) return -1;
-    if (hipMemsetAsync(s.tile_cnt, 0, (tiles + 1) * 8, st) != hipSuccess ||
-        hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess)
+    if (hipMemsetAsync(s.tile_cnt, 0, tiles * 8, st) != hipSuccess || hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess)
       return -1;
-    static const bool ticket = [] {
-      const char* e = getenv("GS_PARSE_TICKET");  // experiment knob: 0 = tiles in blockIdx order
-      return !(e && atoi(e) == 0);
-    }();
     hipLaunchKernelGGL(k_parse_fused, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, src, dst,
-                       (uint64_t)cap, s.bad, aligned, reinterpret_cast<unsigned long long*>(s.tile_cnt), tiles, ticket);
+                       (uint64_t)cap, s.bad, aligned, reinterpret_cast<unsigned long long*>(s.tile_cnt));
     hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
                        s.bad, s.res, host_res, seq, reinterpret_cast<const unsigned long long*>(s.tile_cnt));
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -767,13 +767,18 @@ __global__ __launch_bounds__(256) void k_digest(Table t, unsigned long long* out
   if ((threadIdx.x & 63u) == 0 && sum) atomicAdd(out, sum);
 }
 
-// Stage the sharded delta list as contiguous records. grid = kShards blocks: block s
-// copies shard s to its prefix position (deterministic, no append atomics); rows
-// past `cap` are dropped (the count says how many there were). Block 0 writes the
-// count word (| kFailBit when with_fail and the verdict failed: the exchange carries
-// the verdict, Candidates.merge :79-81); the last block resets the shard counters.
-__global__ __launch_bounds__(256) void k_stage(Table t, Delta D, int64_t* __restrict__ out, uint64_t cap, int width,
-                                               unsigned long long* count_out, int with_fail) {
+// Stage the sharded delta list as contiguous records. grid = kShards blocks of 1024
+// threads: block s copies shard s to its prefix position (deterministic, no append
+// atomics); rows past `cap` are dropped (the count says how many there were). Block 0
+// writes the count word (| kFailBit when with_fail and the verdict failed: the exchange
+// carries the verdict, Candidates.merge :79-81); the last block (a ticket of kShards
+// same-address atomics) resets the shard counters. Blocks of 256 threads took 22 us per
+// 2^22-edge exchange of an 8-rank shard, each walking ~3 K rows in a dependent loop; 8
+// blocks per shard with a separate reset kernel took 8.3 + 4.9 us
+// (profiles/r04_rank_replay.txt).
+constexpr uint32_t kStageBS = 1024;
+__global__ __launch_bounds__(kStageBS) void k_stage(Table t, Delta D, int64_t* __restrict__ out, uint64_t cap,
+                                                    int width, unsigned long long* count_out, int with_fail) {
   __shared__ uint32_t cnt[kShards];
   __shared__ uint64_t off_sh, total_sh;
   __shared__ uint32_t last;
@@ -792,7 +797,7 @@ __global__ __launch_bounds__(256) void k_stage(Table t, Delta D, int64_t* __rest
   __syncthreads();
   const int64_t* in = D.drec + (size_t)s * D.shard_cap * 3;
   const uint64_t off = off_sh;
-  for (uint32_t j = threadIdx.x; j < cnt[s]; j += 256) {
+  for (uint32_t j = threadIdx.x; j < cnt[s]; j += kStageBS) {
     const uint64_t pos = off + j;
     if (pos >= cap) break;
     int64_t* r = out + pos * width;
@@ -1014,7 +1019,7 @@ void launch_digest(const Table& t, unsigned long long* out, uint64_t bound, hipS
 
 void launch_stage(const Table& t, const Delta& D, int64_t* out, uint64_t cap, int width,
                   unsigned long long* count_out, bool with_fail, hipStream_t st) {
-  hipLaunchKernelGGL(k_stage, dim3(kShards), dim3(256), 0, st, t, D, out, cap, width, count_out, with_fail ? 1 : 0);
+  hipLaunchKernelGGL(k_stage, dim3(kShards), dim3(kStageBS), 0, st, t, D, out, cap, width, count_out, with_fail ? 1 : 0);
 }
 
 void launch_report(uint32_t* ctr, uint64_t n, unsigned long long* out, unsigned epoch, hipStream_t st) {

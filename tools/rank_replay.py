@@ -10,7 +10,8 @@ in one process. This tool instead measures what ONE rank's GPU would do:
      delta tracking and takes its records; then folds every other rank's records of
      exchange b - 3 (the native group's lag). Every rank's records are kept;
   2. replay: rank 0 alone -- reset, then per exchange its own tracked fold, the take
-     of its records, and the fold of the other ranks' recorded rows of exchange b - 3,
+     of its records, and the fold of the other ranks' recorded rows of exchange b - 3
+     (one launch over all of them, as the native group does),
      all on the summary's stream (no overlap of own and remote folds, which the native
      group has: an upper bound of the rank's GPU time);
   3. compare with the plain 1-GPU pass of the whole stream (T1): projected efficiency
@@ -42,6 +43,8 @@ def main():
     ap.add_argument("--log-batch", type=int, default=22)
     ap.add_argument("--ramp-log2", type=int, default=22)
     ap.add_argument("--ramp-log-batch", type=int, default=20)
+    ap.add_argument("--own-only", action="store_true",
+                    help="only rank 0's own folds, untracked vs tracked + takes (for a kernel trace of the tax)")
     a = ap.parse_args()
     E, N = 16 << a.scale, a.ranks
     per = E // N
@@ -64,14 +67,35 @@ def main():
         for x in range(0, m, 1 << 20):
             s.fold_device(src[base + x:], dst[base + x:], n=min(1 << 20, m - x))
 
+    cap = max(m for _, m in bounds) + 256
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    scratch = torch.empty((cap, 3), dtype=torch.int64, device="cuda")
+    if a.own_only:
+        rep = gs.Summary("cc", capacity_hint=hint)
+        for tracked in (False, True, False, True):
+            rep.set_delta_tracking(tracked)
+            best = None
+            for _ in range(a.reps):
+                rep.reset()
+                rep.sync()
+                t = time.perf_counter()
+                for o, m in bounds:
+                    fold_own(rep, 0, o, m)
+                    if tracked:
+                        rep.take_delta_records(scratch, cap, cnt)
+                rep.sync()
+                el = time.perf_counter() - t
+                best = el if best is None else min(best, el)
+            print("rank 0 own folds %s: %.2f ms" % ("tracked + takes" if tracked else "untracked, no takes",
+                                                     best * 1e3), flush=True)
+        rep.close()
+        return 0
+
     # 1. record
     summ = [gs.Summary("cc", capacity_hint=hint) for _ in range(N)]
     for s in summ:
         s.set_delta_tracking(True)
-    cap = max(m for _, m in bounds) + 256
     recs = [[None] * nex for _ in range(N)]
-    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-    scratch = torch.empty((cap, 3), dtype=torch.int64, device="cuda")
     t0 = time.perf_counter()
     for b in range(nex):
         o, m = bounds[b]
@@ -133,7 +157,10 @@ def main():
     one.close()
 
     # 2. replay rank 0 alone
-    remote = [[recs[q][e] for q in range(1, N) if recs[q][e].shape[0]] for e in range(nex)]
+    # one launch per exchange over all other ranks' rows, as the native group folds them (one exchange-layout
+    # launch on its apply stream), not one small launch per (rank, exchange)
+    remote = [[x] if x.shape[0] else [] for x in
+              (torch.cat([recs[q][e] for q in range(1, N)]) for e in range(nex))]
     rows = sum(int(x.shape[0]) for e in range(nex) for x in remote[e])
 
     def run_rank(parts):
