@@ -202,6 +202,62 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
   return kNoSlot;
 }
 
+// The end of an insert attempt at slot h: `old` is the key the slot held (the CAS's
+// return when `tried`, else an agent-scope read). Slot won, found, or -- held by another
+// id -- the probe continues at h + 1.
+template <bool TTAS>
+__device__ __forceinline__ uint32_t insert_finish(const Table& t, int64_t key, uint32_t h, unsigned long long old,
+                                                  bool tried, uint32_t& link, bool& fresh) {
+  fresh = false;
+  if (tried && old == (unsigned long long)kEmpty) {
+    fresh = true;
+    if (t.mark_new) t.tab[h].aux = kAuxNew;
+    link = h << 1;
+    return h;
+  }
+  if ((int64_t)old == key) {
+    link = load_link_fresh(t.tab + h);
+    return h;
+  }
+  h = (h + 1) & t.mask;
+  int64_t k;
+  uint32_t l;
+  load_slot(t.tab + h, k, l);
+  return lookup_resolve<TTAS>(t, key, h, k, l, link, fresh);
+}
+
+// Both endpoints' first probes read EMPTY (a young table: config 5's first windows,
+// config 4's insert phase): their key CASes (and, TTAS, the re-reads before them) go out
+// together instead of one endpoint's chain after the other's -- one dependent atomic
+// round trip less per edge that inserts both ends. Precondition: ku != kv, hu != hv,
+// neither id is kEmpty.
+#ifndef GS_PAIR_INSERT
+#define GS_PAIR_INSERT 1  // 0: endpoints inserted one after the other (experiment switch)
+#endif
+template <bool TTAS>
+__device__ __forceinline__ void insert_pair(const Table& t, int64_t ku, uint32_t hu, int64_t kv, uint32_t hv,
+                                            uint32_t& su, uint32_t& lu, bool& nu, uint32_t& sv, uint32_t& lv,
+                                            bool& nv) {
+  unsigned long long ou = (unsigned long long)kEmpty, ov = (unsigned long long)kEmpty;
+  if (TTAS) {
+    ou = __hip_atomic_load((unsigned long long*)&t.tab[hu].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ov = __hip_atomic_load((unsigned long long*)&t.tab[hv].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const bool tu = ou == (unsigned long long)kEmpty, tv = ov == (unsigned long long)kEmpty;
+  // Both tests before either CAS, and no use of the first CAS's result before the second
+  // is issued (left to itself the compiler tested the second re-read after the first CAS
+  // and waited for that CAS). A slot the re-read found taken gets no CAS: a hub's slot
+  // must not queue same-address atomics (RMAT-20: 0.69 -> 0.745 ms/step with no-op CASes).
+  const uint32_t tv32 = tv ? 1u : 0u;
+  asm volatile("" ::"v"(tv32) : "memory");  // the second test is materialised here, before either CAS
+  __builtin_amdgcn_sched_barrier(0);
+  if (tu) ou = atomicCAS((unsigned long long*)&t.tab[hu].key, (unsigned long long)kEmpty, (unsigned long long)ku);
+  if (tv32) ov = atomicCAS((unsigned long long*)&t.tab[hv].key, (unsigned long long)kEmpty, (unsigned long long)kv);
+  __builtin_amdgcn_sched_barrier(0);
+  su = insert_finish<TTAS>(t, ku, hu, ou, tu, lu, nu);
+  sv = insert_finish<TTAS>(t, kv, hv, ov, tv, lv, nv);
+}
+
 __device__ __forceinline__ uint32_t lookup_insert(const Table& t, int64_t key, uint32_t& link, bool& fresh) {
   const uint32_t h = hash_slot(key, t.shift);
   int64_t k;
@@ -233,6 +289,15 @@ __device__ __forceinline__ uint32_t lookup_find(const Table& t, int64_t key, uin
 // probes and writes the ids after its finds and hook, so that the returning atomic
 // overlaps the find loads instead of preceding them (config 5 with the CAS-only
 // insert: p50 13.4 -> 12.5 us, p99 27.2 -> 24.8; profiles/r03_insert_ab.txt).
+// The reservation is wave-aggregated: one atomic per wave for the wave's new vertices
+// (a wave scan of the per-lane counts gives each lane its offset). One per inserting lane
+// serialised on the shard's counter while a young table fills: ~1 K same-address
+// atomics per shard per 2^16-edge window of config 5, ~16 K per 2^20-edge batch of
+// config 4's insert phase (11 ns each at the memory side, profiles/r01_calib_atomic.log).
+// Both calls are made in wave-uniform control flow.
+#ifndef GS_WAVE_RESERVE
+#define GS_WAVE_RESERVE 1  // 0: one reservation atomic per inserting lane (experiment switch)
+#endif
 struct NewVertices {
   uint32_t k = 0, pos = 0, su = 0, sv = 0;
   bool nu = false;
@@ -245,11 +310,32 @@ __device__ __forceinline__ NewVertices reserve_new_vertices(const Table& t, int 
   r.nu = nu;
   r.su = su;
   r.sv = sv;
-  if (r.k) r.pos = atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], r.k);
+  if (!GS_WAVE_RESERVE) {
+    if (r.k) r.pos = atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], r.k);
+    return r;
+  }
+  const int lane = (int)(threadIdx.x & 63u);
+  uint32_t x = r.k;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  const uint32_t total = __shfl(x, 63, 64);
+  // until write_new_vertices: lane 0 holds the wave's base (the returning atomic overlaps
+  // the finds), every lane its exclusive offset
+  r.pos = x - r.k;
+  if (total && lane == 0) r.pos = atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], total);
   return r;
 }
 
-__device__ __forceinline__ void write_new_vertices(const Table& t, int shard, const NewVertices& r) {
+__device__ __forceinline__ void write_new_vertices(const Table& t, int shard, NewVertices r) {
+  if (GS_WAVE_RESERVE) {
+    const uint32_t excl = r.pos;
+    const uint32_t base = __shfl(r.pos, 0, 64);
+    // lane 0's own offset is 0: its pos became the base
+    r.pos = base + ((threadIdx.x & 63u) == 0 ? 0u : excl);
+  }
   if (!r.k || !t.vlist) return;
   if (r.pos + r.k > t.vshard_cap) {
     raise_flag(t, CTR_VOVF, 2);

@@ -358,11 +358,18 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   uint32_t fresh0 = kNoSlot, fresh1 = kNoSlot;  // slots this thread inserted
   bool has_rec = false;  // TRACK: this edge's record (a self-loop's new vertex, or its hook)
   int64_t rec[3] = {0, 0, 0};
+  bool nu = false, nv = false;
+  uint32_t su = kNoSlot, sv = kNoSlot;
   if (valid) {
-    bool nu, nv;
-    const uint32_t su = lookup_resolve<!TAKE && GS_INSERT_TTAS>(t, ks, hu, k0u, l0u, lu, nu);
-    const uint32_t sv = lookup_resolve<!TAKE && GS_INSERT_TTAS>(t, kd, hv, k0v, l0v, lv, nv);
-    nvx = reserve_new_vertices(t, shard, nu, su, nv, sv);  // ids written after the hook
+    if (GS_PAIR_INSERT && k0u == kEmpty && k0v == kEmpty && hu != hv && ks != kd && ks != kEmpty && kd != kEmpty) {
+      insert_pair<!TAKE && GS_INSERT_TTAS>(t, ks, hu, kd, hv, su, lu, nu, sv, lv, nv);
+    } else {
+      su = lookup_resolve<!TAKE && GS_INSERT_TTAS>(t, ks, hu, k0u, l0u, lu, nu);
+      sv = lookup_resolve<!TAKE && GS_INSERT_TTAS>(t, kd, hv, k0v, l0v, lv, nv);
+    }
+  }
+  nvx = reserve_new_vertices(t, shard, nu, su, nv, sv);  // one atomic per wave; ids written after the hook
+  if (valid) {
     if (nu) fresh0 = su;
     if (nv) fresh1 = sv;
     if (dbg) atomicAdd(&dbg[1], (nu ? 1u : 0u) + ((nv && sv != su) ? 1u : 0u));

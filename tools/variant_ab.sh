@@ -1,24 +1,20 @@
 #!/bin/bash
-# A/B of experiment builds on one GPU box (run from the repo root on the box):
-# every variant library (gelly-streaming_amd/lib_<v>/, `make variant V=<v> VFLAGS=...`;
-# "base" = the product build) runs the same bench lines, interleaved twice, into
-# gpurun_out/variant_ab/<tag>/. A bench line that fails ends the run (no retries).
-# Usage: bash tools/variant_ab.sh <tag> "<v1> <v2> ..." "<bench args 1>" ["<bench args 2>" ...]
+# A/B of the default build against lib_<variant> (GS_LIB_VARIANT) on the bench lines named in WORKLOADS
+# (bip, r20, er, n1), two rounds, one box. Usage: VARIANT=noreserve WORKLOADS="bip r20 er" bash tools/variant_ab.sh
 set -u
-TAG=$1; VARIANTS=$2; shift 2
-R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/variant_ab/$TAG
+O=gpurun_out/variant_ab
 mkdir -p $O
-cd $R
-for rep in 1 2; do
-  for v in $VARIANTS; do
-    i=0
-    for a in "$@"; do
-      i=$((i + 1))
-      if [ "$v" = base ]; then env=""; else env="GS_LIB_VARIANT=$v"; fi
-      f=$O/${v}_${i}_rep$rep.json
-      env $env timeout -k 10 240 python bench.py $a > $f 2> $O/${v}_${i}_rep$rep.err || { echo "$v [$a] failed rc=$?"; exit 1; }
-      echo "$v rep$rep [$a]: $(python -c "import json,sys; d=json.loads(open('$f').read().strip().splitlines()[-1]); c=d['config']; print(d['value'], d['ms_per_step'], c.get('p50_us'), c.get('p99_us'))")"
-    done
-  done
-done
+for r in 1 2; do for v in default $VARIANT; do for w in $WORKLOADS; do
+  if [ $v = default ]; then unset GS_LIB_VARIANT; else export GS_LIB_VARIANT=$v; fi
+  case $w in
+    bip) A="--workload bip";; r20) A="--scale 20";; er) A="--workload er-latency";; n1) A="--steps 5 --warmup 2";;
+    ingest) A="--workload ingest";;
+  esac
+  timeout -k 10 300 python bench.py $A --no-cpu-baseline --no-profile-pass > $O/${w}_${v}_$r.json 2> $O/${w}_${v}_$r.err || { tail -5 $O/${w}_${v}_$r.err; exit 1; }
+  python - $O/${w}_${v}_$r.json "$w $v $r" <<'PY'
+import json, sys
+l = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); c = l["config"]
+extra = {k: c[k] for k in ("p50_us", "p99_us", "tail") if k in c}
+print(sys.argv[2], l["ms_per_step"], l["value"], extra.get("tail", extra) if extra else "")
+PY
+done; done; done
