@@ -355,9 +355,12 @@ int server_start(gs_summary* h) {
   b->seq = h->srv_seq;
   b->bc_init = h->srv_seq;
   GS_HIP(hipMemcpyAsync(&h->srv_bc->seq, &b->bc_init, 8, hipMemcpyHostToDevice, h->stream));
-  // ~250 ms without a window: the launch leaves on its own (wall clock 100 MHz)
+  // ~2 ms without a window: the launch leaves on its own (wall clock 100 MHz). It holds
+  // its stream's hardware queue while resident, so another stream that shares the queue
+  // waits at most that long behind an idle server (the config-5 windows arrive
+  // back to back; a restart costs one launch).
   gs::launch_window_server(h->kind == GS_KIND_SIGNED, h->table(), h->delta(), h->srv_box, h->srv_bc, h->done_dev,
-                           h->srv_seq, 25000000ull, h->stream);
+                           h->srv_seq, 200000ull, h->stream);
   GS_HIP(hipGetLastError());
   h->srv_running = true;
   h->srv_launches++;

@@ -287,7 +287,7 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
                                            const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                            int64_t* __restrict__ dst, uint64_t cap,
                                            unsigned long long* __restrict__ bad, bool aligned, uint64_t tile,
-                                           unsigned long long* __restrict__ status);
+                                           unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat);
 
 // Single pass (GS_PARSE_FUSED, default): no k_count_lines pass and no scan. Every block
 // counts its tile's '\n' from the masks it builds anyway and finds the count before its
@@ -300,32 +300,70 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
 // is read once instead of twice (the count pass was 126 us of a 684 MB parse).
 
 constexpr unsigned long long kStP = 1ull << 63, kStA = 1ull << 62, kStVal = (1ull << 62) - 1;
+// Early aggregates: a tile that lies wholly inside the text publishes its '\n' count as
+// soon as its staging loads arrive, before the LDS staging, masks and scan: each wave adds
+// (1 << kStWaveShift) | (its count) to the tile's status word, and the aggregate is
+// complete once all four waves have added. (The look-back's waits are for predecessors'
+// aggregates; this moves them a staging-and-scan earlier.)
+#ifndef GS_PARSE_EARLY
+#define GS_PARSE_EARLY 1  // 0: aggregates published after the scan (experiment switch)
+#endif
+constexpr int kStWaveShift = 56;
+constexpr unsigned long long kStWaves = 7ull << kStWaveShift, kStCnt = (1ull << kStWaveShift) - 1;
+// The inclusive prefixes (kStP | value) live in a second array, pstat: the aggregate word
+// takes atomic adds that may still be in flight when the tile's prefix is known.
+__device__ __forceinline__ bool st_has_agg(unsigned long long w) {
+  return (w & kStA) != 0 || (w & kStWaves) == (4ull << kStWaveShift);
+}
+__device__ __forceinline__ unsigned long long st_agg(unsigned long long w) {
+  return (w & kStA) ? (w & kStVal) : (w & kStCnt);
+}
+// '\n' bytes in 16 staged bytes (exact zero-byte count of x ^ 0x0A0A0A0A per word)
+__device__ __forceinline__ uint32_t nl_count16(const uint4& v) {
+  uint32_t c = 0;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = w[i] ^ 0x0A0A0A0Au;
+    const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+    c += __popc(t);
+  }
+  return c;
+}
 
 // Wave 0 of tile `tile`: '\n' before the tile (decoupled look-back over 64 predecessors
 // per round); publishes the tile's inclusive count. agg = the tile's own '\n' count.
 // Between unsuccessful rounds the wave backs off (s_sleep 8 -> 64): every waiting wave
 // re-reading 64 status words at once slowed the other blocks' staging loads.
 __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restrict__ text, unsigned long long* status,
-                                                        uint64_t tile, unsigned long long agg) {
+                                                        unsigned long long* pstat, uint64_t tile, unsigned long long agg,
+                                                        bool published) {
   const int lane = threadIdx.x & 63;
   if (tile == 0) {
-    if (lane == 0) __hip_atomic_store(status, kStP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_store(pstat, kStP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 0;
   }
-  if (lane == 0) __hip_atomic_store(status + tile, kStA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // (published: the waves' early adds already carry the aggregate; a store here could
+  // overtake one of them)
+  if (lane == 0 && !published)
+    __hip_atomic_store(status + tile, kStA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned long long excl = 0;
   int64_t base = (int64_t)tile - 1;
   const unsigned long long t_start = wall_clock64();
   int backoff = 0;
   for (;;) {
     const int64_t ti = base - lane;  // lane 0: the nearest predecessor
-    const unsigned long long w =
-        ti >= 0 ? __hip_atomic_load(status + ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kStP;
-    const unsigned long long pm = __ballot((w & kStP) != 0), am = __ballot((w & (kStP | kStA)) != 0);
+    const unsigned long long wp =
+        ti >= 0 ? __hip_atomic_load(pstat + ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kStP;
+    const unsigned long long wa =
+        ti >= 0 ? __hip_atomic_load(status + ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const bool has_p = (wp & kStP) != 0;
+    const unsigned long long w = has_p ? wp : wa;
+    const unsigned long long pm = __ballot(has_p), am = __ballot(has_p || st_has_agg(wa));
     const int j = pm ? __ffsll((long long)pm) - 1 : 64;  // nearest final prefix in this window
     const unsigned long long need = j >= 64 ? ~0ull : ((2ull << j) - 1ull);  // lanes 0..j
     if ((am & need) == need) {
-      unsigned long long v = lane <= j ? (w & kStVal) : 0ull;
+      unsigned long long v = lane <= j ? (has_p ? (w & kStVal) : st_agg(w)) : 0ull;
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
       excl += v;
@@ -349,15 +387,15 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
     }
     ++backoff;
   }
-  if (lane == 0) __hip_atomic_store(status + tile, kStP | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) __hip_atomic_store(pstat + tile, kStP | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return excl;
 }
 
 __global__ __launch_bounds__(256) void k_parse_fused(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                                      int64_t* __restrict__ src, int64_t* __restrict__ dst, uint64_t cap,
                                                      unsigned long long* __restrict__ bad, bool aligned,
-                                                     unsigned long long* __restrict__ status) {
-  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, blockIdx.x, status);
+                                                     unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat) {
+  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, blockIdx.x, status, pstat);
 }
 
 // One tile per block (44 VGPRs, 8 blocks per CU).
@@ -365,7 +403,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
                                                const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                                int64_t* __restrict__ dst, uint64_t cap,
                                                unsigned long long* __restrict__ bad, bool aligned, uint64_t tile0) {
-  parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile0 + blockIdx.x, nullptr);
+  parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile0 + blockIdx.x, nullptr, nullptr);
 }
 
 template <bool FUSED>
@@ -373,7 +411,7 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
                                            const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                            int64_t* __restrict__ dst, uint64_t cap,
                                            unsigned long long* __restrict__ bad, bool aligned, uint64_t tile,
-                                           unsigned long long* __restrict__ status) {
+                                           unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat) {
   constexpr uint32_t kSeg = kTile / 256;  // bytes per thread in the line-start scan
   constexpr uint32_t kExtra = 2;          // '\n' masks past the tile: lines that cross its end
   constexpr uint32_t kSlots = (kTile + kOver + 4095) / 4096;
@@ -399,6 +437,17 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
   if (f2) v2 = *reinterpret_cast<const uint4*>(text + t0 + i0 + 8192u);
   if (f3) v3 = *reinterpret_cast<const uint4*>(text + t0 + i0 + 12288u);
   if (f4) v4 = *reinterpret_cast<const uint4*>(text + t0 + i0 + 16384u);
+  // one-pass: a tile wholly inside the (aligned) text publishes its '\n' count from the
+  // staged registers (slots 0-3 are exactly its 16 KiB), wave by wave, right away
+  const bool early = GS_PARSE_EARLY && FUSED && tile != 0 && aligned && t0 + kTile <= len;
+  if (early) {
+    uint32_t c = nl_count16(v0) + nl_count16(v1) + nl_count16(v2) + nl_count16(v3);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63u) == 0)
+      __hip_atomic_fetch_add(status + tile, (1ull << kStWaveShift) | (unsigned long long)c, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
   auto put = [&](bool f, uint32_t i, const uint4& v) {
     if (f) {
       *reinterpret_cast<uint4*>(lds + kLds0 + i) = v;
@@ -536,7 +585,8 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
     }
     __shared__ unsigned long long pre_sh;
     if (wid == 0) {
-      const unsigned long long e = look_back(text, status, tile, (unsigned long long)wnl[0] + wnl[1] + wnl[2] + wnl[3]);
+      const unsigned long long e =
+          look_back(text, status, pstat, tile, (unsigned long long)wnl[0] + wnl[1] + wnl[2] + wnl[3], early);
       if (lane == 0) pre_sh = e;
     }
     __syncthreads();
@@ -564,7 +614,7 @@ __global__ void k_parse_result(const uint64_t* tile_pre, const uint64_t* tile_cn
                                const uint8_t* text, uint64_t len, const unsigned long long* bad, uint64_t* res,
                                unsigned long long* host, unsigned long long seq, const unsigned long long* status) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  // '\n' through the last tile (fused: its status word), + 1: a last line may lack '\n'
+  // '\n' through the last tile (fused: its prefix word), + 1: a last line may lack '\n'
   const uint64_t nl = status ? (status[tiles - 1] & kStVal) : tile_pre[tiles - 1] + tile_cnt[tiles - 1];
   const uint64_t lines = nl + (text[len - 1] != '\n' ? 1u : 0u);
   const uint64_t b = *bad;
@@ -585,13 +635,16 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
   if (tiles > s.tiles_cap) return -1;
   const bool aligned = ((uintptr_t)text & 15u) == 0;
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
-  if (fused) {  // status words (s.tile_cnt) zeroed, then one pass
-    if (hipMemsetAsync(s.tile_cnt, 0, tiles * 8, st) != hipSuccess || hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess)
+  if (fused) {  // aggregate words (s.tile_cnt) and prefix words (s.tile_pre) zeroed, then one pass
+    if (hipMemsetAsync(s.tile_cnt, 0, tiles * 8, st) != hipSuccess || hipMemsetAsync(s.tile_pre, 0, tiles * 8, st) != hipSuccess ||
+        hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess)
       return -1;
+    unsigned long long* agg = reinterpret_cast<unsigned long long*>(s.tile_cnt);
+    unsigned long long* pre = reinterpret_cast<unsigned long long*>(s.tile_pre);
     hipLaunchKernelGGL(k_parse_fused, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, src, dst,
-                       (uint64_t)cap, s.bad, aligned, reinterpret_cast<unsigned long long*>(s.tile_cnt));
+                       (uint64_t)cap, s.bad, aligned, agg, pre);
     hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
-                       s.bad, s.res, host_res, seq, reinterpret_cast<const unsigned long long*>(s.tile_cnt));
+                       s.bad, s.res, host_res, seq, pre);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   hipLaunchKernelGGL(k_count_lines, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, s.tile_cnt, aligned,

@@ -172,6 +172,36 @@ __device__ __forceinline__ bool take_tail(const Table& t, const FoldArgs& a, con
   unsigned long long nv = 0;
   if (solo && threadIdx.x < 64)
     nv = __hip_atomic_load(t.ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (solo && !signed_kind) {
+    // A one-block CC window: the rows, the count word and the staged-rows tally go out
+    // together and ONE drain covers them all (the multi-block path needs its rows in
+    // memory before the ticket, and a signed window's verdict is read after the drain):
+    // one dependent round trip less on the latency floor (the 64-edge window).
+    for (uint32_t j = threadIdx.x; j < nb; j += kFoldBS) {
+      if (j < a.take_cap) {
+        int64_t* r = a.take_out + (size_t)j * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          __hip_atomic_store(r + c, lrec[j * 3 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(a.take_count, (unsigned long long)lcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_SENT)),
+                (unsigned long long)(lcnt < a.take_cap ? lcnt : a.take_cap));
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x >= 64) return false;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) nv += __shfl_xor(nv, o, 64);
+    if (threadIdx.x != 0) return false;
+    __hip_atomic_store(a.done + 1, done_value(a.seq, nv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.done + 2, done_value(a.seq, (unsigned long long)lcnt), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return true;
+  }
   if (threadIdx.x == 0)
     base_sh = (nb && !solo) ? atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE)),
                                         (unsigned long long)nb)

@@ -282,7 +282,11 @@ int gs_delta_stage(gs_handle h, int64_t* send, size_t cap, int width, uint64_t* 
  * edges, and the window's last block publishes rows, count word and completion word
  * exactly as the fused launch does. Results are identical; any other call on the
  * handle stops the server first (it restarts at the next window), and a server idle
- * for ~250 ms leaves on its own. The edge buffers of a window must be complete before
+ * for ~2 ms leaves on its own. While it runs, the server occupies the handle stream's
+ * hardware queue: work of ANOTHER stream that HIP mapped onto the same queue
+ * (GPU_MAX_HW_QUEUES, 4 by default, are shared round-robin by the process's streams)
+ * starts only after the server leaves, i.e. within ~2 ms of the last window (a stop or a
+ * call on this handle ends it at once). The edge buffers of a window must be complete before
  * the window is posted and must not be rewritten while the server runs (each window
  * reads its edges once; a stream pre-staged in HBM, as BASELINE config 5 has it).
  * gs_window_server_stats: server launches and windows served. */

@@ -238,5 +238,8 @@ def test_config5_window_take_all_windows(gs, oracle_mod, mode):
         assert total >= s.num_vertices() - len(set(s.labels()[1].tolist()))
         if mode == "server":
             st = s.window_server_stats()
-            # only the checkpoint reads stopped it (and, rarely, an idle exit)
-            assert st["windows"] >= nwin - len(checkpoints) - 4 and st["launches"] <= len(checkpoints) + 4, st
+            # the checkpoint reads stopped it; and when HIP put the replica's stream on the
+            # server's hardware queue, each rep.sync() waits for the idle exit (~2 ms): at
+            # most one more launch per 32 windows (gs_set_window_server's header)
+            assert st["windows"] >= nwin - len(checkpoints) - 4, st
+            assert st["launches"] <= len(checkpoints) + nwin // 32 + 4, st
