@@ -611,13 +611,14 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
 // memory) also host[1..2] = the same two words and then host[0] = seq (system-scope
 // release): the caller spins on that word instead of a copy and a stream synchronisation
 __global__ void k_parse_result(const uint64_t* tile_pre, const uint64_t* tile_cnt, uint64_t tiles,
-                               const uint8_t* text, uint64_t len, const unsigned long long* bad, uint64_t* res,
+                               const uint8_t* text, uint64_t len, unsigned long long* bad, uint64_t* res,
                                unsigned long long* host, unsigned long long seq, const unsigned long long* status) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   // '\n' through the last tile (fused: its prefix word), + 1: a last line may lack '\n'
   const uint64_t nl = status ? (status[tiles - 1] & kStVal) : tile_pre[tiles - 1] + tile_cnt[tiles - 1];
   const uint64_t lines = nl + (text[len - 1] != '\n' ? 1u : 0u);
   const uint64_t b = *bad;
+  *bad = ~0ull;  // ready for the next parse (the one-pass path does not memset it)
   res[0] = lines;
   res[1] = b;
   if (host) {
@@ -636,9 +637,11 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
   const bool aligned = ((uintptr_t)text & 15u) == 0;
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
   if (fused) {  // aggregate words (s.tile_cnt) and prefix words (s.tile_pre) zeroed, then one pass
-    if (hipMemsetAsync(s.tile_cnt, 0, tiles * 8, st) != hipSuccess || hipMemsetAsync(s.tile_pre, 0, tiles * 8, st) != hipSuccess ||
-        hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess)
-      return -1;
+    // one fill: the aggregate words and the prefix words are adjacent (tile_pre = tile_cnt
+    // + tiles_cap); `bad` is reset by the previous parse's k_parse_result
+    if (hipMemsetAsync(s.tile_cnt, 0, (s.tiles_cap + tiles) * 8, st) != hipSuccess) return -1;
+    if (!s.bad_ready && hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess) return -1;
+    s.bad_ready = true;
     unsigned long long* agg = reinterpret_cast<unsigned long long*>(s.tile_cnt);
     unsigned long long* pre = reinterpret_cast<unsigned long long*>(s.tile_pre);
     hipLaunchKernelGGL(k_parse_fused, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, src, dst,
@@ -693,6 +696,7 @@ int parse_scratch_init(ParseScratch& s, void* mem, size_t max_len) {
   s.cub_tmp = reinterpret_cast<void*>(((uintptr_t)(s.res + 4) + 255) & ~(uintptr_t)255);
   s.cub_bytes = cub;
   s.tiles_cap = tiles;
+  s.bad_ready = false;
   return 0;
 }
 

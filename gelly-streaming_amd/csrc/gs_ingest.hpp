@@ -14,6 +14,7 @@ struct ParseScratch {
   void* cub_tmp = nullptr;
   size_t cub_bytes = 0;
   uint64_t tiles_cap = 0;
+  bool bad_ready = false;  // `bad` holds ~0 (k_parse_result resets it after every parse)
 };
 
 // Device bytes needed to parse up to max_len bytes of text.
