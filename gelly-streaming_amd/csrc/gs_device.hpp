@@ -80,7 +80,9 @@ enum CounterBlock : int {
   CTR_DBG_ITERS,                 //   hook-loop iterations,
   CTR_DBG_CASFAIL,               //   failed hook CASes
   CTR_TAKE_SHARD,                // [kTicketShards] block tickets, first level (block b -> shard b mod 16)
-  CTR_COUNT = CTR_TAKE_SHARD + 16
+  CTR_SRV_NV = CTR_TAKE_SHARD + 16,  // resident window server: vertices after its last window (u64)
+  CTR_SRV_NV_HI,
+  CTR_COUNT
 };
 __host__ __device__ constexpr int ctr_index(int c) { return c * kCtrStride; }
 
@@ -123,6 +125,7 @@ struct Delta {
   // fused window take (k_fold TAKE): the block's records go to an LDS buffer instead
   int64_t* lrec = nullptr;   // [kFoldBS][3] (LDS)
   uint32_t* lcnt = nullptr;  // its fill (LDS)
+  uint32_t* lnv = nullptr;   // resident window server: the block's new vertices of the window (LDS)
 };
 
 __device__ __forceinline__ uint32_t hash_slot(int64_t key, int shift) {
@@ -303,8 +306,9 @@ struct NewVertices {
   bool nu = false;
 };
 
+// lnv (optional, LDS): the block's count of new vertices, for the window server's tickets
 __device__ __forceinline__ NewVertices reserve_new_vertices(const Table& t, int shard, bool nu, uint32_t su, bool nv,
-                                                            uint32_t sv) {
+                                                            uint32_t sv, uint32_t* lnv = nullptr) {
   NewVertices r;
   r.k = (nu ? 1u : 0u) + ((nv && sv != su) ? 1u : 0u);
   r.nu = nu;
@@ -312,6 +316,7 @@ __device__ __forceinline__ NewVertices reserve_new_vertices(const Table& t, int 
   r.sv = sv;
   if (!GS_WAVE_RESERVE) {
     if (r.k) r.pos = atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], r.k);
+    if (lnv && r.k) atomicAdd(lnv, r.k);
     return r;
   }
   const int lane = (int)(threadIdx.x & 63u);
@@ -325,7 +330,10 @@ __device__ __forceinline__ NewVertices reserve_new_vertices(const Table& t, int 
   // until write_new_vertices: lane 0 holds the wave's base (the returning atomic overlaps
   // the finds), every lane its exclusive offset
   r.pos = x - r.k;
-  if (total && lane == 0) r.pos = atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], total);
+  if (total && lane == 0) {
+    r.pos = atomicAdd(&t.ctr[ctr_index(CTR_NV + shard)], total);
+    if (lnv) atomicAdd(lnv, total);
+  }
   return r;
 }
 

@@ -112,6 +112,7 @@ struct FoldArgs {
   unsigned long long* take_count;
   unsigned long long* done;
   unsigned long long seq;
+  bool server = false;  // resident window server: vertices carried by the tickets (take_tail)
 };
 
 constexpr int kCombineRounds = 2;  // wave-level hook combining (combine_hooks)
@@ -157,20 +158,44 @@ __device__ unsigned long long g_strace_cap = 0;
 // A signed summary's count word carries the verdict (| kFailBit once it failed): the
 // take's consumer replays the records AND the verdict (Candidates.merge :79-81).
 // Returns true in the one thread that published the window (the last block's thread 0).
+// Window-server CC windows carry their totals through the tickets: each block adds
+// {1, its rows, its new vertices} packed in one 64-bit word (16 + 24 + 24 bits), so the
+// last block knows the window's rows and inserts from the returned values, and the vertex
+// count is the previous window's (CTR_SRV_NV, loaded at the start of the tail) plus this
+// window's inserts: no round of counter loads after the ticket (config 5's latency).
+#ifndef GS_TAKE_CARRY
+#define GS_TAKE_CARRY 1  // 0: the publisher loads the counters after the ticket (experiment switch)
+#endif
+__device__ __forceinline__ unsigned long long tk_pack(unsigned long long n, unsigned long long rows,
+                                                      unsigned long long newv) {
+  return n | (rows << 16) | (newv << 40);
+}
+__device__ __forceinline__ unsigned long long tk_n(unsigned long long w) { return w & 0xFFFFull; }
+__device__ __forceinline__ unsigned long long tk_rows(unsigned long long w) { return (w >> 16) & 0xFFFFFFull; }
+__device__ __forceinline__ unsigned long long tk_newv(unsigned long long w) { return w >> 40; }
+
 __device__ __forceinline__ bool take_tail(const Table& t, const FoldArgs& a, const int64_t* lrec, uint32_t lcnt,
-                                          bool signed_kind, uint32_t blk, uint32_t nblocks) {
+                                          bool signed_kind, uint32_t blk, uint32_t nblocks, uint32_t newv = 0) {
   __shared__ unsigned long long base_sh;
   __shared__ uint32_t last_sh;
   const uint32_t nb = min(lcnt, kFoldBS);
   // a one-block window owns the whole output: no reservation and no ticket (two
   // dependent atomics of a small window's latency)
   const bool solo = nblocks == 1;
+  unsigned long long* srv_nv = reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_SRV_NV));
+  // the ticket-carried form: window-server CC windows (the packed fields hold 2^16 blocks,
+  // 2^24 rows and 2^24 new vertices: 4096 blocks of 256 edges stay far inside)
+  const bool carried = GS_TAKE_CARRY && a.server && !signed_kind && nblocks <= 4096;
+  // the vertex count before this window (server: exact, kept by every window's publisher
+  // and set at the session's start; stable while the window runs)
+  unsigned long long nv0 = 0;
+  if (a.server && threadIdx.x == 0) nv0 = __hip_atomic_load(srv_nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // a one-block window's vertex count is final once its own fold is (its inserts were
   // counted by returning atomics): the count loads go out now, beside the row stores.
   // (Not the verdict: the fold raises it with no-return atomics, ordered only by the
   // drain below.)
   unsigned long long nv = 0;
-  if (solo && threadIdx.x < 64)
+  if (solo && !carried && threadIdx.x < 64)
     nv = __hip_atomic_load(t.ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (solo && !signed_kind) {
     // A one-block CC window: the rows, the count word and the staged-rows tally go out
@@ -189,12 +214,18 @@ __device__ __forceinline__ bool take_tail(const Table& t, const FoldArgs& a, con
       __hip_atomic_store(a.take_count, (unsigned long long)lcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_SENT)),
                 (unsigned long long)(lcnt < a.take_cap ? lcnt : a.take_cap));
+      if (carried) {
+        nv = nv0 + newv;
+        __hip_atomic_store(srv_nv, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x >= 64) return false;
+    if (!carried) {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) nv += __shfl_xor(nv, o, 64);
+      for (int o = 32; o >= 1; o >>= 1) nv += __shfl_xor(nv, o, 64);
+    }
     if (threadIdx.x != 0) return false;
     __hip_atomic_store(a.done + 1, done_value(a.seq, nv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(a.done + 2, done_value(a.seq, (unsigned long long)lcnt), __ATOMIC_RELAXED,
@@ -227,8 +258,45 @@ __device__ __forceinline__ bool take_tail(const Table& t, const FoldArgs& a, con
   // atomic made after the counting block's rows were acknowledged: the chain of
   // returned values orders every block's rows before the last block's reads.)
   // (Up to 16 blocks count on the top word directly; one block needs no ticket.)
+  constexpr uint32_t kTS = 16;
+  if (carried) {
+    if (threadIdx.x != 0) return false;
+    unsigned long long* top = reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE_DONE));
+    unsigned long long mine = tk_pack(1, nb, newv);
+    uint32_t expect = nblocks;
+    if (nblocks > kTS) {
+      const uint32_t shard = blk % kTS;
+      const uint32_t in_shard = (nblocks - shard + kTS - 1) / kTS;
+      unsigned long long* sw = reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE_SHARD + shard));
+      const unsigned long long o = atomicAdd(sw, mine);
+      if (tk_n(o) != in_shard - 1) return false;
+      mine = tk_pack(1, tk_rows(o) + nb, tk_newv(o) + newv);  // the shard's totals go up
+      expect = kTS;
+    }
+    const unsigned long long o2 = atomicAdd(top, mine);
+    if (tk_n(o2) != expect - 1) return false;
+    const unsigned long long total = tk_rows(o2) + tk_rows(mine);
+    const unsigned long long nvw = nv0 + tk_newv(o2) + tk_newv(mine);
+    __hip_atomic_store(a.take_count, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_SENT)),
+              total < a.take_cap ? total : a.take_cap);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE)), 0ull, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(top, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (nblocks > kTS) {
+#pragma unroll
+      for (int k = 0; k < (int)kTS; ++k)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_TAKE_SHARD + k)), 0ull,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __hip_atomic_store(srv_nv, nvw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as below)
+    __hip_atomic_store(a.done + 1, done_value(a.seq, nvw), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.done + 2, done_value(a.seq, total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return true;
+  }
   if (threadIdx.x == 0) {
-    constexpr uint32_t kTS = 16;
     bool last = true;
     if (nblocks > kTS) {
       const uint32_t shard = blk % kTS;
@@ -261,6 +329,7 @@ __device__ __forceinline__ bool take_tail(const Table& t, const FoldArgs& a, con
   const unsigned long long word = total | (failed ? kFailBit : 0ull);
   __hip_atomic_store(a.take_count, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
   atomicAdd(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_SENT)), total < a.take_cap ? total : a.take_cap);
+  if (a.server) __hip_atomic_store(srv_nv, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // signed server windows
   if (!solo) {
     __hip_atomic_store(take, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(t.ctr + ctr_index(CTR_TAKE_DONE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -398,7 +467,7 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
       sv = lookup_resolve<!TAKE && GS_INSERT_TTAS>(t, kd, hv, k0v, l0v, lv, nv);
     }
   }
-  nvx = reserve_new_vertices(t, shard, nu, su, nv, sv);  // one atomic per wave; ids written after the hook
+  nvx = reserve_new_vertices(t, shard, nu, su, nv, sv, TAKE ? D.lnv : nullptr);  // one atomic per wave
   if (valid) {
     if (nu) fresh0 = su;
     if (nv) fresh1 = sv;
@@ -480,10 +549,23 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
                                                            unsigned long long* done, unsigned long long seq0,
                                                            unsigned long long idle_ticks) {
   __shared__ int64_t lrec[kFoldBS * 3];
-  __shared__ uint32_t lcnt;
+  __shared__ uint32_t lcnt, lnv;
   __shared__ unsigned long long w[8];
   D.lrec = lrec;
   D.lcnt = &lcnt;
+  D.lnv = &lnv;
+  // the session's vertex count (CTR_SRV_NV): every window's publisher adds its inserts
+  // (take_tail); block 0 drains it before it hands out the first window
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    unsigned long long c =
+        __hip_atomic_load(t.ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (threadIdx.x == 0)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(t.ctr + ctr_index(CTR_SRV_NV)), c, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);
+  }
   unsigned long long last = seq0;
   unsigned long long last_done = 0;  // block 0: completion number of the last window it took
 #ifdef GS_SERVER_TRACE
@@ -556,11 +638,12 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
     a.take_count = reinterpret_cast<unsigned long long*>(w[6]);
     a.done = done;
     a.seq = w[7];
+    a.server = true;
     // only the blocks that hold edges of this window take part (a small window is one
     // block's ticket, not the whole grid's)
     const uint32_t active = (a.n + kFoldBS - 1) / kFoldBS;
     if (blockIdx.x < active) {
-      if (threadIdx.x == 0) lcnt = 0;
+      if (threadIdx.x == 0) lcnt = 0, lnv = 0;
       // a failed verdict is final (no kernel boundary here: read it at the memory side)
       const bool failed = SIGNED && __builtin_amdgcn_readfirstlane(
                                         __hip_atomic_load(&t.ctr[ctr_index(CTR_FAIL)], __ATOMIC_RELAXED,
@@ -586,12 +669,12 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
           tr[6] = active;
         }
       }
-      if (take_tail(t, a, lrec, lcnt, SIGNED, blockIdx.x, active) && tr) {
+      if (take_tail(t, a, lrec, lcnt, SIGNED, blockIdx.x, active, lnv) && tr) {
         tr[4] = tfold;
         tr[5] = wall_clock64();
       }
 #else
-      take_tail(t, a, lrec, lcnt, SIGNED, blockIdx.x, active);
+      take_tail(t, a, lrec, lcnt, SIGNED, blockIdx.x, active, lnv);
 #endif
     }
     __syncthreads();  // LDS (lrec, lcnt, w) is reused by the next window
