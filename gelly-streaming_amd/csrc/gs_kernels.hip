@@ -735,7 +735,10 @@ void launch_dedup(const int64_t* src, const int64_t* dst, uint32_t n, unsigned l
 // thread owns kExportPer slots of a kExportPer x kExportBS-slot tile (coalesced 16-B
 // loads); the block reserves its output range with ONE atomic per tile.
 constexpr uint32_t kExportBS = 1024;
-constexpr int kExportPer = 16;
+#ifndef GS_EXPORT_LOCKSTEP
+#define GS_EXPORT_LOCKSTEP 1  // 0: one find after another, 16 slots per thread (experiment switch)
+#endif
+constexpr int kExportPer = GS_EXPORT_LOCKSTEP ? 8 : 16;
 
 __global__ __launch_bounds__(kExportBS) void k_export(Table t, int64_t* __restrict__ ov, int64_t* __restrict__ ol,
                                                       uint8_t* __restrict__ op, uint64_t cap_out, uint64_t s_begin,
@@ -763,15 +766,35 @@ __global__ __launch_bounds__(kExportBS) void k_export(Table t, int64_t* __restri
         }
       }
     }
+    // Read-only finds. Their first hops go out together (after the folds' path splitting
+    // most vertices hang directly under their root), and only a vertex whose parent is
+    // not a root walks on alone: 16 finds one after another made the final label pass
+    // of RMAT-20 80 us, a chain of dependent loads per thread.
+    int64_t kq[PER];
+    uint32_t lq[PER];
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {  // read-only finds (no stores between the loads)
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t sj = (uint32_t)(tile + (uint64_t)j * kExportBS + threadIdx.x);
+      kq[j] = vk[j];
+      lq[j] = pp[j];
+      if (GS_EXPORT_LOCKSTEP && ((occ >> j) & 1u) && (pp[j] >> 1) != sj) load_slot(t.tab + (pp[j] >> 1), kq[j], lq[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
       lk[j] = vk[j];
       if (!((occ >> j) & 1u)) continue;
+      const uint32_t sj = (uint32_t)(tile + (uint64_t)j * kExportBS + threadIdx.x);
+      const uint32_t p = pp[j] >> 1;
+      if (p == sj) {  // a root
+        pp[j] = 0;
+        continue;
+      }
       uint32_t acc;
-      int64_t kx = vk[j];
-      find_ro(t, (uint32_t)(tile + (uint64_t)j * kExportBS + threadIdx.x), pp[j], kx, acc);
+      if (!GS_EXPORT_LOCKSTEP) load_slot(t.tab + p, kq[j], lq[j]);  // (the switch's form: the hop here)
+      int64_t kx = kq[j];
+      find_ro(t, p, lq[j], kx, acc);  // from the parent: zero more hops when it is the root
       lk[j] = kx;
-      pp[j] = acc;
+      pp[j] = acc ^ (pp[j] & 1u);
     }
     // block exclusive scan of cnt: wave inclusive scan + wave totals in LDS
     uint32_t x = cnt;
