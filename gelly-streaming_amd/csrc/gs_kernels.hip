@@ -141,7 +141,8 @@ __device__ unsigned long long g_blog_n = 0;
 //   [2] last block to start folding (max)        [3] last block done folding (max)
 //   [4] publishing block enters take_tail        [5] completion word stored
 //   [6] blocks that took part
-// followed by 64 counters: a histogram of every block's fold time in 0.5-us buckets.
+// followed by 128 counters: histograms of every block's fold time in 0.5-us buckets (64..127: the
+// session's first 64 windows).
 __device__ unsigned long long* g_strace = nullptr;
 __device__ unsigned long long g_strace_cap = 0;
 #endif
@@ -661,7 +662,8 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
         atomicMax(tr + 2, tgo);
         atomicMax(tr + 3, tfold);
         // histogram of per-block fold times (0.5 us buckets) after the cap records
-        const unsigned long long bkt = min((tfold - tgo) / 50ull, 63ull);
+        // (buckets 64..127: the session's first 64 windows, a young table)
+        const unsigned long long bkt = min((tfold - tgo) / 50ull, 63ull) + (s - seq0 <= 64 ? 64ull : 0ull);
         atomicAdd(g_strace + g_strace_cap * 8 + bkt, 1ull);
         if (blockIdx.x == 0) {
           tr[0] = tseen;

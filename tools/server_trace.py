@@ -44,7 +44,7 @@ def main():
     rec = torch.empty(cap * 3, dtype=torch.int64, device="cuda")
     cnt = torch.empty(1, dtype=torch.int64, device="cuda")
     TC = 1 << 13
-    tr = torch.zeros(TC * 8 + 64, dtype=torch.int64, device="cuda")
+    tr = torch.zeros(TC * 8 + 128, dtype=torch.int64, device="cuda")
     s.sync()
     if L.gs_debug_server_trace(tr.data_ptr(), TC):
         raise SystemExit("gs_debug_server_trace failed")
@@ -93,11 +93,14 @@ def main():
                                                          np.percentile(host[-m:][sl], 99)) +
                       "  ".join("%s %.2f" % (kx, np.percentile(v[-m:][sl], 50)) for kx, v in ph.items()
                                 if kx != "host-device"))
-        # per-block fold times over all blocks of the measured pass
-        c = np.cumsum(hist)
-        q = lambda f: 0.5 * (int(np.searchsorted(c, f * c[-1])) + 0.5)  # noqa: E731
-        print("   per-block fold time (%d blocks): p10 %.2f  p50 %.2f  p90 %.2f  p99 %.2f us" % (
-            int(c[-1]), q(0.1), q(0.5), q(0.9), q(0.99)))
+        # per-block fold times over all blocks of the measured pass: old windows, young (first 64) windows
+        for nm, hh in (("windows 64-", hist[:64]), ("windows 0-63", hist[64:128])):
+            c = np.cumsum(hh)
+            if c[-1] == 0:
+                continue
+            q = lambda f: 0.5 * (int(np.searchsorted(c, f * c[-1])) + 0.5)  # noqa: E731
+            print("   per-block fold time, %s (%d blocks): p10 %.2f  p50 %.2f  p90 %.2f  p99 %.2f us" % (
+                nm, int(c[-1]), q(0.1), q(0.5), q(0.9), q(0.99)))
         sys.stdout.flush()
     s.close()
     return 0
