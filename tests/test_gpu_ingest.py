@@ -182,3 +182,18 @@ def test_parse_newlines_at_tile_edges(gs, oracle_mod, sep):
                 got = _gpu_parse(gs, text, sep)
                 assert (got[2], got[3]) == (en, eb), (base, d, end)
                 assert np.array_equal(got[0], es) and np.array_equal(got[1], ed), (base, d, end)
+
+
+def test_parse_malformed_then_clean_reuses_scratch(gs, oracle_mod):
+    """The one-pass parse does not reset its malformed-line word per call: the previous
+    parse's result kernel does. A parse that reports a malformed line, then clean texts
+    of growing and shrinking sizes (fewer tiles than before: stale status words beyond
+    the new tile count are never read), each report exactly the oracle's result."""
+    rng = np.random.default_rng(11)
+    texts = [_random_text(rng, 40000, 0) + b"12 x\n" + _random_text(rng, 100, 0), _random_text(rng, 40000, 0),
+             _random_text(rng, 300, 0), b"1 2\nnot a line\n", _random_text(rng, 70000, 0), _random_text(rng, 5, 0)]
+    for text in texts:
+        es, ed, en, eb = oracle_mod.parse_edges(text, 0)
+        s, d, n, b = _gpu_parse(gs, text, 0)
+        assert (n, b) == (en, eb), (len(text), n, b, en, eb)
+        assert np.array_equal(s, es) and np.array_equal(d, ed)
