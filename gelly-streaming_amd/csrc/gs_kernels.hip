@@ -912,16 +912,19 @@ __global__ __launch_bounds__(256) void k_digest(Table t, unsigned long long* out
   if ((threadIdx.x & 63u) == 0 && sum) atomicAdd(out, sum);
 }
 
-// Stage the sharded delta list as contiguous records. grid = kShards blocks of 1024
-// threads: block s copies shard s to its prefix position (deterministic, no append
-// atomics); rows past `cap` are dropped (the count says how many there were). Block 0
-// writes the count word (| kFailBit when with_fail and the verdict failed: the exchange
-// carries the verdict, Candidates.merge :79-81); the last block (a ticket of kShards
-// same-address atomics) resets the shard counters. Blocks of 256 threads took 22 us per
-// 2^22-edge exchange of an 8-rank shard, each walking ~3 K rows in a dependent loop; 8
-// blocks per shard with a separate reset kernel took 8.3 + 4.9 us
-// (profiles/r04_rank_replay.txt).
-constexpr uint32_t kStageBS = 1024;
+// Stage the sharded delta list as contiguous records. grid = kShards blocks: block s
+// copies shard s to its prefix position (deterministic, no append atomics); rows past
+// `cap` are dropped (the count says how many there were). Block 0 writes the count word
+// (| kFailBit when with_fail and the verdict failed: the exchange carries the verdict,
+// Candidates.merge :79-81); the last block (a ticket of kShards same-address atomics)
+// resets the shard counters. Block size (profiles/r04_rank_replay.txt): alone, 1024
+// threads copy an 8-rank shard's exchange in 13 us against 22 with 256; but in the
+// exchange step the stage runs beside the folds, and 64 blocks of 1024 threads took
+// slots the folds needed (one-rank RCCL step 46.9-47.5 ms vs 42.2-42.9 with 256).
+#ifndef GS_STAGE_BS
+#define GS_STAGE_BS 256  // threads per k_stage block (experiment switch)
+#endif
+constexpr uint32_t kStageBS = GS_STAGE_BS;
 __global__ __launch_bounds__(kStageBS) void k_stage(Table t, Delta D, int64_t* __restrict__ out, uint64_t cap,
                                                     int width, unsigned long long* count_out, int with_fail) {
   __shared__ uint32_t cnt[kShards];
