@@ -623,6 +623,14 @@ def bench_ingest(args):
     ok = n == E and bad == -1 and bool(torch.equal(ps, src)) and bool(torch.equal(pd, dst))
     nbytes = int(text.numel())
     alg = nbytes + 16 * E  # text read once + int64 pair written per edge
+    # the parse kernel's own duration, HIP events around it inside gs_parse_edges_device
+    # (an extra pass after the timed region: the events add a synchronisation per parse)
+    gs.parse_set_profiling(True)
+    for _ in range(max(3, args.steps)):
+        gs.parse_edges_device(text, ps, pd)
+    k_us_tot, k_n = gs.parse_profile()
+    gs.parse_set_profiling(False)
+    k_us = k_us_tot / max(k_n, 1)
     with gs.Summary("cc", device=0, capacity_hint=1 << 24) as summ:
         th = bytes(text_h)
         t1 = time.perf_counter()
@@ -634,9 +642,15 @@ def bench_ingest(args):
     c0 = time.perf_counter()
     oracle.parse_edges(sample, 0)
     cpu_el = time.perf_counter() - c0
-    roof = {"kernel": "k_parse_fused (one pass: decoupled look-back over the tiles' line counts)", "bound": "hbm", "achieved": round(alg / el / 1e9, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / el / 1e9 / HBM_PEAK_GBS, 4),
-            "traffic": None, "note": "algorithmic bytes = text + 16 B/edge; wall time incl. sync"}
+    roof = {"kernel": "k_parse_fused (one pass: decoupled look-back over the tiles' line counts)", "bound": "hbm",
+            "achieved": round(alg / k_us / 1e3, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg / k_us / 1e3 / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel_avg_us": round(k_us, 2), "kernel_launches_timed": k_n,
+            "achieved_wall": round(alg / el / 1e9, 1), "frac_wall": round(alg / el / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "algorithmic bytes = text + 16 B/edge per parse; achieved = those bytes / the parse kernel's "
+                    "average duration (HIP events around k_parse_fused, gs_parse_set_profiling, an untimed pass); "
+                    "achieved_wall = the same bytes / the timed per-call wall time (launches, the result kernel "
+                    "and the host's poll of the mapped result included)"}
     pm, extra = _matching_pmc("pmc_ingest_traffic.json", {"workload": "ingest-rmat26-text"})
     if pm is not None:  # the parse's fabric bytes (+ a count pass's, two-pass builds), its VALU/LDS activity
         t_parse, extra = _traffic_fields(pm, 0, 0)

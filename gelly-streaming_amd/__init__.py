@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "gs_take_delta_records", "gs_fold_take_device", "gs_delta_stage", "gs_fold_records_device", "gs_fold_exchange_device",
     "gs_get_stream", "gs_set_pipelining", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity", "gs_counters",
     "gs_gen_rmat", "gs_gen_er", "gs_gen_bip",
-    "gs_parse_edges_device", "gs_fold_text",
+    "gs_parse_edges_device", "gs_fold_text", "gs_parse_set_profiling", "gs_parse_profile",
     "gs_group_unique_id", "gs_group_create", "gs_group_fold_device", "gs_group_finish", "gs_group_stats",
     "gs_group_destroy", "gs_group_tree_combine", "gs_combine_exported_device",
     "gs_group_fold_batches_device", "gs_group_set_ramp", "gs_export_labels_part_device",
@@ -145,6 +145,8 @@ def lib():
     L.gs_gen_bip.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, _vp, _sz]
     L.gs_parse_edges_device.argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp, _vp, _sz, ctypes.POINTER(_u64),
                                         ctypes.POINTER(_i64)]
+    L.gs_parse_set_profiling.argtypes = [ctypes.c_int]
+    L.gs_parse_profile.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]
     L.gs_fold_text.argtypes = [_vp, ctypes.c_char_p, _sz, ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(_i64)]
     L.gs_group_unique_id.argtypes = [_vp]
     L.gs_group_create.argtypes = [ctypes.POINTER(_vp), _vp, _vp, ctypes.c_int, ctypes.c_int, _sz]
@@ -608,6 +610,23 @@ def parse_edges_device(text, src, dst, sep=SEP_WHITESPACE, stream=None):
     if rc not in (GS_OK, GS_ERR_PARSE, GS_ERR_TRUNCATED):
         raise GSError(rc, "gs_parse_edges_device failed")
     return n.value, bad.value
+
+
+def parse_set_profiling(on):
+    """gs_parse_set_profiling: time each parse kernel of this thread with HIP events."""
+    rc = lib().gs_parse_set_profiling(1 if on else 0)
+    if rc:
+        raise GSError(rc, "gs_parse_set_profiling failed")
+
+
+def parse_profile():
+    """gs_parse_profile: (summed parse-kernel microseconds, parses) since profiling was turned on."""
+    us = ctypes.c_double()
+    n = _u64()
+    rc = lib().gs_parse_profile(ctypes.byref(us), ctypes.byref(n))
+    if rc:
+        raise GSError(rc, "gs_parse_profile failed")
+    return us.value, n.value
 
 
 def gen_rmat(src, dst, start, count, scale, seed, scramble=True, stream=None):

@@ -629,7 +629,8 @@ __global__ void k_parse_result(const uint64_t* tile_pre, const uint64_t* tile_cn
 }
 
 int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, int64_t* src, int64_t* dst, size_t cap,
-                       ParseScratch& s, unsigned long long* host_res, unsigned long long seq, bool fused) {
+                       ParseScratch& s, unsigned long long* host_res, unsigned long long seq, bool fused,
+                       hipEvent_t kev0, hipEvent_t kev1) {
   if (len == 0) return hipMemsetAsync(s.res, 0xFF, 16, st) == hipSuccess &&
                         hipMemsetAsync(s.res, 0, 8, st) == hipSuccess ? 0 : -1;
   const uint64_t tiles = (len + kTile - 1) / kTile;
@@ -644,8 +645,10 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
     s.bad_ready = true;
     unsigned long long* agg = reinterpret_cast<unsigned long long*>(s.tile_cnt);
     unsigned long long* pre = reinterpret_cast<unsigned long long*>(s.tile_pre);
+    if (kev0 && hipEventRecord(kev0, st) != hipSuccess) return -1;
     hipLaunchKernelGGL(k_parse_fused, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, src, dst,
                        (uint64_t)cap, s.bad, aligned, agg, pre);
+    if (kev1 && hipEventRecord(kev1, st) != hipSuccess) return -1;
     hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
                        s.bad, s.res, host_res, seq, pre);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -715,6 +718,11 @@ struct ParseCache {
   unsigned long long* host = nullptr;  // mapped {seq, lines, bad}
   unsigned long long* host_dev = nullptr;
   unsigned long long seq = 0;
+  // gs_parse_set_profiling: the parse kernel between two events, summed
+  bool prof = false;
+  hipEvent_t kev[2] = {nullptr, nullptr};
+  double prof_us = 0.0;
+  uint64_t prof_n = 0;
 };
 thread_local ParseCache t_parse;
 
@@ -761,7 +769,9 @@ extern "C" int gs_parse_edges_device(void* stream, const char* text, size_t len,
     const char* e = getenv("GS_PARSE_MODE");
     return !(e && atoi(e) == 0);
   }();
-  const int rc = gs::parse_text_enqueue(st, text, len, sep, src, dst, cap, c.s, c.host_dev, seq, one_pass);
+  const bool prof = c.prof && one_pass;
+  const int rc = gs::parse_text_enqueue(st, text, len, sep, src, dst, cap, c.s, c.host_dev, seq, one_pass,
+                                        prof ? c.kev[0] : nullptr, prof ? c.kev[1] : nullptr);
   if (rc) return GS_ERR_HIP;
   // spin on the mapped record; a long parse hands over to the stream synchronisation
   const auto t0 = std::chrono::steady_clock::now();
@@ -777,7 +787,33 @@ extern "C" int gs_parse_edges_device(void* stream, const char* text, size_t len,
   *n_lines = __atomic_load_n(c.host + 1, __ATOMIC_ACQUIRE);
   const unsigned long long b = __atomic_load_n(c.host + 2, __ATOMIC_ACQUIRE);
   *bad_line = b == ~0ull ? -1 : (int64_t)b;
+  if (prof) {
+    float ms = 0.f;
+    if (hipEventSynchronize(c.kev[1]) != hipSuccess || hipEventElapsedTime(&ms, c.kev[0], c.kev[1]) != hipSuccess)
+      return GS_ERR_HIP;
+    c.prof_us += 1e3 * (double)ms;
+    ++c.prof_n;
+  }
   if (*bad_line >= 0) return GS_ERR_PARSE;
   if (*n_lines > cap) return GS_ERR_TRUNCATED;
+  return GS_OK;
+}
+
+extern "C" int gs_parse_set_profiling(int on) {
+  ParseCache& c = t_parse;
+  if (on && !c.kev[0]) {
+    for (hipEvent_t& e : c.kev)
+      if (hipEventCreate(&e) != hipSuccess) return GS_ERR_HIP;  // timing events
+  }
+  c.prof = on != 0;
+  c.prof_us = 0.0;
+  c.prof_n = 0;
+  return GS_OK;
+}
+
+extern "C" int gs_parse_profile(double* kernel_us, uint64_t* parses) {
+  if (!kernel_us || !parses) return GS_ERR_INVALID;
+  *kernel_us = t_parse.prof_us;
+  *parses = t_parse.prof_n;
   return GS_OK;
 }

@@ -26,7 +26,8 @@ int parse_scratch_init(ParseScratch& s, void* mem, size_t max_len);
 // Returns 0 or -1 (HIP failure).
 int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, int64_t* src, int64_t* dst, size_t cap,
                        ParseScratch& s,
-                       unsigned long long* host_res = nullptr, unsigned long long seq = 0, bool fused = true);
+                       unsigned long long* host_res = nullptr, unsigned long long seq = 0, bool fused = true,
+                       hipEvent_t kev0 = nullptr, hipEvent_t kev1 = nullptr);  // optional: bracket the parse kernel
 // Parse device text; synchronises st. Returns 0 or -1 (HIP failure).
 int parse_text(hipStream_t st, const char* text, size_t len, int sep, int64_t* src, int64_t* dst, size_t cap,
                ParseScratch& s, uint64_t* n_lines, int64_t* bad_line);

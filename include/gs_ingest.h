@@ -53,6 +53,13 @@ int gs_parse_edges_device(void* stream, const char* text, size_t len, int sep, i
  * records before its map threw). */
 int gs_fold_text(gs_handle h, const char* text, size_t len, int sep, uint64_t* n_edges, int64_t* bad_line);
 
+/* Kernel timing of gs_parse_edges_device (measurement; per calling thread): with it on,
+ * each parse brackets its parse kernel with HIP events, and gs_parse_profile returns
+ * the summed kernel time (microseconds) and the number of parses since it was turned
+ * on. Off by default (the events cost a synchronisation per parse). */
+int gs_parse_set_profiling(int on);
+int gs_parse_profile(double* kernel_us, uint64_t* parses);
+
 #ifdef __cplusplus
 }
 #endif

@@ -197,3 +197,20 @@ def test_parse_malformed_then_clean_reuses_scratch(gs, oracle_mod):
         s, d, n, b = _gpu_parse(gs, text, 0)
         assert (n, b) == (en, eb), (len(text), n, b, en, eb)
         assert np.array_equal(s, es) and np.array_equal(d, ed)
+
+
+def test_parse_profiling_counts_kernel_time(gs):
+    """gs_parse_set_profiling / gs_parse_profile (the bench's roofline timing): each
+    parse adds its kernel time; turning it on again starts from zero."""
+    rng = np.random.default_rng(12)
+    text = _random_text(rng, 20000, 0)
+    gs.parse_set_profiling(True)
+    for _ in range(3):
+        _gpu_parse(gs, text, 0)
+    us, n = gs.parse_profile()
+    assert n == 3 and us > 0.0
+    gs.parse_set_profiling(True)
+    assert gs.parse_profile() == (0.0, 0)
+    gs.parse_set_profiling(False)
+    _gpu_parse(gs, text, 0)
+    assert gs.parse_profile()[1] == 0
