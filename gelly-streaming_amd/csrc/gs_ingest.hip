@@ -300,6 +300,12 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
 // is read once instead of twice (the count pass was 126 us of a 684 MB parse).
 
 constexpr unsigned long long kStP = 1ull << 63, kStA = 1ull << 62, kStVal = (1ull << 62) - 1;
+#ifndef GS_LB_SLEEP0
+#define GS_LB_SLEEP0 8  // look-back back-off: s_sleep of the first three unsuccessful rounds (experiment switch)
+#endif
+#ifndef GS_LB_SLEEP1
+#define GS_LB_SLEEP1 64  // ... and of the later ones
+#endif
 // Early aggregates: a tile that lies wholly inside the text publishes its '\n' count as
 // soon as its staging loads arrive, before the LDS staging, masks and scan: each wave adds
 // (1 << kStWaveShift) | (its count) to the tile's status word, and the aggregate is
@@ -381,9 +387,9 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
       break;
     }
     if (backoff < 3) {
-      __builtin_amdgcn_s_sleep(8);
+      __builtin_amdgcn_s_sleep(GS_LB_SLEEP0);
     } else {
-      __builtin_amdgcn_s_sleep(64);
+      __builtin_amdgcn_s_sleep(GS_LB_SLEEP1);
     }
     ++backoff;
   }
