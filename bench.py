@@ -160,6 +160,10 @@ def parse():
                    help="native: RCCL inside libgs_summary (gs_group_*); torch: torch.distributed all-gather")
     p.add_argument("--er-mode", choices=["launch", "server"], default="server",
                    help="er-latency: which window mode `value` reports (both are measured)")
+    p.add_argument("--profile-serial", action="store_true",
+                   help="with --profile-only: after the timed steps, run the roofline's serialised pass (HIP events "
+                        "around every k_fold launch) and stop; with --steps 0 a kernel trace then holds only that "
+                        "pass, whose k_fold average is the line's fold_avg_us")
     p.add_argument("--profile-only", action="store_true",
                    help="profiling runs (tools/pmc_workload.sh): only the timed work -- no checks, no host legs, "
                         "so that every dispatch of the profiled kernel is of the measured shape")
@@ -828,6 +832,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if args.profile_only:  # profiling / tracing run: the timed steps only
+        if args.profile_serial and not grouped:  # (+ the roofline's serialised pass)
+            summ.set_profiling(True)
+            one_step()
+            summ.sync()
+            nf, fold_ms = summ.kernel_stats("fold")
+            summ.set_profiling(False)
+            print(json.dumps({"serial_pass_fold_launches": int(nf), "fold_avg_us": round(fold_ms * 1e3 / max(nf, 1), 2)}),
+                  flush=True)
         if isinstance(xch, NativeExchange):
             xch.g.close()
         summ.close()
