@@ -54,7 +54,13 @@ constexpr int kDeltaSets = GS_DELTA_SETS;
 #define GS_WAVE_APPEND 1  // 0: one append atomic per record (experiment switch)
 #endif
 #ifndef GS_INSERT_TTAS
-#define GS_INSERT_TTAS 1
+// The agent-scope re-read of an EMPTY-looking slot before its key CAS (test-and-test-and-set)
+// in throughput folds. Off since the paired key CASes: with both endpoints' CASes in flight
+// together the re-read costs more than the hub CASes it avoids (serialised k_fold -4.7 %
+// on RMAT-26, -4 % on RMAT-20; steps -0.5 / -1.9 / -0.5 % on configs 3 / 2 / 4 over three
+// interleaved rounds, profiles/r04_insert_path_ab.txt). Before them it was the other way
+// round (RMAT-20 0.656 vs 0.690 ms, profiles/r04_hook_ttas_ab.txt).
+#define GS_INSERT_TTAS 0
 #endif
 enum CounterBlock : int {
   CTR_NV = 0,                    // [kShards] new-vertex counts (= vertex-list fill per shard)
@@ -172,11 +178,11 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
       return h;
     }
     // An EMPTY read may be a stale line of a slot another XCD has filled; the CAS settles
-    // it (it returns the winner's key). Throughput folds first re-read the slot with an
-    // agent-scope load (test-and-test-and-set): all of a hub's occurrences in a young
-    // table's batch would otherwise queue CASes on its slot (RMAT-20: 0.656 vs 0.690
-    // ms/step without). The window takes (TAKE) skip the re-read: one round trip less per
-    // insert (config 5 p50 13.6 -> 12.9 us, p99 27.1 -> 25.5; profiles/r03_insert_ab.txt).
+    // it (it returns the winner's key). With TTAS (GS_INSERT_TTAS, off by default since
+    // the paired key CASes) a throughput fold first re-reads the slot with an agent-scope
+    // load, so that a hub's occurrences in a young table's batch do not queue CASes on
+    // its slot. The window takes (TAKE) never re-read: one round trip less per insert
+    // (config 5 p50 13.6 -> 12.9 us, p99 27.1 -> 25.5; profiles/r03_insert_ab.txt).
     if (TTAS && k == kEmpty) {
       k = (int64_t)__hip_atomic_load((unsigned long long*)&t.tab[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (k == key) {
