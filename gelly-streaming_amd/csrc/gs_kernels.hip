@@ -462,10 +462,12 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   uint32_t su = kNoSlot, sv = kNoSlot;
   if (valid) {
     if (GS_PAIR_INSERT && k0u == kEmpty && k0v == kEmpty && hu != hv && ks != kd && ks != kEmpty && kd != kEmpty) {
-      insert_pair<!TAKE && GS_INSERT_TTAS>(t, ks, hu, kd, hv, su, lu, nu, sv, lv, nv);
+      insert_pair<!TAKE && (GS_INSERT_TTAS || TRACK)>(t, ks, hu, kd, hv, su, lu, nu, sv, lv, nv);
     } else {
-      su = lookup_resolve<!TAKE && GS_INSERT_TTAS>(t, ks, hu, k0u, l0u, lu, nu);
-      sv = lookup_resolve<!TAKE && GS_INSERT_TTAS>(t, kd, hv, k0v, l0v, lv, nv);
+      // (the re-read stays in the exchange's tracked own folds: one-rank RCCL step 42.6-43.2
+      // with it vs 43.7-43.8 ms without, profiles/r04_insert_path_ab.txt section 7)
+      su = lookup_resolve<!TAKE && (GS_INSERT_TTAS || TRACK)>(t, ks, hu, k0u, l0u, lu, nu);
+      sv = lookup_resolve<!TAKE && (GS_INSERT_TTAS || TRACK)>(t, kd, hv, k0v, l0v, lv, nv);
     }
   }
   nvx = reserve_new_vertices(t, shard, nu, su, nv, sv, TAKE ? D.lnv : nullptr);  // one atomic per wave
