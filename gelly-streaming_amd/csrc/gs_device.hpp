@@ -59,7 +59,8 @@ constexpr int kDeltaSets = GS_DELTA_SETS;
 // together the re-read costs more than the hub CASes it avoids (serialised k_fold -4.7 %
 // on RMAT-26, -4 % on RMAT-20; steps -0.5 / -1.9 / -0.5 % on configs 3 / 2 / 4 over three
 // interleaved rounds, profiles/r04_insert_path_ab.txt). Before them it was the other way
-// round (RMAT-20 0.656 vs 0.690 ms, profiles/r04_hook_ttas_ab.txt).
+// round (RMAT-20 0.656 vs 0.690 ms, profiles/r04_hook_ttas_ab.txt). The exchange's tracked
+// own folds keep it regardless (fold_block: GS_INSERT_TTAS || TRACK).
 #define GS_INSERT_TTAS 0
 #endif
 enum CounterBlock : int {
