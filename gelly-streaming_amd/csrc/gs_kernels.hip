@@ -353,11 +353,13 @@ __device__ __forceinline__ bool take_tail(const Table& t, const FoldArgs& a, con
   return true;
 }
 
-template <bool SIGNED, bool TRACK, bool TAKE>
+template <bool SIGNED, bool TRACK, bool TAKE, bool ROWS = false>
 __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const FoldArgs& a, uint32_t blk,
                                            bool failed, unsigned long long n_word, uint32_t* dbg);
 
-template <bool SIGNED, bool TRACK, bool TAKE>
+// ROWS: a group's gathered remote rows (exchange layout); they keep the insert re-read
+// (profiles/r04_rank_replay.txt section 8: 47 M rows fold in 2.86 ms with it, 3.94 without)
+template <bool SIGNED, bool TRACK, bool TAKE, bool ROWS = false>
 __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) {
   __shared__ int64_t lrec[TAKE ? kFoldBS * 3 : 1];
   __shared__ uint32_t lcnt;
@@ -387,9 +389,9 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
   const bool failed = SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0;
   if (failed && !TAKE) return;
 #ifdef GS_BLOCKLOG
-  fold_block<SIGNED, TRACK, TAKE>(t, D, a, blockIdx.x, failed, n_word, SIGNED ? nullptr : dbg);
+  fold_block<SIGNED, TRACK, TAKE, ROWS>(t, D, a, blockIdx.x, failed, n_word, SIGNED ? nullptr : dbg);
 #else
-  fold_block<SIGNED, TRACK, TAKE>(t, D, a, blockIdx.x, failed, n_word, nullptr);
+  fold_block<SIGNED, TRACK, TAKE, ROWS>(t, D, a, blockIdx.x, failed, n_word, nullptr);
 #endif
 #ifdef GS_BLOCKLOG
   if (!SIGNED) {
@@ -423,7 +425,7 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
 
 // The fold of one block's edges (edge i = blk * kFoldBS + threadIdx.x): relabel probes,
 // shortcut, finds, wave-combined hooks. Shared by k_fold and the resident window server.
-template <bool SIGNED, bool TRACK, bool TAKE>
+template <bool SIGNED, bool TRACK, bool TAKE, bool ROWS>
 __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const FoldArgs& a, uint32_t blk,
                                            bool failed, unsigned long long n_word, uint32_t* dbg) {
   const int shard = (int)((blk + a.shard0) & (kShards - 1));
@@ -462,12 +464,12 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   uint32_t su = kNoSlot, sv = kNoSlot;
   if (valid) {
     if (GS_PAIR_INSERT && k0u == kEmpty && k0v == kEmpty && hu != hv && ks != kd && ks != kEmpty && kd != kEmpty) {
-      insert_pair<!TAKE && (GS_INSERT_TTAS || TRACK)>(t, ks, hu, kd, hv, su, lu, nu, sv, lv, nv);
+      insert_pair<!TAKE && (GS_INSERT_TTAS || TRACK || ROWS)>(t, ks, hu, kd, hv, su, lu, nu, sv, lv, nv);
     } else {
       // (the re-read stays in the exchange's tracked own folds: one-rank RCCL step 42.6-43.2
       // with it vs 43.7-43.8 ms without, profiles/r04_insert_path_ab.txt section 7)
-      su = lookup_resolve<!TAKE && (GS_INSERT_TTAS || TRACK)>(t, ks, hu, k0u, l0u, lu, nu);
-      sv = lookup_resolve<!TAKE && (GS_INSERT_TTAS || TRACK)>(t, kd, hv, k0v, l0v, lv, nv);
+      su = lookup_resolve<!TAKE && (GS_INSERT_TTAS || TRACK || ROWS)>(t, ks, hu, k0u, l0u, lu, nu);
+      sv = lookup_resolve<!TAKE && (GS_INSERT_TTAS || TRACK || ROWS)>(t, kd, hv, k0v, l0v, lv, nv);
     }
   }
   nvx = reserve_new_vertices(t, shard, nu, su, nv, sv, TAKE ? D.lnv : nullptr);  // one atomic per wave
@@ -1119,6 +1121,11 @@ void launch_fold(bool sign, bool track, const Table& t, const Delta& D, const Fo
   if (f.take_out) {  // fused window take (always tracked)
     if (sign) hipLaunchKernelGGL((k_fold<true, true, true>), g, b, 0, st, t, D, a);
     else hipLaunchKernelGGL((k_fold<false, true, true>), g, b, 0, st, t, D, a);
+    return;
+  }
+  if ((f.rows || f.stride == 3) && !track) {  // other replicas' rows (a group's exchange layout, or 24-B records)
+    if (sign) hipLaunchKernelGGL((k_fold<true, false, false, true>), g, b, 0, st, t, D, a);
+    else hipLaunchKernelGGL((k_fold<false, false, false, true>), g, b, 0, st, t, D, a);
     return;
   }
   if (!sign && !track) hipLaunchKernelGGL((k_fold<false, false, false>), g, b, 0, st, t, D, a);
