@@ -133,6 +133,8 @@ TARGET = {"rmat-cc": ("k_fold<false, false, false>", "rmat26-cc-stream", "pmc_fo
 kname, wname, fname = TARGET
 if workload == "ingest" and "k_parse_fused" in out["kernels"]:  # the one-pass parse (round 4 default)
     kname = "k_parse_fused"
+if kname not in out["kernels"] and kname.endswith(">") and kname[:-1] + ", false>" in out["kernels"]:
+    kname = kname[:-1] + ", false>"  # k_fold<SIGNED, TRACK, TAKE, ROWS> (round 4: the ROWS instantiation)
 r = out["kernels"].get(kname, {})
 if "derived" in r and r["derived"].get("read_requests"):
     import hashlib
