@@ -156,6 +156,11 @@ def parse():
     p.add_argument("--ramp-log-batch", type=int, default=20)
     p.add_argument("--capacity-log2", type=int, default=0,
                    help="relabel-table capacity hint of the CC summary (log2 vertices; 0: 2^scale)")
+    p.add_argument("--rccl-max-channels", type=int, default=0,
+                   help="NCCL_MAX_NCHANNELS of the RCCL communicators (0: RCCL's default). Set in this process's "
+                        "environment before anything initialises HIP or RCCL, inherited by every rank; reported in "
+                        "config.rccl. RCCL's collective kernels run beside the fold lanes and hold CU slots the "
+                        "folds need (DESIGN.md section 5)")
     p.add_argument("--exchange-impl", choices=["native", "torch"], default="native",
                    help="native: RCCL inside libgs_summary (gs_group_*); torch: torch.distributed all-gather")
     p.add_argument("--er-mode", choices=["launch", "server"], default="server",
@@ -223,11 +228,18 @@ def launch_check(args):
     group, world counted by an all-reduce, one JSON line on rank 0."""
     world, rank, _ = check_world(args)
     checks = None
+    rccl = rccl_setting()
     if world > 1:
         dist.init_process_group("gloo")
         t = torch.ones(1)
         dist.all_reduce(t)
         formed = int(t.item())
+        # every rank would create its communicators with the same channel cap
+        ch = rccl["NCCL_MAX_NCHANNELS"] or 0
+        lo, hi = torch.tensor([ch]), torch.tensor([ch])
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        rccl["same_on_all_ranks"] = int(lo.item()) == int(hi.item())
         if args.launch_check_digest is not None:
             d = (args.launch_check_digest + rank * args.launch_check_digest_skew) % (1 << 64)
             checks = replica_digest_checks(d, world, args.launch_check_digest, torch.device("cpu"))
@@ -237,7 +249,7 @@ def launch_check(args):
     if formed != args.gpus:
         raise SystemExit("--gpus %d but %d rank(s) joined" % (args.gpus, formed))
     if rank == 0:
-        line = {"launch_check": True, "n_gpus": formed, "workload": args.workload}
+        line = {"launch_check": True, "n_gpus": formed, "workload": args.workload, "rccl": rccl}
         if checks is not None:
             line["self_check"] = checks
         print(json.dumps(line), flush=True)
@@ -436,6 +448,7 @@ def bench_bip(args):
             cfg.update({"verdict_parity": agree and oks[0] and oks[1] == (first < 0),
                         "parallelism": "edge-shard x%d, per-batch signed delta all-gather (native group)" % world})
         cfg["clean_stream_digest"] = dig
+        cfg["rccl"] = rccl_setting() if group is not None else None
         cfg["ids"] = "first-appearance order (SURVEY.md 8(d) config 4: the reference's exact regime)"
         cfg["reference_quirk_check"] = {
             "prefix_edges": cap, "diverges": div["diverges"], "gpu_equals_reference": gpu_str == div["quirk"],
@@ -729,8 +742,18 @@ def bench_dropin(args):
     print(json.dumps(line), flush=True)
 
 
+def rccl_setting():
+    """config.rccl: the channel cap every communicator of this process was created with (the env
+    RCCL reads at communicator creation; None = RCCL's default)."""
+    v = os.environ.get("NCCL_MAX_NCHANNELS")
+    return {"NCCL_MAX_NCHANNELS": int(v) if v else None}
+
+
 def main():
     args = parse()
+    if args.rccl_max_channels > 0:
+        # before anything touches HIP or RCCL (the ranks of self_launch inherit it, and parse it again)
+        os.environ["NCCL_MAX_NCHANNELS"] = str(args.rccl_max_channels)
     if args.seed is None:
         args.seed = 0x5EED0020 if args.scale == 20 else 0x5EED0026
     rc = self_launch(args)
@@ -1020,6 +1043,7 @@ def main():
                        "capacity_hint": 1 << (args.capacity_log2 or xlog),
                        "vertices_labelled": int(labelled), "self_check": checks, "exchange_phases": phases,
                        "pcie_inclusive": pcie,
+                       "rccl": rccl_setting() if grouped else None,
                        "parallelism": ("edge-shard x%d, per-batch delta all-gather (%s)" % (world, args.exchange_impl))
                        if xch is not None else "single GPU"},
             "roofline": roof,

@@ -47,9 +47,9 @@ EXPORTED_SYMBOLS = (
     "gs_combine", "gs_sync", "gs_num_vertices", "gs_find", "gs_export_labels", "gs_export_labels_device",
     "gs_bip_status", "gs_export_colouring", "gs_serialize", "gs_deserialize", "gs_set_delta_tracking",
     "gs_take_delta_records", "gs_fold_take_device", "gs_delta_stage", "gs_fold_records_device", "gs_fold_exchange_device",
-    "gs_get_stream", "gs_set_pipelining", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity", "gs_counters",
+    "gs_get_stream", "gs_set_pipelining", "gs_set_profiling", "gs_kernel_stats", "gs_table_capacity", "gs_counters", "gs_debug_counters",
     "gs_gen_rmat", "gs_gen_er", "gs_gen_bip",
-    "gs_parse_edges_device", "gs_fold_text", "gs_parse_set_profiling", "gs_parse_profile",
+    "gs_parse_edges_device", "gs_fold_text", "gs_parse_set_profiling", "gs_parse_profile", "gs_parse_release",
     "gs_group_unique_id", "gs_group_create", "gs_group_fold_device", "gs_group_finish", "gs_group_stats",
     "gs_group_destroy", "gs_group_tree_combine", "gs_combine_exported_device",
     "gs_group_fold_batches_device", "gs_group_set_ramp", "gs_export_labels_part_device",
@@ -140,6 +140,7 @@ def lib():
     L.gs_kernel_stats.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double)]
     L.gs_table_capacity.argtypes = [_vp, ctypes.POINTER(_u64)]
     L.gs_counters.argtypes = [_vp, ctypes.POINTER(_u64)]
+    L.gs_debug_counters.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.c_int]
     L.gs_gen_rmat.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, ctypes.c_int]
     L.gs_gen_er.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, ctypes.c_int]
     L.gs_gen_bip.argtypes = [_vp, _vp, _vp, _u64, _u64, ctypes.c_int, _u64, _vp, _sz]
@@ -506,6 +507,14 @@ class Summary:
         keys = ("vertices", "failed", "err", "ovf", "sent", "hooks", "hook_iters", "cas_fail")
         return dict(zip(keys, list(a)))
 
+    def debug_counters(self):
+        """Fold diagnostics (gs_debug_counters; debug build only, zeros otherwise)."""
+        a = (_u64 * 16)()
+        _check(lib().gs_debug_counters(self._h, a, 16))
+        keys = ("edges", "key_cas", "key_cas_lost", "ttas", "shortcut", "same_root", "find_loads", "hooks_ok",
+                "extra_probes")
+        return dict(zip(keys, list(a)))
+
     def table_capacity(self):
         n = _u64()
         _check(lib().gs_table_capacity(self._h, ctypes.byref(n)))
@@ -627,6 +636,13 @@ def parse_profile():
     if rc:
         raise GSError(rc, "gs_parse_profile failed")
     return us.value, n.value
+
+
+def parse_release():
+    """gs_parse_release: free this thread's parse cache (device scratch, mapped record, events)."""
+    rc = lib().gs_parse_release()
+    if rc:
+        raise GSError(rc, "gs_parse_release failed")
 
 
 def gen_rmat(src, dst, start, count, scale, seed, scramble=True, stream=None):

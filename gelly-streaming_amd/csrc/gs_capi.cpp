@@ -358,9 +358,16 @@ int server_start(gs_summary* h) {
   // ~2 ms without a window: the launch leaves on its own (wall clock 100 MHz). It holds
   // its stream's hardware queue while resident, so another stream that shares the queue
   // waits at most that long behind an idle server (the config-5 windows arrive
-  // back to back; a restart costs one launch).
+  // back to back; a restart costs one launch). GS_SERVER_IDLE_US overrides it (tests of
+  // the exit paths with late workgroups).
+  const char* idle_env = getenv("GS_SERVER_IDLE_US");  // read per start: a server start is rare
+  const long long idle_us = idle_env ? atoll(idle_env) : 0;
+  const unsigned long long idle_ticks = idle_us > 0 ? (unsigned long long)idle_us * 100ull : 200000ull;
+  const char* late_env = getenv("GS_SERVER_LATE_US");  // test hook: the last workgroup starts this late
+  const long long late_us = late_env ? atoll(late_env) : 0;
   gs::launch_window_server(h->kind == GS_KIND_SIGNED, h->table(), h->delta(), h->srv_box, h->srv_bc, h->done_dev,
-                           h->srv_seq, 200000ull, h->stream);
+                           h->srv_seq, idle_ticks, late_us > 0 ? (unsigned long long)late_us * 100ull : 0ull,
+                           h->stream);
   GS_HIP(hipGetLastError());
   h->srv_running = true;
   h->srv_launches++;
@@ -479,6 +486,21 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       return fail(GS_ERR_CAPACITY, "delta list full: stage or take the delta records after at most " +
                                        std::to_string(h->delta_edges) + " folded edges");
   }
+  // Young-table head: the first plain fold of an empty table folds its first 2^14 edges alone
+  // on the handle stream, and every lane (this fold's rest and the next pipelined folds) waits
+  // for it. On an empty table every occurrence of a hub reads EMPTY and CASes the hub's key,
+  // and those same-address CASes serialise at the memory side (RMAT-20's first micro-batch:
+  // 258 K of its 524 K key CASes lost, 611 K failed hook CASes, 150 us against ~30 us for a
+  // later batch; tools/fold_stats.py). The head inserts the stream's hubs; the rest reads
+  // their keys. Config 2: 0.597 -> 0.552-0.558 ms/step; config 4 (uniform endpoints, no hubs)
+  // pays the head's latency: 0.852-0.857 -> 0.858-0.865 (profiles/r05_young_ab.txt).
+  // GS_YOUNG_HEAD_LOG2 = k overrides the size (0: off).
+  static const int young_head_log2 = [] {
+    const char* e = getenv("GS_YOUNG_HEAD_LOG2");
+    return e ? atoi(e) : 14;
+  }();
+  const bool young_head = young_head_log2 > 0 && check_cap && !track && fs.rows == 0 && !fs.take_out &&
+                          h->e_launched == 0 && h->nv_exact == 0 && n > ((size_t)2 << young_head_log2);
   if (check_cap && units) {
     if (int rc = ensure_capacity(h, units)) return rc;
   }
@@ -493,13 +515,16 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     if (int rc = join_pipe_lanes(h)) return rc;  // the side stream is NOT joined: union commutes
   }
   const bool sign = h->kind == GS_KIND_SIGNED;
-  for (size_t off = 0; off < n; off += kMaxChunk) {
-    const uint32_t c = (uint32_t)std::min<size_t>(kMaxChunk, n - off);
-    const uint32_t blocks = (c + gs::kFoldBS - 1) / gs::kFoldBS;
+  for (size_t off = 0, c = 0; off < n; off += c) {
+    const bool head = young_head && off == 0;
+    c = head ? ((size_t)1 << young_head_log2) : std::min<size_t>(kMaxChunk, n - off);
+    const uint32_t blocks = (uint32_t)((c + gs::kFoldBS - 1) / gs::kFoldBS);
     if (track && !fs.take_out) h->delta_fill_ub[h->dset] += per_shard_edges(c);  // (a fused take bypasses the set)
     hipStream_t st = side ? h->side : h->stream;
     if (side) h->side_dirty = true;
-    if (pipe) {  // the lane waits for the caller's work on the handle stream, not for the other lane
+    if (head) {
+      if (int rc = join_pipe_lanes(h)) return rc;  // (idle after a reset)
+    } else if (pipe) {  // the lane waits for the caller's work on the handle stream, not for the other lane
       st = h->lane[h->lane_next];
       h->lane_next = (h->lane_next + 1) % h->pipe_depth;
       // An idle handle stream has nothing to order behind: no marker. (With 4 hardware
@@ -613,7 +638,7 @@ int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t
     if (nparts == 1 && use_vertex_list(h, h->nv_ub))
       gs::launch_export_list(h->table(), v, l, p, cap, h->nv_ub, h->stream);
     else
-      gs::launch_export(h->table(), v, l, p, cap, h->stream, part, nparts);
+      gs::launch_export(h->table(), v, l, p, cap, h->stream, part, nparts, h->vlist_ok);
   }
   GS_HIP(hipGetLastError());
   uint64_t cnt = 0;
@@ -1127,7 +1152,7 @@ int gs_combine(gs_handle dst, gs_handle src) {
       if (use_vertex_list(src, bound))
         gs::launch_export_list(src->table(), src->x_v, src->x_l, src->x_p, src->x_cap, bound, src->stream);
       else
-        gs::launch_export(src->table(), src->x_v, src->x_l, src->x_p, src->x_cap, src->stream);
+        gs::launch_export(src->table(), src->x_v, src->x_l, src->x_p, src->x_cap, src->stream, 0, 1, src->vlist_ok);
     }
     GS_HIP(hipGetLastError());
     GS_HIP(hipMemcpyAsync(src->x_cnt, src->ctr + gs::ctr_index(gs::CTR_EXPORT), 4, hipMemcpyDeviceToDevice,
@@ -1306,7 +1331,8 @@ static int server_take(gs_handle h, const int64_t* src, const int64_t* dst, size
     h->srv_running = false;
     GS_HIP(hipStreamSynchronize(h->stream));  // join the launch that left
     if (__atomic_load_n(&b->taken, __ATOMIC_ACQUIRE) == seq && __atomic_load_n(h->h_done, __ATOMIC_ACQUIRE) < dseq) {
-      // It left INSIDE this window (a workgroup never became resident within ~2 s): some
+      // It left INSIDE this window (a workgroup did not become resident within 8 x the
+      // idle limit, ~16 ms): some
       // of the window's edges are folded and their rows written, the count word is not.
       // Replaying it would lose those hooks' records, so the window fails; the take
       // counters are cleared so that the handle's next take starts clean.
@@ -1486,6 +1512,19 @@ int gs_counters(gs_handle h, uint64_t* out8) {
   out8[5] = c[gs::ctr_index(gs::CTR_DBG_HOOKS)];
   out8[6] = c[gs::ctr_index(gs::CTR_DBG_ITERS)];
   out8[7] = c[gs::ctr_index(gs::CTR_DBG_CASFAIL)];
+  return GS_OK;
+}
+
+int gs_debug_counters(gs_handle h, uint64_t* out, int n) {
+  if (int rc = check(h)) return rc;
+  if (!out || n < 0) return fail(GS_ERR_INVALID, "out is null");
+  DeviceGuard g(h->device);
+  if (int rc_ = join_lanes(h)) return rc_;
+  std::vector<uint32_t> c(gs::CTR_COUNT * gs::kCtrStride);
+  GS_HIP(hipMemcpyAsync(c.data(), h->ctr, c.size() * 4, hipMemcpyDeviceToHost, h->stream));
+  GS_HIP(hipStreamSynchronize(h->stream));
+  const int have = gs::CTR_DBG_LAST_ - gs::CTR_DBG_EDGES;
+  for (int i = 0; i < n && i < 16; ++i) out[i] = i < have ? c[gs::ctr_index(gs::CTR_DBG_EDGES + i)] : 0;
   return GS_OK;
 }
 

@@ -89,9 +89,26 @@ enum CounterBlock : int {
   CTR_TAKE_SHARD,                // [kTicketShards] block tickets, first level (block b -> shard b mod 16)
   CTR_SRV_NV = CTR_TAKE_SHARD + 16,  // resident window server: vertices after its last window (u64)
   CTR_SRV_NV_HI,
+  // debug build only (-DGS_DEBUG_COUNTERS, gs_debug_counters): where a fold's memory operations go
+  CTR_DBG_EDGES,                 // valid edges / rows folded
+  CTR_DBG_KCAS,                  // key CASes issued (inserts)
+  CTR_DBG_KCAS_LOST,             //   ... that found the slot taken (another id, or this id by another lane)
+  CTR_DBG_TTAS,                  // agent-scope re-reads of an EMPTY-looking slot before its key CAS
+  CTR_DBG_SHORT,                 // edges settled by the shared-parent shortcut (no find)
+  CTR_DBG_SAME,                  // edges whose finds met one root (no hook)
+  CTR_DBG_FINDLD,                // parent loads of the finds (fold phase, before the hook)
+  CTR_DBG_HOOKOK,                // hooks whose CAS joined two trees
+  CTR_DBG_PROBES,                // extra linear-probe loads (beyond each endpoint's first)
+  CTR_DBG_LAST_,
   CTR_COUNT
 };
 __host__ __device__ constexpr int ctr_index(int c) { return c * kCtrStride; }
+
+#ifdef GS_DEBUG_COUNTERS
+#define GS_DBG(c) atomicAdd(&t.ctr[ctr_index(c)], 1u)
+#else
+#define GS_DBG(c) ((void)0)
+#endif
 
 // aux bits of a slot
 constexpr uint32_t kAuxPresent = 1u;  // reserved slot only: INT64_MIN is a vertex
@@ -185,6 +202,7 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
     // its slot. The window takes (TAKE) never re-read: one round trip less per insert
     // (config 5 p50 13.6 -> 12.9 us, p99 27.1 -> 25.5; profiles/r03_insert_ab.txt).
     if (TTAS && k == kEmpty) {
+      GS_DBG(CTR_DBG_TTAS);
       k = (int64_t)__hip_atomic_load((unsigned long long*)&t.tab[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (k == key) {
         link = load_link_fresh(t.tab + h);
@@ -192,8 +210,10 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
       }
     }
     if (k == kEmpty) {
+      GS_DBG(CTR_DBG_KCAS);
       const unsigned long long old =
           atomicCAS((unsigned long long*)&t.tab[h].key, (unsigned long long)kEmpty, (unsigned long long)key);
+      if (old != (unsigned long long)kEmpty) GS_DBG(CTR_DBG_KCAS_LOST);
       if (old == (unsigned long long)kEmpty) {
         fresh = true;
         if (t.mark_new) t.tab[h].aux = kAuxNew;  // only the inserting thread writes a fresh slot's aux
@@ -206,6 +226,7 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
       }
     }
     h = (h + 1) & t.mask;
+    GS_DBG(CTR_DBG_PROBES);
     load_slot(t.tab + h, k, l);
   }
   raise_flag(t, CTR_ERR, 0);
@@ -219,6 +240,7 @@ template <bool TTAS>
 __device__ __forceinline__ uint32_t insert_finish(const Table& t, int64_t key, uint32_t h, unsigned long long old,
                                                   bool tried, uint32_t& link, bool& fresh) {
   fresh = false;
+  if (tried && old != (unsigned long long)kEmpty) GS_DBG(CTR_DBG_KCAS_LOST);
   if (tried && old == (unsigned long long)kEmpty) {
     fresh = true;
     if (t.mark_new) t.tab[h].aux = kAuxNew;
@@ -232,6 +254,7 @@ __device__ __forceinline__ uint32_t insert_finish(const Table& t, int64_t key, u
   h = (h + 1) & t.mask;
   int64_t k;
   uint32_t l;
+  GS_DBG(CTR_DBG_PROBES);
   load_slot(t.tab + h, k, l);
   return lookup_resolve<TTAS>(t, key, h, k, l, link, fresh);
 }
@@ -250,6 +273,8 @@ __device__ __forceinline__ void insert_pair(const Table& t, int64_t ku, uint32_t
                                             bool& nv) {
   unsigned long long ou = (unsigned long long)kEmpty, ov = (unsigned long long)kEmpty;
   if (TTAS) {
+    GS_DBG(CTR_DBG_TTAS);
+    GS_DBG(CTR_DBG_TTAS);
     ou = __hip_atomic_load((unsigned long long*)&t.tab[hu].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ov = __hip_atomic_load((unsigned long long*)&t.tab[hv].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -261,6 +286,8 @@ __device__ __forceinline__ void insert_pair(const Table& t, int64_t ku, uint32_t
   const uint32_t tv32 = tv ? 1u : 0u;
   asm volatile("" ::"v"(tv32) : "memory");  // the second test is materialised here, before either CAS
   __builtin_amdgcn_sched_barrier(0);
+  if (tu) GS_DBG(CTR_DBG_KCAS);
+  if (tv32) GS_DBG(CTR_DBG_KCAS);
   if (tu) ou = atomicCAS((unsigned long long*)&t.tab[hu].key, (unsigned long long)kEmpty, (unsigned long long)ku);
   if (tv32) ov = atomicCAS((unsigned long long*)&t.tab[hv].key, (unsigned long long)kEmpty, (unsigned long long)kv);
   __builtin_amdgcn_sched_barrier(0);
@@ -400,6 +427,8 @@ __device__ __forceinline__ void find_root2(const Table& t, uint32_t& xa, uint32_
   while (!(da && db)) {
     int64_t kpa = 0, kpb = 0;
     uint32_t lpa = 0, lpb = 0;
+    if (!FRESH && !da) GS_DBG(CTR_DBG_FINDLD);
+    if (!FRESH && !db) GS_DBG(CTR_DBG_FINDLD);
     if (!da) load_slot(t.tab + (la >> 1), kpa, lpa);
     if (!db) load_slot(t.tab + (lb >> 1), kpb, lpb);
     if (FRESH) {
@@ -425,11 +454,6 @@ __device__ __forceinline__ uint32_t find_ro(const Table& t, uint32_t x, uint32_t
   return x;
 }
 
-#ifdef GS_DEBUG_COUNTERS
-#define GS_DBG(c) atomicAdd(&t.ctr[ctr_index(c)], 1u)
-#else
-#define GS_DBG(c) ((void)0)
-#endif
 
 // Wave-level combining of hooks that target the same root (the hub of a skewed
 // stream: while a giant component forms, most active edges of a wave are
@@ -566,6 +590,7 @@ __device__ __forceinline__ bool hook(const Table& t, uint32_t a, uint32_t la, in
     const uint32_t seen = own ? expect : load_link_fresh(t.tab + hi);
     const uint32_t old = seen == expect ? atomicCAS(&t.tab[hi].link, expect, desired) : seen;
     if (old == expect) {
+      GS_DBG(CTR_DBG_HOOKOK);
       if (TRACK) {
         rec[0] = a_lo ? kb : ka;
         rec[1] = a_lo ? ka : kb;

@@ -287,7 +287,8 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
                                            const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                            int64_t* __restrict__ dst, uint64_t cap,
                                            unsigned long long* __restrict__ bad, bool aligned, uint64_t tile,
-                                           unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat);
+                                           unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat,
+                                           unsigned long long lb_timeout);
 
 // Single pass (GS_PARSE_FUSED, default): no k_count_lines pass and no scan. Every block
 // counts its tile's '\n' from the masks it builds anyway and finds the count before its
@@ -343,7 +344,7 @@ __device__ __forceinline__ uint32_t nl_count16(const uint4& v) {
 // re-reading 64 status words at once slowed the other blocks' staging loads.
 __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restrict__ text, unsigned long long* status,
                                                         unsigned long long* pstat, uint64_t tile, unsigned long long agg,
-                                                        bool published) {
+                                                        bool published, unsigned long long lb_timeout) {
   const int lane = threadIdx.x & 63;
   if (tile == 0) {
     if (lane == 0) __hip_atomic_store(pstat, kStP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -377,10 +378,17 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
       base -= 64;  // the whole window was own counts: continue further back
       continue;
     }
-    if (wall_clock64() - t_start > 5000000ull) {  // ~50 ms (100 MHz clock): count it directly
+    if (wall_clock64() - t_start > lb_timeout) {  // ~50 ms (100 MHz clock) by default: count it directly
+      // every '\n' before the tile, 16 bytes per lane and load (one byte per lane
+      // and load made a late tile of a large text millions of dependent loads)
       unsigned long long c = 0;
       const uint64_t end = tile * kTile;
-      for (uint64_t q = (uint64_t)lane; q < end; q += 64) c += text[q] == '\n';
+      const uint64_t head = min(end, (uint64_t)((16u - ((uintptr_t)text & 15u)) & 15u));
+      for (uint64_t q = (uint64_t)lane; q < head; q += 64) c += text[q] == '\n';
+      const uint4* v16 = reinterpret_cast<const uint4*>(text + head);
+      const uint64_t n16 = (end - head) / 16;
+      for (uint64_t q = (uint64_t)lane; q < n16; q += 64) c += nl_count16(v16[q]);
+      for (uint64_t q = head + 16 * n16 + (uint64_t)lane; q < end; q += 64) c += text[q] == '\n';
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
       excl = c;
@@ -400,8 +408,9 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
 __global__ __launch_bounds__(256) void k_parse_fused(const uint8_t* __restrict__ text, uint64_t len, int sep,
                                                      int64_t* __restrict__ src, int64_t* __restrict__ dst, uint64_t cap,
                                                      unsigned long long* __restrict__ bad, bool aligned,
-                                                     unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat) {
-  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, blockIdx.x, status, pstat);
+                                                     unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat,
+                                                     unsigned long long lb_timeout) {
+  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, blockIdx.x, status, pstat, lb_timeout);
 }
 
 // One tile per block (44 VGPRs, 8 blocks per CU).
@@ -409,7 +418,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
                                                const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                                int64_t* __restrict__ dst, uint64_t cap,
                                                unsigned long long* __restrict__ bad, bool aligned, uint64_t tile0) {
-  parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile0 + blockIdx.x, nullptr, nullptr);
+  parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile0 + blockIdx.x, nullptr, nullptr, 0ull);
 }
 
 template <bool FUSED>
@@ -417,7 +426,8 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
                                            const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                            int64_t* __restrict__ dst, uint64_t cap,
                                            unsigned long long* __restrict__ bad, bool aligned, uint64_t tile,
-                                           unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat) {
+                                           unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat,
+                                           unsigned long long lb_timeout) {
   constexpr uint32_t kSeg = kTile / 256;  // bytes per thread in the line-start scan
   constexpr uint32_t kExtra = 2;          // '\n' masks past the tile: lines that cross its end
   constexpr uint32_t kSlots = (kTile + kOver + 4095) / 4096;
@@ -592,7 +602,8 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
     __shared__ unsigned long long pre_sh;
     if (wid == 0) {
       const unsigned long long e =
-          look_back(text, status, pstat, tile, (unsigned long long)wnl[0] + wnl[1] + wnl[2] + wnl[3], early);
+          look_back(text, status, pstat, tile, (unsigned long long)wnl[0] + wnl[1] + wnl[2] + wnl[3], early,
+                    lb_timeout);
       if (lane == 0) pre_sh = e;
     }
     __syncthreads();
@@ -652,8 +663,12 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
     unsigned long long* agg = reinterpret_cast<unsigned long long*>(s.tile_cnt);
     unsigned long long* pre = reinterpret_cast<unsigned long long*>(s.tile_pre);
     if (kev0 && hipEventRecord(kev0, st) != hipSuccess) return -1;
+    // GS_PARSE_LB_TIMEOUT_US (test hook, read per call): how long a look-back waits before it
+    // counts the '\n' before its tile itself (default ~50 ms; 0: at once)
+    const char* lbe = getenv("GS_PARSE_LB_TIMEOUT_US");
+    const unsigned long long lb_timeout = lbe ? 100ull * strtoull(lbe, nullptr, 10) : 5000000ull;
     hipLaunchKernelGGL(k_parse_fused, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, src, dst,
-                       (uint64_t)cap, s.bad, aligned, agg, pre);
+                       (uint64_t)cap, s.bad, aligned, agg, pre, lb_timeout);
     if (kev1 && hipEventRecord(kev1, st) != hipSuccess) return -1;
     hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
                        s.bad, s.res, host_res, seq, pre);
@@ -732,12 +747,32 @@ struct ParseCache {
 };
 thread_local ParseCache t_parse;
 
+// Free the cache's device scratch, mapped result record and timing events (on the device
+// they belong to). Safe between parses: gs_parse_edges_device returns only after the parse's
+// last kernel has written the mapped result, so nothing in flight still reads the scratch.
+int parse_cache_free(ParseCache& c) {
+  if (c.device < 0) return 0;
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) return -1;
+  if (cur != c.device && hipSetDevice(c.device) != hipSuccess) return -1;
+  int rc = 0;
+  if (c.mem && hipFree(c.mem) != hipSuccess) rc = -1;
+  if (c.host && hipHostFree(c.host) != hipSuccess) rc = -1;
+  for (hipEvent_t e : c.kev)
+    if (e && hipEventDestroy(e) != hipSuccess) rc = -1;
+  if (cur != c.device && hipSetDevice(cur) != hipSuccess) rc = -1;
+  c = ParseCache();
+  return rc;
+}
+
 int parse_cache_ready(hipStream_t st, size_t len) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return -1;
   ParseCache& c = t_parse;
-  if (c.device != dev) {  // (a thread moved to another device: the old scratch stays allocated there)
-    c = ParseCache();
+  if (c.device != dev) {  // first use, or the thread moved to another device: free the old device's cache
+    const bool prof = c.prof;
+    if (parse_cache_free(c)) return -1;
+    if (prof && gs_parse_set_profiling(1) != GS_OK) return -1;  // the timing events live on the new device
     c.device = dev;
     if (hipHostMalloc(&c.host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void**>(&c.host_dev), c.host, 0) != hipSuccess)
@@ -815,6 +850,10 @@ extern "C" int gs_parse_set_profiling(int on) {
   c.prof_us = 0.0;
   c.prof_n = 0;
   return GS_OK;
+}
+
+extern "C" int gs_parse_release(void) {
+  return parse_cache_free(t_parse) ? GS_ERR_HIP : GS_OK;
 }
 
 extern "C" int gs_parse_profile(double* kernel_us, uint64_t* parses) {

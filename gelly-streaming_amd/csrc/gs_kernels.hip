@@ -115,7 +115,10 @@ struct FoldArgs {
   bool server = false;  // resident window server: vertices carried by the tickets (take_tail)
 };
 
-constexpr int kCombineRounds = 2;  // wave-level hook combining (combine_hooks)
+#ifndef GS_COMBINE_ROUNDS
+#define GS_COMBINE_ROUNDS 2
+#endif
+constexpr int kCombineRounds = GS_COMBINE_ROUNDS;  // wave-level hook combining (combine_hooks)
 
 #ifdef GS_BLOCKLOG
 // Diagnostic build (make -C gelly-streaming_amd blocklog): every CC
@@ -463,6 +466,7 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   bool nu = false, nv = false;
   uint32_t su = kNoSlot, sv = kNoSlot;
   if (valid) {
+    GS_DBG(CTR_DBG_EDGES);
     if (GS_PAIR_INSERT && k0u == kEmpty && k0v == kEmpty && hu != hv && ks != kd && ks != kEmpty && kd != kEmpty) {
       insert_pair<!TAKE && (GS_INSERT_TTAS || TRACK || ROWS)>(t, ks, hu, kd, hv, su, lu, nu, sv, lv, nv);
     } else {
@@ -492,6 +496,7 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
     if (su != kNoSlot && sv != kNoSlot && su != sv) {  // a self-loop adds its vertex, never a conflict
       const uint32_t pu = lu >> 1, pv = lv >> 1;
       if (pu == pv || pu == sv || pv == su) {  // shared parent, or parent/child
+        GS_DBG(CTR_DBG_SHORT);
         if (SIGNED) {
           const uint32_t par = (pu == pv) ? ((lu ^ lv) & 1u) : (pu == sv ? (lu & 1u) : (lv & 1u));
           if ((need ^ par) & 1u) atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);
@@ -503,6 +508,7 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
         find_root2<false>(t, ru, lu, kru, pru, rv, lv, krv, prv);
         need ^= pru ^ prv;
         if (ru == rv) {
+          GS_DBG(CTR_DBG_SAME);
           if (SIGNED && (need & 1u)) atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);
         } else {
           act = true;
@@ -543,19 +549,30 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
 // (Round 3: descriptor loads after the poll and a drained broadcast cost 2.7 us of
 // every window: tools/server_trace.py.)
 // Exit conditions every wave reaches: a stop request, or no window for idle_ticks
-// (block 0 then tells the others and the host), or -- for the other blocks -- twice
-// that without any word from block 0. Block 0 does not leave idle while the last window
-// it handed out is incomplete (a workgroup that was not yet resident still has to fold
-// its edges: leaving would cut the window in half), except after 8 x idle_ticks; it
+// (block 0 then tells the others and the host), or -- for the other blocks -- 10 x
+// idle_ticks without any word from block 0. Block 0 does not leave idle while the last
+// window it handed out is incomplete (a workgroup that was not yet resident still has to
+// fold its edges: leaving would cut the window in half), except after 8 x idle_ticks; it
 // stores the seq of every window it takes in box->taken, so the host tells "left
-// before the window" (post it again) from "left inside it" (an error).
+// before the window" (post it again) from "left inside it" (an error). The other blocks'
+// own limit lies beyond block 0's longest stay: a window block 0 takes while
+// it waits for a late workgroup (its predecessor completes, the host posts the next one)
+// finds every other block still polling. Block 0 always broadcasts its exit, so the
+// others normally leave with it.
 template <bool SIGNED>
 __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, ServerBox* box, ServerBcast* bc,
                                                            unsigned long long* done, unsigned long long seq0,
-                                                           unsigned long long idle_ticks) {
+                                                           unsigned long long idle_ticks,
+                                                           unsigned long long late_ticks) {
   __shared__ int64_t lrec[kFoldBS * 3];
   __shared__ uint32_t lcnt, lnv;
   __shared__ unsigned long long w[8];
+  // test hook (GS_SERVER_LATE_US): the last workgroup starts late, as one the dispatcher
+  // held back behind another stream's kernels would (the exit paths' late-block test)
+  if (late_ticks && blockIdx.x == gridDim.x - 1) {
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < late_ticks) __builtin_amdgcn_s_sleep(8);
+  }
   D.lrec = lrec;
   D.lcnt = &lcnt;
   D.lnv = &lnv;
@@ -581,7 +598,7 @@ __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, Ser
       const uint32_t lane = threadIdx.x;
       const bool b0 = blockIdx.x == 0;
       const unsigned long long t0 = wall_clock64();
-      const unsigned long long limit = b0 ? idle_ticks : 2 * idle_ticks;
+      const unsigned long long limit = b0 ? idle_ticks : 10 * idle_ticks;
       unsigned long long* line = b0 ? &box->seq : &bc->seq;
       unsigned long long v = 0, s = 0;
       for (;;) {
@@ -737,6 +754,22 @@ void launch_dedup(const int64_t* src, const int64_t* dst, uint32_t n, unsigned l
   if (n) hipLaunchKernelGGL(k_dedup, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, n, tab, mask, w);
 }
 
+// One listed vertex -> output row pos: its key, canonical label (root key) and parity.
+__device__ __forceinline__ void export_one(const Table& t, uint32_t s, int64_t* ov, int64_t* ol, uint8_t* op,
+                                           uint64_t pos, uint64_t cap_out) {
+  int64_t k;
+  uint32_t l, acc;
+  load_slot(t.tab + s, k, l);
+  const int64_t v = settle_key(t, s, k);
+  int64_t kx = v;
+  find_ro(t, s, l, kx, acc);
+  if (pos < cap_out) {  // (non-temporal stores here measured no different: 0.82 ms either way)
+    ov[pos] = v;
+    ol[pos] = kx;
+    if (op) op[pos] = (uint8_t)acc;
+  }
+}
+
 // Export (vertex, label, parity) of every occupied slot of [s_begin, s_end). Each
 // thread owns kExportPer slots of a kExportPer x kExportBS-slot tile (coalesced 16-B
 // loads); the block reserves its output range with ONE atomic per tile.
@@ -746,13 +779,30 @@ constexpr uint32_t kExportBS = 1024;
 #endif
 constexpr int kExportPer = GS_EXPORT_LOCKSTEP ? 8 : 16;
 
+// by_list: the whole table with a complete vertex list, whose fill the host only bounds (the
+// bound charges 2 vertices to every fold whose capacity report has not landed: right after a
+// pass of folds it overstates RMAT-20's 646 K vertices ~10x). The kernel reads the real count
+// and walks the list when it is under 1/8 of the slots (use_vertex_list's rule), as
+// k_export_list does; else it scans. RMAT-20's label pass: 90 us scanning 2^23 slots.
 __global__ __launch_bounds__(kExportBS) void k_export(Table t, int64_t* __restrict__ ov, int64_t* __restrict__ ol,
                                                       uint8_t* __restrict__ op, uint64_t cap_out, uint64_t s_begin,
-                                                      uint64_t s_end) {
+                                                      uint64_t s_end, int by_list) {
   constexpr int PER = kExportPer;
   __shared__ uint32_t wsum[kExportBS / 64];
   __shared__ uint32_t base_sh;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (by_list && !t.ctr[ctr_index(CTR_VOVF)]) {
+    __shared__ uint32_t lcnt[kShards];
+    __shared__ uint64_t lpre[kShards + 1];
+    const uint64_t total = vlist_prefix(t, lcnt, lpre);
+    if (total * 8 < s_end - s_begin) {  // block-uniform
+      const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+      if (g0 == 0) t.ctr[ctr_index(CTR_EXPORT)] = (uint32_t)total;
+      for (uint64_t g = g0; g < total && g < cap_out; g += (uint64_t)gridDim.x * blockDim.x)
+        export_one(t, vlist_at(t, lpre, g), ov, ol, op, g, cap_out);
+      return;
+    }
+  }
   for (uint64_t tile = s_begin + (uint64_t)blockIdx.x * (kExportBS * PER); tile < s_end;
        tile += (uint64_t)gridDim.x * (kExportBS * PER)) {
     int64_t vk[PER], lk[PER];
@@ -836,20 +886,6 @@ __global__ __launch_bounds__(kExportBS) void k_export(Table t, int64_t* __restri
 
 // Export over the vertex list: entry g -> output row g (deterministic, no atomics).
 // If the list overflowed (CTR_VOVF) every slot is scanned with appends instead.
-__device__ __forceinline__ void export_one(const Table& t, uint32_t s, int64_t* ov, int64_t* ol, uint8_t* op,
-                                           uint64_t pos, uint64_t cap_out) {
-  int64_t k;
-  uint32_t l, acc;
-  load_slot(t.tab + s, k, l);
-  const int64_t v = settle_key(t, s, k);
-  int64_t kx = v;
-  find_ro(t, s, l, kx, acc);
-  if (pos < cap_out) {  // (non-temporal stores here measured no different: 0.82 ms either way)
-    ov[pos] = v;
-    ol[pos] = kx;
-    if (op) op[pos] = (uint8_t)acc;
-  }
-}
 
 __global__ __launch_bounds__(256) void k_export_list(Table t, int64_t* __restrict__ ov, int64_t* __restrict__ ol,
                                                      uint8_t* __restrict__ op, uint64_t cap_out) {
@@ -1136,13 +1172,13 @@ void launch_fold(bool sign, bool track, const Table& t, const Delta& D, const Fo
 
 void launch_window_server(bool sign, const Table& t, const Delta& D, ServerBox* box, ServerBcast* bc,
                           unsigned long long* done, unsigned long long seq0, unsigned long long idle_ticks,
-                          hipStream_t st) {
+                          unsigned long long late_ticks, hipStream_t st) {
   if (sign)
     hipLaunchKernelGGL(k_window_server<true>, dim3(kServerBlocks), dim3(kFoldBS), 0, st, t, D, box, bc, done, seq0,
-                       idle_ticks);
+                       idle_ticks, late_ticks);
   else
     hipLaunchKernelGGL(k_window_server<false>, dim3(kServerBlocks), dim3(kFoldBS), 0, st, t, D, box, bc, done, seq0,
-                       idle_ticks);
+                       idle_ticks, late_ticks);
 }
 
 int window_server_resident_blocks(bool sign, int device) {
@@ -1155,14 +1191,15 @@ int window_server_resident_blocks(bool sign, int device) {
 }
 
 void launch_export(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, hipStream_t st, int part,
-                   int nparts) {
+                   int nparts, bool by_list) {
   const uint64_t all = (uint64_t)t.r0 + 1;
   const uint64_t s0 = all * (uint64_t)part / (uint64_t)nparts, s1 = all * (uint64_t)(part + 1) / (uint64_t)nparts;
   const uint64_t tile = (uint64_t)kExportPer * kExportBS;
   const uint64_t tiles = (s1 - s0 + tile - 1) / tile;
   const uint64_t cap_blocks = 4096ull * 256 / kExportBS;
   const unsigned g = (unsigned)(tiles < cap_blocks ? (tiles ? tiles : 1) : cap_blocks);
-  hipLaunchKernelGGL(k_export, dim3(g), dim3(kExportBS), 0, st, t, ov, ol, op, cap_out, s0, s1);
+  hipLaunchKernelGGL(k_export, dim3(g), dim3(kExportBS), 0, st, t, ov, ol, op, cap_out, s0, s1,
+                     (by_list && nparts == 1) ? 1 : 0);
 }
 
 void launch_export_list(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, uint64_t bound,

@@ -65,7 +65,7 @@ struct alignas(64) ServerBcast {    // device memory: block 0 -> the other block
 };
 void launch_window_server(bool sign, const Table& t, const Delta& D, ServerBox* box, ServerBcast* bc,
                           unsigned long long* done, unsigned long long seq0, unsigned long long idle_ticks,
-                          hipStream_t st);
+                          unsigned long long late_ticks, hipStream_t st);
 // Workgroups of k_window_server that can be resident on the device at once (occupancy x
 // CUs): a window completes only when all kServerBlocks of them run together.
 int window_server_resident_blocks(bool sign, int device);
@@ -76,8 +76,10 @@ void launch_dedup(const int64_t* src, const int64_t* dst, uint32_t n, unsigned l
                   uint8_t* w, hipStream_t st);
 void launch_reset_list(const Table& t, uint32_t* nxt, uint64_t bound, hipStream_t st);
 void launch_fold(bool sign, bool track, const Table& t, const Delta& D, const FoldLaunch& f, hipStream_t st);
+// by_list: the vertex list is complete as far as the host knows; the kernel walks it when the
+// real vertex count (read on the device) is under 1/8 of the slots, else it scans
 void launch_export(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, hipStream_t st,
-                   int part = 0, int nparts = 1);
+                   int part = 0, int nparts = 1, bool by_list = false);
 void launch_export_list(const Table& t, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out, uint64_t bound,
                         hipStream_t st);
 // order-independent digest of the (vertex, label, parity) set, added into *out

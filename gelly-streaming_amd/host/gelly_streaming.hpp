@@ -92,45 +92,111 @@ struct MapFunction {
 // after the all-window reduce; creating a GPU summary each time would cost a table
 // allocation and initialisation per window. Released handles are reset (O(touched
 // vertices) on the device, asynchronous) and handed to the next summary of the same
-// kind, device and capacity.
+// kind and device whose table size class fits (up to kClassSlack classes larger).
+//
+// HBM budget (the Java HandlePool's model): the pool accounts the HBM of
+// every handle it has handed out (table slots x 16 B + the vertex list's 4 B per slot).
+// Summaries a Flink job drops without release() -- per-emission copies with object reuse
+// off, window partials cleared after a fire -- return their handles only when the JVM
+// finalizes them; set_budget's `collect` hook stands for System.gc() +
+// System.runFinalization(), which acquire() runs before a create would pass the budget.
 // --------------------------------------------------------------------------
 class HandlePool {
  public:
+  static constexpr int kClassSlack = 2;
+  static constexpr size_t kMaxFree = 64;
   static HandlePool& instance() {
     static HandlePool p;
     return p;
   }
+  // gs_create's table for a capacity hint: 4 slots per expected vertex, a power of two, >= 1024
+  static uint64_t slots_for(uint64_t hint) {
+    const uint64_t want = std::max<uint64_t>(4 * std::max<uint64_t>(hint, 1), 1024);
+    uint64_t s = 1;
+    while (s < want) s <<= 1;
+    return s;
+  }
+  static uint64_t bytes_of_slots(uint64_t slots) { return slots * 20; }
+  static int size_class(uint64_t slots) {
+    int c = 0;
+    while ((2ull << c) <= slots) ++c;
+    return c;
+  }
+  // budget of the handed-out handles' HBM (0: none) and the finalization hook it runs
+  void set_budget(uint64_t bytes, std::function<void()> collect) {
+    budget_ = bytes;
+    collect_ = std::move(collect);
+  }
   gs_handle acquire(int kind, int device, uint64_t capacity_hint) {
-    auto& free = free_[{kind, device, capacity_hint}];
-    if (!free.empty()) {
-      gs_handle h = free.back();
-      free.pop_back();
-      ++reused_;
-      return h;
+    const uint64_t slots = slots_for(capacity_hint);
+    if (gs_handle h = take(kind, device, size_class(slots))) return h;
+    if (budget_ && collect_ && outstanding_ + bytes_of_slots(slots) > budget_) {
+      ++collections_;
+      collect_();  // the dropped summaries' destructors release into this pool
+      if (gs_handle h = take(kind, device, size_class(slots))) return h;
     }
     gs_handle h = nullptr;
     gs_check(gs_create(&h, device, kind, capacity_hint));
     ++created_;
+    bytes_[h] = bytes_of_slots(slots);
+    add_outstanding(bytes_[h]);
     return h;
   }
-  void release(gs_handle h, int kind, int device, uint64_t capacity_hint) {
-    // the value AND the configuration (tracking, pipelining, profiling) of a fresh handle
-    if (gs_reset_config(h) != GS_OK) {  // a broken handle is not pooled
+  void release(gs_handle h, int kind, int device) {
+    auto it = bytes_.find(h);
+    if (it != bytes_.end()) outstanding_ -= it->second;
+    uint64_t slots = 0;
+    // the value AND the configuration (tracking, pipelining, profiling) of a fresh handle;
+    // a table keeps a grown capacity across resets: account and pool it by its real size
+    if (gs_reset_config(h) != GS_OK || gs_table_capacity(h, &slots) != GS_OK) {  // a broken handle is not pooled
+      bytes_.erase(h);
       gs_destroy(h);
       return;
     }
-    free_[{kind, device, capacity_hint}].push_back(h);
+    if (nfree_ < kMaxFree) {
+      bytes_[h] = bytes_of_slots(slots);
+      free_[{kind, device, size_class(slots)}].push_back(h);
+      ++nfree_;
+    } else {
+      bytes_.erase(h);
+      gs_destroy(h);
+    }
   }
   size_t created() const { return created_; }
   size_t reused() const { return reused_; }
+  size_t collections() const { return collections_; }
+  uint64_t outstanding_bytes() const { return outstanding_; }
+  uint64_t peak_outstanding_bytes() const { return peak_; }
+  size_t live_handles() const { return bytes_.size(); }  // handed out + pooled
   ~HandlePool() {
     for (auto& kv : free_)
       for (gs_handle h : kv.second) gs_destroy(h);
   }
 
  private:
-  std::map<std::tuple<int, int, uint64_t>, std::vector<gs_handle>> free_;
-  size_t created_ = 0, reused_ = 0;
+  gs_handle take(int kind, int device, int cls) {
+    for (auto it = free_.lower_bound({kind, device, cls}); it != free_.end(); ++it) {
+      const auto& k = it->first;
+      if (std::get<0>(k) != kind || std::get<1>(k) != device || std::get<2>(k) > cls + kClassSlack) break;
+      if (it->second.empty()) continue;
+      gs_handle h = it->second.back();
+      it->second.pop_back();
+      --nfree_;
+      ++reused_;
+      add_outstanding(bytes_[h]);
+      return h;
+    }
+    return nullptr;
+  }
+  void add_outstanding(uint64_t b) {
+    outstanding_ += b;
+    peak_ = std::max(peak_, outstanding_);
+  }
+  std::map<std::tuple<int, int, int>, std::vector<gs_handle>> free_;
+  std::map<gs_handle, uint64_t> bytes_;
+  size_t nfree_ = 0, created_ = 0, reused_ = 0, collections_ = 0;
+  uint64_t budget_ = 0, outstanding_ = 0, peak_ = 0;
+  std::function<void()> collect_;
 };
 
 // --------------------------------------------------------------------------
@@ -176,7 +242,15 @@ class GpuSummary {
   // failed verdict (Candidates(false)) is applied to it then
   gs_handle ensure() {
     if (h_) return h_;
-    h_ = HandlePool::instance().acquire(kind_, device_, hint_);
+    // the table for the size asked for (size_for), else the pending image's vertex count
+    // (its header: u32 magic, kind, ok, 0, u64 n), else the constructor's hint
+    uint64_t hint = sized_ ? sized_ : hint_;
+    if (!sized_ && image_.size() >= 24) {
+      uint64_t n = 0;
+      std::memcpy(&n, image_.data() + 16, 8);
+      if (n) hint = n;
+    }
+    h_ = HandlePool::instance().acquire(kind_, device_, hint);
     if (!image_.empty()) {
       std::vector<uint8_t> img;
       img.swap(image_);
@@ -192,12 +266,18 @@ class GpuSummary {
     return h_;
   }
   bool acquired() const { return h_ != nullptr; }
+  // size the handle taken at first use for about `vertices` vertices (GpuSummary.sizeFor: a
+  // copy asks for its source's count); no effect once a handle is held
+  void size_for(uint64_t vertices) {
+    if (!h_) sized_ = std::max<uint64_t>(vertices, 1);
+  }
   // back to the pool (the glue's explicit release of a summary the combine dropped); the
   // object reads as a fresh initial value afterwards
   void release() {
     n_ = 0;
+    sized_ = 0;
     image_.clear();
-    if (h_) HandlePool::instance().release(h_, kind_, device_, hint_);
+    if (h_) HandlePool::instance().release(h_, kind_, device_);
     h_ = nullptr;
   }
   // Java serialization of the summary object: [0] 1 = an image follows, [1] failed
@@ -279,6 +359,7 @@ class GpuSummary {
   int kind_;
   int device_;
   uint64_t hint_;
+  uint64_t sized_ = 0;  // size_for(): vertices of the first handle (0: hint_ / the image's count)
   size_t flush_edges_;
   gs_handle h_ = nullptr;
   std::unique_ptr<int64_t[]> src_, dst_;  // [flush_edges_] each, allocated on first push

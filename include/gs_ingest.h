@@ -60,6 +60,13 @@ int gs_fold_text(gs_handle h, const char* text, size_t len, int sep, uint64_t* n
 int gs_parse_set_profiling(int on);
 int gs_parse_profile(double* kernel_us, uint64_t* parses);
 
+/* gs_parse_edges_device keeps a per-thread cache (device scratch of ~1.25 x the longest
+ * text parsed, a mapped result record, timing events) across calls. gs_parse_release frees
+ * the calling thread's cache; a thread that parses calls it before it ends (a pool thread of
+ * a JNI host: when its task finishes). A thread that moves to another device frees the old
+ * device's cache at its next parse. */
+int gs_parse_release(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -338,6 +338,14 @@ int gs_capacity_stats(gs_handle h, uint64_t* waits, uint64_t* syncs, double* wai
  * count in the debug build (make -C gelly-streaming_amd debug). */
 int gs_counters(gs_handle h, uint64_t* out8);
 
+/* Diagnostics of the fold's memory operations (synchronises), debug build only (all
+ * zero otherwise): out[0] edges / rows folded, [1] key CASes issued, [2] key CASes that
+ * found the slot taken, [3] agent-scope re-reads before a key CAS, [4] edges settled by
+ * the shared-parent shortcut, [5] edges whose finds met one root, [6] parent loads of
+ * the finds, [7] hooks that joined two trees, [8] extra linear-probe loads. n <= 16
+ * entries are written. Not a reference interface: the tools behind DESIGN.md use it. */
+int gs_debug_counters(gs_handle h, uint64_t* out, int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -41,6 +41,7 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 	private final boolean failedInitially;  // new GpuCandidates(false): applied at the first use
 	private transient long handle;          // 0 until the first use
 	private transient byte[] image;         // read by readObject, applied at the first use
+	private transient long sized;           // sizeFor(): the vertices the first handle is taken for (0: default)
 	private transient long[] src;           // edge buffers, allocated at the first edge
 	private transient long[] dst;
 	private transient byte[] par;
@@ -175,7 +176,7 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 	@Override
 	public long handle() {
 		if (handle == 0) {
-			long h = HandlePool.SIGNED.acquire();
+			long h = HandlePool.SIGNED.acquire(GpuSummary.hintFor(sized, image));
 			try {
 				if (image != null) {
 					GsNative.deserialize(h, image);  // rows and verdict
@@ -195,8 +196,16 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 	/** Back to the pool (the combine dropped this summary, GpuBipartitenessCheck); it reads
 	 *  as a fresh initial value afterwards. */
 	@Override
+	public void sizeFor(long vertices) {
+		if (handle == 0) {
+			sized = Math.max(vertices, 1L);
+		}
+	}
+
+	@Override
 	public void release() {
 		n = 0;
+		sized = 0;
 		plain = true;
 		image = null;
 		if (handle != 0) {
@@ -208,10 +217,12 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 	// ---- Java serialization (the Merger's fields, SummaryAggregation.java:95-103)
 	private void writeObject(ObjectOutputStream out) throws IOException {
 		out.defaultWriteObject();
-		byte[] img = image;
-		if (img == null && (handle != 0 || n > 0)) {
+		byte[] img = image;  // not yet applied and nothing buffered on top: ship it as it came
+		if (handle != 0 || n > 0) {
+			// edges buffered on a deserialised copy belong in the image (ADVICE r4): flush()
+			// applies the pending image to a handle first, then folds them
 			flush();
-			img = GsNative.serialize(handle);
+			img = GsNative.serialize(handle());
 		}
 		out.writeObject(img);  // null: never used (failedInitially travels as a field)
 	}

@@ -42,6 +42,7 @@ public class GpuDisjointSet extends DisjointSet<Long> implements GpuSummary {
 
 	private transient long handle;   // 0 until the first use
 	private transient byte[] image;  // read by readObject, applied at the first use
+	private transient long sized;    // sizeFor(): the vertices the first handle is taken for (0: default)
 	private transient long[] src;    // edge buffers, allocated at the first union
 	private transient long[] dst;
 	private transient int n;
@@ -129,7 +130,7 @@ public class GpuDisjointSet extends DisjointSet<Long> implements GpuSummary {
 	@Override
 	public long handle() {
 		if (handle == 0) {
-			long h = HandlePool.CC.acquire();
+			long h = HandlePool.CC.acquire(GpuSummary.hintFor(sized, image));
 			if (image != null) {
 				try {
 					GsNative.deserialize(h, image);
@@ -147,8 +148,16 @@ public class GpuDisjointSet extends DisjointSet<Long> implements GpuSummary {
 	/** Back to the pool: the combine dropped this summary (GpuConnectedComponents), or it
 	 *  is no longer needed. It reads as a fresh, empty initial value afterwards. */
 	@Override
+	public void sizeFor(long vertices) {
+		if (handle == 0) {
+			sized = Math.max(vertices, 1L);
+		}
+	}
+
+	@Override
 	public void release() {
 		n = 0;
+		sized = 0;
 		image = null;
 		if (handle != 0) {
 			HandlePool.CC.release(handle);
@@ -159,10 +168,12 @@ public class GpuDisjointSet extends DisjointSet<Long> implements GpuSummary {
 	// ---- Java serialization (the Merger's fields, SummaryAggregation.java:95-103)
 	private void writeObject(ObjectOutputStream out) throws IOException {
 		out.defaultWriteObject();
-		byte[] img = image;  // not yet applied: ship it as it came
-		if (img == null && (handle != 0 || n > 0)) {
+		byte[] img = image;  // not yet applied and nothing buffered on top: ship it as it came
+		if (handle != 0 || n > 0) {
+			// edges buffered on a deserialised copy belong in the image (ADVICE r4): flush()
+			// applies the pending image to a handle first, then folds them
 			flush();
-			img = GsNative.serialize(handle);
+			img = GsNative.serialize(handle());
 		}
 		out.writeObject(img);  // null: never used, the empty initial value
 	}

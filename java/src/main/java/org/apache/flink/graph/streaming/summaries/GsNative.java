@@ -37,6 +37,7 @@ final class GsNative {
 	// ---- queries (gs_find, gs_num_vertices, gs_export_labels, gs_bip_status, gs_export_colouring)
 	static native Long find(long h, long v);
 	static native long numVertices(long h);
+	static native long tableCapacity(long h);  // gs_table_capacity: slots (the pool's HBM accounting)
 	static native int exportLabels(long h, long[] v, long[] label);
 	static native boolean bipStatus(long h);
 	static native int exportColouring(long h, long[] comp, long[] v, byte[] sign);

@@ -168,6 +168,16 @@ JNIEXPORT jlong JNICALL FN(numVertices)(JNIEnv* env, jclass c, jlong h) {
   return (jlong)n;
 }
 
+JNIEXPORT jlong JNICALL FN(tableCapacity)(JNIEnv* env, jclass c, jlong h) {
+  (void)c;
+  uint64_t slots = 0;
+  if (gs_table_capacity(H(h), &slots) != GS_OK) {
+    throw_gs(env);
+    return 0;
+  }
+  return (jlong)slots;
+}
+
 JNIEXPORT jint JNICALL FN(exportLabels)(JNIEnv* env, jclass c, jlong h, jlongArray v, jlongArray l) {
   (void)c;
   const jsize cap = (*env)->GetArrayLength(env, v);

@@ -1,0 +1,105 @@
+// The GPU summaries' HBM lifetime under Flink's default object handling,
+// modelled on the C++ host mirror. With object reuse off Flink
+//   * copies the initial value for every (partition, window) fold state
+//     (TypeSerializer.copy, S/SummaryBulkAggregation.java:79-80) -- a GPU copy is a pooled
+//     handle plus gs_combine, sized from its source's vertex count;
+//   * clears a window's fold state after the window fires: the partial is dropped, never
+//     released (S/SummaryAggregation.java:107-119);
+//   * copies the Merger's output for every chained collect before the sink reads it; the
+//     copy is dropped once the sink is done.
+// The dropped summaries' handles come back only when the JVM finalizes them. Here they go
+// to a finalizer queue that is emptied only when the pool's byte budget asks for it (the
+// Java pool's System.gc() + System.runFinalization()). The run must keep the handles handed
+// out within the budget (plus the one create that triggers a pass) and end with the
+// oracle's summary.
+// Usage: test_handle_budget <edges.bin: int64 src,dst pairs> <window edges> <budget bytes> <out.bin>
+// out.bin: int64 n, then n rows of int64 {v, label}. Prints one JSON line of pool statistics.
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "gelly_streaming.hpp"
+
+using namespace gelly;
+
+static void die(const std::string& m) {
+  std::fprintf(stderr, "FAIL %s\n", m.c_str());
+  std::exit(1);
+}
+
+// GpuSummarySerializer.copy: a fresh summary sized from the source's vertex count, combined into
+static DisjointSetRef copy_of(DisjointSet& src, uint64_t default_hint) {
+  auto c = std::make_shared<DisjointSet>(0, default_hint);
+  c->size_for(src.size());
+  c->merge(src);
+  return c;
+}
+
+int main(int argc, char** argv) {
+  if (argc != 5) die("usage: test_handle_budget <edges.bin> <window> <budget bytes> <out.bin>");
+  FILE* f = std::fopen(argv[1], "rb");
+  if (!f) die("cannot open edges");
+  std::vector<int64_t> e;
+  int64_t buf[4096];
+  size_t got;
+  while ((got = std::fread(buf, 8, 4096, f)) > 0) e.insert(e.end(), buf, buf + got);
+  std::fclose(f);
+  const size_t n = e.size() / 2, window = std::strtoull(argv[2], nullptr, 0);
+  const uint64_t budget = std::strtoull(argv[3], nullptr, 0);
+  const uint64_t default_hint = 1 << 16;  // the operator's initial value (the pool's default hint)
+  std::vector<std::shared_ptr<GpuSummary>> finalizer_queue;  // dropped, not yet finalized
+  size_t finalized = 0, max_queue = 0;
+  HandlePool& pool = HandlePool::instance();
+  pool.set_budget(budget, [&] {  // System.gc() + System.runFinalization()
+    finalized += finalizer_queue.size();
+    finalizer_queue.clear();
+  });
+  uint64_t worst = 0;  // handed-out bytes seen after any acquire that had to create
+  try {
+    ConnectedComponents<NullValue>::CombineCC combine;
+    const auto initialVal = std::make_shared<DisjointSet>(0, default_hint);  // never used itself
+    DisjointSetRef summary = std::make_shared<DisjointSet>(0, default_hint);  // Merger.summary
+    size_t windows = 0;
+    for (size_t i = 0; i < n; i += window, ++windows) {
+      // the window's fold state: a copy of the initial value (empty: the default hint)
+      auto partial = std::make_shared<DisjointSet>(0, default_hint);
+      const size_t j = std::min(n, i + window);
+      for (size_t k = i; k < j; ++k) partial->union_(e[2 * k], e[2 * k + 1]);  // UpdateCC.foldEdges
+      // Merger.flatMap: summary = reduce(partial, summary); the input the combine dropped is
+      // NOT released -- Flink clears the window state and the object waits for finalization
+      DisjointSetRef kept = combine.reduce(partial, summary);
+      DisjointSetRef dropped = kept == partial ? summary : partial;
+      summary = kept;
+      finalizer_queue.push_back(dropped);
+      // the emission: copied for the chained collect, read by the sink, dropped
+      DisjointSetRef out = copy_of(*summary, default_hint);
+      if (out->size() != summary->size()) die("the emitted copy differs from the summary");
+      finalizer_queue.push_back(out);
+      max_queue = std::max(max_queue, finalizer_queue.size());
+      worst = std::max(worst, pool.outstanding_bytes());
+    }
+    (void)initialVal;
+    const auto rows = summary->rows();
+    std::vector<int64_t> o = {(int64_t)rows.size()};
+    for (const auto& r : rows) {
+      o.push_back(r.v);
+      o.push_back(r.label);
+    }
+    FILE* g = std::fopen(argv[4], "wb");
+    if (!g || std::fwrite(o.data(), 8, o.size(), g) != o.size()) die("cannot write output");
+    std::fclose(g);
+    std::printf(
+        "{\"windows\": %zu, \"budget\": %llu, \"peak_outstanding\": %llu, \"worst_after_window\": %llu, "
+        "\"created\": %zu, \"reused\": %zu, \"collections\": %zu, \"finalized\": %zu, \"max_queue\": %zu, "
+        "\"live_handles\": %zu}\n",
+        windows, (unsigned long long)budget, (unsigned long long)pool.peak_outstanding_bytes(),
+        (unsigned long long)worst, pool.created(), pool.reused(), pool.collections(), finalized, max_queue,
+        pool.live_handles());
+    finalizer_queue.clear();
+    summary.reset();
+  } catch (const std::exception& x) {
+    die(x.what());
+  }
+  return 0;
+}

@@ -12,7 +12,8 @@
 //     and the glue releases the input the combine dropped back to the handle pool;
 //   * at window `ckpt` the Merger's `summary` and `initialVal` are written and read back
 //     into new objects, which take handles on first use and apply the image, and the
-//     stream continues through them.
+//     stream continues through them; the restored summary first buffers three extra
+//     edges (ids from 2^50) and goes through writeObject / readObject once more.
 // Usage: test_java_serialization <cc|signed> <edges.bin: int64 src,dst pairs> <window edges>
 //                                <ckpt window> <out.bin>
 // out.bin: int64 ok, int64 n, then n rows of int64 {v, label or component, parity or sign}.
@@ -94,6 +95,18 @@ static int run(const std::vector<int64_t>& e, size_t window, size_t ckpt, const 
       summary = S::readObject(img_s);
       initialVal = same ? summary : S::readObject(img_i);
       if (summary->acquired()) die("restored summary took a handle before its first use");
+      // edges buffered on a deserialised copy that has no handle yet (its image
+      // still pending) must travel in its next image. Three edges outside the stream (ids
+      // from 2^50; the driver adds them to the oracle's input) are folded into the restored
+      // summary, which is serialised and read back once more before the stream continues.
+      const int64_t X = (int64_t)1 << 50;
+      fold_edge(*summary, X + 1, e[0]);
+      fold_edge(*summary, X + 2, X + 1);
+      if constexpr (std::is_same<S, DisjointSet>::value) fold_edge(*summary, X + 3, X + 3);
+      const std::vector<uint8_t> img_b = summary->writeObject();
+      summary->release();
+      summary = S::readObject(img_b);
+      if (same) initialVal = summary;
     }
   }
   // final emission

@@ -84,3 +84,20 @@ def test_digest_self_check_two_ranks_gloo():
     assert r.returncode == 0, r.stderr[-3000:]
     chk = _last_json(r.stdout)["self_check"]
     assert not chk["replica_label_digests_equal"] and not chk["digest_equals_single_gpu"]
+
+
+def test_rccl_channel_knob_reaches_every_rank():
+    """--rccl-max-channels sets NCCL_MAX_NCHANNELS before anything initialises
+    HIP or RCCL; the self-launched ranks inherit it and report it (config.rccl), checked equal on
+    every rank over gloo. Without the flag the line says RCCL's default (None)."""
+    env = _env()
+    env.pop("NCCL_MAX_NCHANNELS", None)
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check", "--rccl-max-channels", "8"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rc = _last_json(r.stdout)["rccl"]
+    assert rc == {"NCCL_MAX_NCHANNELS": 8, "same_on_all_ranks": True}
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _last_json(r.stdout)["rccl"]["NCCL_MAX_NCHANNELS"] is None

@@ -214,3 +214,58 @@ def test_parse_profiling_counts_kernel_time(gs):
     gs.parse_set_profiling(False)
     _gpu_parse(gs, text, 0)
     assert gs.parse_profile()[1] == 0
+
+
+def test_parse_release_frees_the_cache_and_parses_again(gs, oracle_mod):
+    """gs_parse_release frees the thread's parse cache (device scratch, mapped record,
+    timing events); the next parse rebuilds it and is still exact, a second release in a row is a
+    no-op, and a worker thread that parses and releases leaves no allocation behind (the device's
+    free memory returns to where it was)."""
+    import threading
+    import torch
+    rng = np.random.default_rng(13)
+    text = _random_text(rng, 30000, 0)
+    es, ed, en, eb = oracle_mod.parse_edges(text, 0)
+    for _ in range(2):
+        s, d, n, b = _gpu_parse(gs, text, 0)
+        assert (n, b) == (en, eb) and np.array_equal(s, es) and np.array_equal(d, ed)
+        gs.parse_release()
+        gs.parse_release()
+    big = _random_text(rng, 400000, 0)
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    err = []
+
+    def worker():
+        try:
+            _gpu_parse(gs, big, 0)
+            gs.parse_release()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            err.append(e)
+
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join()
+    assert not err, err
+    torch.cuda.synchronize()
+    # the worker's text and outputs are torch tensors (cached by torch's allocator, not returned);
+    # the library's scratch of ~1.25 x the text went back to the device
+    torch.cuda.empty_cache()
+    assert torch.cuda.mem_get_info()[0] >= free0 - (1 << 20)
+
+
+@pytest.mark.parametrize("offset", [0, 1, 7])
+def test_parse_lookback_fallback_counts_directly(gs, oracle_mod, offset, monkeypatch):
+    """a tile whose predecessors have not published within the look-back's timeout
+    counts the '\\n' before it itself (16-byte loads across the wave, an unaligned head and
+    tail byte by byte). GS_PARSE_LB_TIMEOUT_US=0 makes every tile that finds an unpublished
+    predecessor take that path; the result is still the oracle's, for aligned and unaligned
+    texts of many tiles."""
+    rng = np.random.default_rng(17 + offset)
+    monkeypatch.setenv("GS_PARSE_LB_TIMEOUT_US", "0")
+    for nlines in (3000, 120000):
+        text = _random_text(rng, nlines, 0)
+        es, ed, en, eb = oracle_mod.parse_edges(text, 0)
+        s, d, n, b = _gpu_parse(gs, text, 0, offset)
+        assert (n, b) == (en, eb), (nlines, offset, n, b, en, eb)
+        assert np.array_equal(s, es) and np.array_equal(d, ed)

@@ -74,7 +74,7 @@ def test_summaries_survive_java_serialization_by_construction():
         assert "private void readObject(ObjectInputStream in)" in text, cls
         ctors = re.findall(r"public %s\([^)]*\)[^{]*\{(.*?)\n\t\}" % cls, text, flags=re.S)
         assert ctors and not any("acquire" in c for c in ctors), cls
-        assert text.count("HandlePool.%s.acquire()" % pool) == 1, cls  # in handle() only
+        assert text.count("HandlePool.%s.acquire(" % pool) == 1, cls  # in handle() only
     for op in ("GpuConnectedComponents", "GpuBipartitenessCheck"):
         text = _read(os.path.join(PKG, op + ".java"))
         assert ".release();" in text and "extends SummaryBulkAggregation" in text, op
@@ -86,3 +86,42 @@ def test_jni_fold_outside_critical_regions():
     c = re.sub(r"/\*.*?\*/", "", _read(JNI), flags=re.S)
     assert "GetPrimitiveArrayCritical" not in c
     assert "GetLongArrayRegion" in c and "GetByteArrayRegion" in c
+
+
+def test_write_object_serialises_buffered_edges_of_a_deserialised_copy():
+    """union() only buffers, so a deserialised copy (image pending, no handle) with
+    fewer than BATCH buffered edges must not ship its stale image. writeObject serialises
+    whenever a handle exists or edges are buffered (flush() applies the pending image first),
+    the same condition as the C++ mirror (`h_ || n_ ? serialize() : image_`, modelled and
+    oracle-checked in tests/cpp/test_java_serialization.cpp)."""
+    for cls in ("GpuDisjointSet", "GpuCandidates"):
+        text = _read(os.path.join(PKG, cls + ".java"))
+        body = re.search(r"private void writeObject\(ObjectOutputStream out\)[^{]*\{(.*?)\n\t\}", text, flags=re.S)
+        assert body, cls
+        b = body.group(1)
+        assert re.search(r"if \(handle != 0 \|\| n > 0\) \{", b), cls
+        assert "img == null &&" not in b, cls
+        assert "GsNative.serialize(handle())" in b and b.index("flush();") < b.index("GsNative.serialize"), cls
+    mirror = _read(os.path.join(ROOT, "gelly-streaming_amd", "host", "gelly_streaming.hpp"))
+    assert "h_ || n_ ? serialize() : image_" in mirror
+
+
+def test_handle_pool_hbm_budget_by_construction():
+    """the pool accounts the HBM of the handles it hands out and, before a
+    create would pass gs.hbmBudgetBytes, runs System.gc() + System.runFinalization() OUTSIDE
+    its lock (the finalizers release into the pool) and looks again; free handles are kept by
+    size class; copies are sized from their source's vertex count and deserialised summaries
+    from their image. The behaviour is modelled on the C++ mirror (test_handle_budget)."""
+    pool = _read(os.path.join(PKG, "HandlePool.java"))
+    acq = re.search(r"\tlong acquire\(long hint\) \{(.*?)\n\t\}", pool, flags=re.S).group(1)
+    assert "System.gc();" in acq and "System.runFinalization();" in acq
+    assert "BUDGET_BYTES" in acq and "synchronized long acquire" not in pool  # not under the pool's lock
+    assert acq.index("System.runFinalization();") < acq.index("GsNative.create(")
+    assert "GsNative.tableCapacity(h)" in pool
+    ser = _read(os.path.join(PKG, "GpuSummarySerializer.java"))
+    copy = re.search(r"public GpuSummary copy\(.*?\n\t\}", ser, flags=re.S).group(0)
+    assert "sizeFor(GsNative.numVertices(original.handle()))" in copy
+    assert copy.index("sizeFor(") < copy.index("c.handle()")
+    for cls, p in (("GpuDisjointSet", "CC"), ("GpuCandidates", "SIGNED")):
+        assert "HandlePool.%s.acquire(GpuSummary.hintFor(sized, image))" % p in _read(os.path.join(PKG, cls + ".java"))
+    assert "enableObjectReuse" in _read(os.path.join(ROOT, "INTEGRATION.md"))

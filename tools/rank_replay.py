@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--log-batch", type=int, default=22)
     ap.add_argument("--ramp-log2", type=int, default=22)
     ap.add_argument("--ramp-log-batch", type=int, default=20)
+    ap.add_argument("--row-stats", action="store_true",
+                    help="after the record: rank 0's replay phase by phase (own tracked folds, remote rows), with "
+                         "wall time and the debug build's fold counters per phase (GS_LIB_VARIANT=debug for counts)")
     ap.add_argument("--own-only", action="store_true",
                     help="only rank 0's own folds, untracked vs tracked + takes (for a kernel trace of the tax)")
     a = ap.parse_args()
@@ -162,6 +165,8 @@ def main():
     remote = [[x] if x.shape[0] else [] for x in
               (torch.cat([recs[q][e] for q in range(1, N)]) for e in range(nex))]
     rows = sum(int(x.shape[0]) for e in range(nex) for x in remote[e])
+    if a.row_stats:
+        row_stats(rep0, bounds, remote, fold_own, scratch, cap, cnt, a.lag, nex, a.reps)
 
     def run_rank(parts):
         rep0.reset()
@@ -201,6 +206,45 @@ def main():
         N, t1 * 1e3, N, t_all * 1e3, t1 / (N * t_all), t1 * 1e3 / N), flush=True)
     rep0.close()
     return 0
+
+
+def row_stats(rep0, bounds, remote, fold_own, scratch, cap, cnt, lag, nex, reps):
+    """rank 0's replay, phase by phase: own tracked folds + takes vs the other ranks' rows (serialised,
+    synchronised around every phase), with the debug build's fold counters summed per phase."""
+    keys = None
+    for rep in range(reps):
+        rep0.reset()
+        rep0.sync()
+        tot = {"own": [0.0, None, 0], "remote": [0.0, None, 0]}
+
+        def phase(name, fn, units):
+            c0 = rep0.debug_counters()
+            rep0.sync()
+            t = time.perf_counter()
+            fn()
+            rep0.sync()
+            el = time.perf_counter() - t
+            c1 = rep0.debug_counters()
+            d = {k: c1[k] - c0[k] for k in c1}
+            acc = tot[name]
+            acc[0] += el
+            acc[1] = d if acc[1] is None else {k: acc[1][k] + d[k] for k in d}
+            acc[2] += units
+
+        for b in range(nex):
+            o, m = bounds[b]
+            phase("own", lambda: (fold_own(rep0, 0, o, m), rep0.take_delta_records(scratch, cap, cnt)), m)
+            e = b - lag
+            if e >= 0:
+                for x in remote[e]:
+                    phase("remote", lambda: rep0.fold_records(x, x.shape[0]), int(x.shape[0]))
+        for e in range(max(0, nex - lag), nex):
+            for x in remote[e]:
+                phase("remote", lambda: rep0.fold_records(x, x.shape[0]), int(x.shape[0]))
+        for name, (el, d, units) in tot.items():
+            per_unit = " ".join("%s %.3f" % (k, d[k] / max(units, 1)) for k in d)
+            print("row-stats rep %d %s: %d units in %.2f ms (%.1f G units/s, synchronised per phase); per unit: %s"
+                  % (rep, name, units, el * 1e3, units / el / 1e9, per_unit), flush=True)
 
 
 if __name__ == "__main__":
