@@ -273,7 +273,11 @@ int ensure_capacity(gs_summary* h, size_t n) {
   // GPU busy, instead of a drain before every fold (RMAT-20, config 2: 1.07 -> 0.72
   // ms/step).
   const uint64_t slack = 2ull * n * (uint64_t)(std::max({1, h->pipe_depth, h->group_lanes}) + 1);
-  const bool slack_grow = h->cap < kSlackGrowMaxCap && (double)(h->nv_exact + slack) > limit;
+  static const bool slack_on = [] {  // experiment knob GS_SLACK_GROW=0: no slack sizing (tools/fold_stats.py)
+    const char* e = getenv("GS_SLACK_GROW");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool slack_grow = slack_on && h->cap < kSlackGrowMaxCap && (double)(h->nv_exact + slack) > limit;
   if (!slack_grow) {
     // wait for reports of the folds in flight (the GPU keeps working: no drain)
     h->cap_waits++;

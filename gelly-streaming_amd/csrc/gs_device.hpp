@@ -163,6 +163,28 @@ __device__ __forceinline__ void load_slot(const Slot* p, int64_t& key, uint32_t&
   link = v.z;
 }
 
+// Both endpoints' first probes as L1-bypassing (sc1, L2-served) 16-B loads in flight together
+// (experiment switch GS_PROBE_SC1): a plain load may return a line the CU's L1 holds from
+// before another CU's insert, an EMPTY that the key CAS then has to settle.
+#ifndef GS_PROBE_SC1
+#define GS_PROBE_SC1 0
+#endif
+__device__ __forceinline__ void load_slot2_sc1(const Slot* pa, const Slot* pb, int64_t& ka, uint32_t& la, int64_t& kb,
+                                               uint32_t& lb) {
+  uint4 a, b;
+  asm volatile(
+      "global_load_dwordx4 %0, %2, off sc1\n\t"
+      "global_load_dwordx4 %1, %3, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(a), "=&v"(b)
+      : "v"(pa), "v"(pb)
+      : "memory");
+  ka = (int64_t)(((uint64_t)a.y << 32) | a.x);
+  la = a.z;
+  kb = (int64_t)(((uint64_t)b.y << 32) | b.x);
+  lb = b.z;
+}
+
 __device__ __forceinline__ uint32_t load_link_fresh(const Slot* p) {
   return __hip_atomic_load(&p->link, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -267,15 +289,17 @@ __device__ __forceinline__ uint32_t insert_finish(const Table& t, int64_t key, u
 #ifndef GS_PAIR_INSERT
 #define GS_PAIR_INSERT 1  // 0: endpoints inserted one after the other (experiment switch)
 #endif
-template <bool TTAS>
+template <bool TTAS, bool TTAS_V = TTAS>
 __device__ __forceinline__ void insert_pair(const Table& t, int64_t ku, uint32_t hu, int64_t kv, uint32_t hv,
                                             uint32_t& su, uint32_t& lu, bool& nu, uint32_t& sv, uint32_t& lv,
                                             bool& nv) {
   unsigned long long ou = (unsigned long long)kEmpty, ov = (unsigned long long)kEmpty;
   if (TTAS) {
     GS_DBG(CTR_DBG_TTAS);
-    GS_DBG(CTR_DBG_TTAS);
     ou = __hip_atomic_load((unsigned long long*)&t.tab[hu].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (TTAS_V) {
+    GS_DBG(CTR_DBG_TTAS);
     ov = __hip_atomic_load((unsigned long long*)&t.tab[hv].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const bool tu = ou == (unsigned long long)kEmpty, tv = ov == (unsigned long long)kEmpty;
@@ -292,7 +316,7 @@ __device__ __forceinline__ void insert_pair(const Table& t, int64_t ku, uint32_t
   if (tv32) ov = atomicCAS((unsigned long long*)&t.tab[hv].key, (unsigned long long)kEmpty, (unsigned long long)kv);
   __builtin_amdgcn_sched_barrier(0);
   su = insert_finish<TTAS>(t, ku, hu, ou, tu, lu, nu);
-  sv = insert_finish<TTAS>(t, kv, hv, ov, tv, lv, nv);
+  sv = insert_finish<TTAS_V>(t, kv, hv, ov, tv, lv, nv);
 }
 
 __device__ __forceinline__ uint32_t lookup_insert(const Table& t, int64_t key, uint32_t& link, bool& fresh) {

@@ -115,6 +115,12 @@ struct FoldArgs {
   bool server = false;  // resident window server: vertices carried by the tickets (take_tail)
 };
 
+#ifndef GS_ROWS_TTAS
+#define GS_ROWS_TTAS 3  // other replicas' rows: re-read before the key CAS on both sides (experiment switch)
+#endif
+#ifndef GS_DIRECT_FRESH
+#define GS_DIRECT_FRESH 0  // direct hook of a freshly inserted larger-key endpoint (experiment switch)
+#endif
 #ifndef GS_COMBINE_ROUNDS
 #define GS_COMBINE_ROUNDS 2
 #endif
@@ -453,8 +459,12 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   int64_t k0u = 0, k0v = 0;
   uint32_t l0u = 0, l0v = 0;
   if (valid) {
-    load_slot(t.tab + hu, k0u, l0u);
-    load_slot(t.tab + hv, k0v, l0v);
+    if (GS_PROBE_SC1) {
+      load_slot2_sc1(t.tab + hu, t.tab + hv, k0u, l0u, k0v, l0v);
+    } else {
+      load_slot(t.tab + hu, k0u, l0u);
+      load_slot(t.tab + hv, k0v, l0v);
+    }
   }
   uint32_t ru = 0, rv = 0, lu = 0, lv = 0;
   int64_t kru = 0, krv = 0;
@@ -467,13 +477,16 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   uint32_t su = kNoSlot, sv = kNoSlot;
   if (valid) {
     GS_DBG(CTR_DBG_EDGES);
+    // (the re-read stays in the exchange's tracked own folds: one-rank RCCL step 42.6-43.2
+    // with it vs 43.7-43.8 ms without, profiles/r04_insert_path_ab.txt section 7; rows: the
+    // sides GS_ROWS_TTAS names, bit 0 the hooked root's, bit 1 its new parent's)
+    constexpr bool kTu = !TAKE && (GS_INSERT_TTAS || TRACK || (ROWS && (GS_ROWS_TTAS & 1)));
+    constexpr bool kTv = !TAKE && (GS_INSERT_TTAS || TRACK || (ROWS && (GS_ROWS_TTAS & 2)));
     if (GS_PAIR_INSERT && k0u == kEmpty && k0v == kEmpty && hu != hv && ks != kd && ks != kEmpty && kd != kEmpty) {
-      insert_pair<!TAKE && (GS_INSERT_TTAS || TRACK || ROWS)>(t, ks, hu, kd, hv, su, lu, nu, sv, lv, nv);
+      insert_pair<kTu, kTv>(t, ks, hu, kd, hv, su, lu, nu, sv, lv, nv);
     } else {
-      // (the re-read stays in the exchange's tracked own folds: one-rank RCCL step 42.6-43.2
-      // with it vs 43.7-43.8 ms without, profiles/r04_insert_path_ab.txt section 7)
-      su = lookup_resolve<!TAKE && (GS_INSERT_TTAS || TRACK || ROWS)>(t, ks, hu, k0u, l0u, lu, nu);
-      sv = lookup_resolve<!TAKE && (GS_INSERT_TTAS || TRACK || ROWS)>(t, kd, hv, k0v, l0v, lv, nv);
+      su = lookup_resolve<kTu>(t, ks, hu, k0u, l0u, lu, nu);
+      sv = lookup_resolve<kTv>(t, kd, hv, k0v, l0v, lv, nv);
     }
   }
   nvx = reserve_new_vertices(t, shard, nu, su, nv, sv, TAKE ? D.lnv : nullptr);  // one atomic per wave
@@ -493,7 +506,22 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
     }
     ru = su;
     rv = sv;
-    if (su != kNoSlot && sv != kNoSlot && su != sv) {  // a self-loop adds its vertex, never a conflict
+    // Direct hook of a vertex this thread just inserted under the other endpoint, when that one
+    // exists and has the smaller key (GS_DIRECT_FRESH): the fresh vertex is a singleton root, and
+    // any vertex of the other tree with a smaller key is a valid parent (links still only point
+    // to smaller keys, and the other tree's root stays the minimum), so no find of the other
+    // root is needed. Untracked folds only (a tracked record names the new parent as a root).
+    // One CAS on the fresh slot's link; if another lane hooked it first, the general path below.
+    bool direct = false;
+    if (GS_DIRECT_FRESH && !TRACK && su != kNoSlot && sv != kNoSlot && su != sv && nu != nv) {
+      const bool u_hi = nu && kd < ks, v_hi = nv && ks < kd;
+      if (u_hi || v_hi) {
+        const uint32_t x = u_hi ? su : sv, y = u_hi ? sv : su;
+        const uint32_t desired = (y << 1) | (SIGNED ? (need & 1u) : 0u);
+        direct = atomicCAS(&t.tab[x].link, x << 1, desired) == (x << 1);
+      }
+    }
+    if (!direct && su != kNoSlot && sv != kNoSlot && su != sv) {  // a self-loop adds its vertex, never a conflict
       const uint32_t pu = lu >> 1, pv = lv >> 1;
       if (pu == pv || pu == sv || pv == su) {  // shared parent, or parent/child
         GS_DBG(CTR_DBG_SHORT);

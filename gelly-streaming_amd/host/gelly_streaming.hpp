@@ -95,11 +95,13 @@ struct MapFunction {
 // kind and device whose table size class fits (up to kClassSlack classes larger).
 //
 // HBM budget (the Java HandlePool's model): the pool accounts the HBM of
-// every handle it has handed out (table slots x 16 B + the vertex list's 4 B per slot).
-// Summaries a Flink job drops without release() -- per-emission copies with object reuse
-// off, window partials cleared after a fire -- return their handles only when the JVM
+// every handle it holds or has handed out (table slots x 16 B + the vertex list's 4 B per
+// slot). Summaries a Flink job drops without release() -- per-emission copies with object
+// reuse off, window partials cleared after a fire -- return their handles only when the JVM
 // finalizes them; set_budget's `collect` hook stands for System.gc() +
-// System.runFinalization(), which acquire() runs before a create would pass the budget.
+// System.runFinalization(), which acquire() runs before a create would pass the budget;
+// if that is not enough, pooled handles of other sizes are destroyed first. The total then
+// stays within the budget unless live summaries need more (one table over at a time).
 // --------------------------------------------------------------------------
 class HandlePool {
  public:
@@ -128,23 +130,40 @@ class HandlePool {
     collect_ = std::move(collect);
   }
   gs_handle acquire(int kind, int device, uint64_t capacity_hint) {
-    const uint64_t slots = slots_for(capacity_hint);
+    const uint64_t slots = slots_for(capacity_hint), need = bytes_of_slots(slots);
     if (gs_handle h = take(kind, device, size_class(slots))) return h;
-    if (budget_ && collect_ && outstanding_ + bytes_of_slots(slots) > budget_) {
-      ++collections_;
-      collect_();  // the dropped summaries' destructors release into this pool
-      if (gs_handle h = take(kind, device, size_class(slots))) return h;
+    if (budget_ && total_ + need > budget_) {
+      if (collect_) {
+        ++collections_;
+        collect_();  // the dropped summaries' destructors release into this pool
+        if (gs_handle h = take(kind, device, size_class(slots))) return h;
+      }
+      // still over: pooled handles of other sizes make room before a table is created
+      for (auto it = free_.begin(); it != free_.end() && total_ + need > budget_; ++it)
+        while (!it->second.empty() && total_ + need > budget_) {
+          gs_handle f = it->second.back();
+          it->second.pop_back();
+          --nfree_;
+          total_ -= bytes_[f];
+          bytes_.erase(f);
+          gs_destroy(f);
+        }
     }
     gs_handle h = nullptr;
     gs_check(gs_create(&h, device, kind, capacity_hint));
     ++created_;
-    bytes_[h] = bytes_of_slots(slots);
-    add_outstanding(bytes_[h]);
+    bytes_[h] = need;
+    total_ += need;
+    peak_total_ = std::max(peak_total_, total_);
+    add_outstanding(need);
     return h;
   }
   void release(gs_handle h, int kind, int device) {
     auto it = bytes_.find(h);
-    if (it != bytes_.end()) outstanding_ -= it->second;
+    if (it != bytes_.end()) {
+      outstanding_ -= it->second;
+      total_ -= it->second;
+    }
     uint64_t slots = 0;
     // the value AND the configuration (tracking, pipelining, profiling) of a fresh handle;
     // a table keeps a grown capacity across resets: account and pool it by its real size
@@ -155,6 +174,8 @@ class HandlePool {
     }
     if (nfree_ < kMaxFree) {
       bytes_[h] = bytes_of_slots(slots);
+      total_ += bytes_[h];
+      peak_total_ = std::max(peak_total_, total_);
       free_[{kind, device, size_class(slots)}].push_back(h);
       ++nfree_;
     } else {
@@ -167,6 +188,8 @@ class HandlePool {
   size_t collections() const { return collections_; }
   uint64_t outstanding_bytes() const { return outstanding_; }
   uint64_t peak_outstanding_bytes() const { return peak_; }
+  uint64_t total_bytes() const { return total_; }  // every handle the pool accounts: handed out + pooled
+  uint64_t peak_total_bytes() const { return peak_total_; }
   size_t live_handles() const { return bytes_.size(); }  // handed out + pooled
   ~HandlePool() {
     for (auto& kv : free_)
@@ -195,7 +218,7 @@ class HandlePool {
   std::map<std::tuple<int, int, int>, std::vector<gs_handle>> free_;
   std::map<gs_handle, uint64_t> bytes_;
   size_t nfree_ = 0, created_ = 0, reused_ = 0, collections_ = 0;
-  uint64_t budget_ = 0, outstanding_ = 0, peak_ = 0;
+  uint64_t budget_ = 0, outstanding_ = 0, peak_ = 0, total_ = 0, peak_total_ = 0;
   std::function<void()> collect_;
 };
 

@@ -13,13 +13,13 @@
  * TypeSerializer.copy of the Merger's output when object reuse is off, and the window
  * partials Flink clears after a fire (S/SummaryAggregation.java:107-119,
  * S/SummaryBulkAggregation.java:79-83) -- return their handles only through finalize(),
- * and the JVM heap never feels the pressure that would run it. So the pool keeps the HBM
- * of every handle it has handed out (gs_table_capacity x the slot and vertex-list bytes)
- * and, before a create would take that past gs.hbmBudgetBytes, runs System.gc() and
- * System.runFinalization() (outside its lock: the finalizers release into it) and looks
- * in the free lists again. Free handles are kept by table size class, and a summary asks
- * for the size it needs (a copy: its source's vertex count), so a copy of a small partial
- * does not pin a 2^20-vertex table. The C++ host mirror models this pool and a 1,000-window
+ * and the JVM heap never feels the pressure that would run it. So the pool accounts the HBM
+ * of every handle it holds or has handed out (gs_table_capacity x the slot and vertex-list
+ * bytes) and, before a create would take that past gs.hbmBudgetBytes, runs System.gc() and
+ * System.runFinalization() (outside its lock: the finalizers release into it), looks in
+ * the free lists again, and destroys pooled handles of other sizes to make room. Free
+ * handles are kept by table size class, and a summary asks for the size it needs (a copy:
+ * its source's vertex count), so a copy of a small partial does not pin a 2^20-vertex table. The C++ host mirror models this pool and a 1,000-window
  * run with Flink's copies and dropped partials (tests/cpp/test_handle_budget.cpp).
  */
 package org.apache.flink.graph.streaming.summaries;
@@ -35,7 +35,8 @@ final class HandlePool {
 	/** Expected vertices of a summary whose size is not known (the operator's initial value);
 	 *  the table grows past it on its own. */
 	static final long CAPACITY_HINT = Long.getLong("gs.capacityHint", 1L << 20);
-	/** HBM the handed-out handles may hold before a create makes the JVM finalize dropped summaries. */
+	/** HBM the pool's handles (handed out + pooled) may hold before a create makes the JVM
+	 *  finalize dropped summaries. */
 	static final long BUDGET_BYTES = Long.getLong("gs.hbmBudgetBytes", 32L << 30);
 	static final int MAX_FREE = 64;
 	/** Size classes a request may take from above its own (a bigger pooled table serves it). */
@@ -49,6 +50,7 @@ final class HandlePool {
 	private final Map<Long, Long> bytesOf = new HashMap<>();  // every live handle -> its HBM
 	private int nfree;
 	private long outstandingBytes;  // HBM of the handles handed out
+	private long totalBytes;        // HBM of every live handle: handed out + pooled (what the budget bounds)
 	private long created, reused, collections;
 
 	private HandlePool(int kind) {
@@ -75,15 +77,16 @@ final class HandlePool {
 	}
 
 	/** A handle for a summary of about `hint` vertices: a pooled one of that size class (or up to
-	 *  CLASS_SLACK classes larger), else a new one -- after a finalization pass if the handles
-	 *  handed out would exceed the HBM budget. */
+	 *  CLASS_SLACK classes larger), else a new one -- after a finalization pass (and pooled
+	 *  handles of other sizes destroyed) if it would take the pool past the HBM budget. */
 	long acquire(long hint) {
 		final long slots = slotsFor(hint);
 		Long h = take(sizeClass(slots));
 		if (h != null) {
 			return h;
 		}
-		if (outstanding() + bytesOfSlots(slots) > BUDGET_BYTES) {
+		final long need = bytesOfSlots(slots);
+		if (total() + need > BUDGET_BYTES) {
 			System.gc();
 			System.runFinalization();
 			synchronized (this) {
@@ -93,15 +96,28 @@ final class HandlePool {
 			if (h != null) {
 				return h;
 			}
+			evictFor(need);  // pooled handles of other sizes make room
 		}
 		long nh = GsNative.create(DEVICE, kind, hint);
 		synchronized (this) {
 			created++;
-			long b = bytesOfSlots(slots);
-			bytesOf.put(nh, b);
-			outstandingBytes += b;
+			bytesOf.put(nh, need);
+			outstandingBytes += need;
+			totalBytes += need;
 		}
 		return nh;
+	}
+
+	/** Destroy pooled handles until a table of `need` bytes fits the budget (or none is left). */
+	private synchronized void evictFor(long need) {
+		for (ArrayDeque<Long> q : free.values()) {
+			while (!q.isEmpty() && totalBytes + need > BUDGET_BYTES) {
+				long f = q.poll();
+				nfree--;
+				totalBytes -= bytesOf.remove(f);
+				GsNative.destroy(f);
+			}
+		}
 	}
 
 	private synchronized Long take(int cls) {
@@ -127,6 +143,7 @@ final class HandlePool {
 		Long b = bytesOf.get(h);
 		if (b != null) {
 			outstandingBytes -= b;
+			totalBytes -= b;
 		}
 		long slots;
 		try {
@@ -139,6 +156,7 @@ final class HandlePool {
 		}
 		if (nfree < MAX_FREE) {
 			bytesOf.put(h, bytesOfSlots(slots));
+			totalBytes += bytesOfSlots(slots);
 			free.computeIfAbsent(sizeClass(slots), k -> new ArrayDeque<>()).push(h);
 			nfree++;
 		} else {
@@ -149,6 +167,10 @@ final class HandlePool {
 
 	synchronized long outstanding() {
 		return outstandingBytes;
+	}
+
+	synchronized long total() {
+		return totalBytes;
 	}
 
 	synchronized long created() {

@@ -9,8 +9,8 @@
 //     copy is dropped once the sink is done.
 // The dropped summaries' handles come back only when the JVM finalizes them. Here they go
 // to a finalizer queue that is emptied only when the pool's byte budget asks for it (the
-// Java pool's System.gc() + System.runFinalization()). The run must keep the handles handed
-// out within the budget (plus the one create that triggers a pass) and end with the
+// Java pool's System.gc() + System.runFinalization()). The run must keep the HBM the pool
+// accounts (handles handed out + pooled) within the budget (plus one table) and end with the
 // oracle's summary.
 // Usage: test_handle_budget <edges.bin: int64 src,dst pairs> <window edges> <budget bytes> <out.bin>
 // out.bin: int64 n, then n rows of int64 {v, label}. Prints one JSON line of pool statistics.
@@ -90,12 +90,13 @@ int main(int argc, char** argv) {
     if (!g || std::fwrite(o.data(), 8, o.size(), g) != o.size()) die("cannot write output");
     std::fclose(g);
     std::printf(
-        "{\"windows\": %zu, \"budget\": %llu, \"peak_outstanding\": %llu, \"worst_after_window\": %llu, "
+        "{\"windows\": %zu, \"budget\": %llu, \"peak_outstanding\": %llu, \"peak_total\": %llu, "
+        "\"worst_after_window\": %llu, "
         "\"created\": %zu, \"reused\": %zu, \"collections\": %zu, \"finalized\": %zu, \"max_queue\": %zu, "
         "\"live_handles\": %zu}\n",
         windows, (unsigned long long)budget, (unsigned long long)pool.peak_outstanding_bytes(),
-        (unsigned long long)worst, pool.created(), pool.reused(), pool.collections(), finalized, max_queue,
-        pool.live_handles());
+        (unsigned long long)pool.peak_total_bytes(), (unsigned long long)worst, pool.created(), pool.reused(),
+        pool.collections(), finalized, max_queue, pool.live_handles());
     finalizer_queue.clear();
     summary.reset();
   } catch (const std::exception& x) {

@@ -175,7 +175,9 @@ def test_transient_state_operators_match_oracle(oracle_mod, tmp_path, kind, p):
             want = oracle_mod.canonical_candidates_string(*oracle_mod.bip_truth(ws, wd))
             assert got[w] == want, w
             fails += want == "(false,{})"
-        assert fails == 1  # the injected odd cycle's window only: the state does not carry over
+        # the injected edge closes an odd cycle with edges of EARLIER windows: the whole stream is not
+        # bipartite, yet no window alone fails -- the reset state carries no verdict over
+        assert not oracle_mod.bip_truth(s, d)[0] and fails == 0
     m = re.search(r"handles created (\d+) reused (\d+)", r.stdout)
     created, reused = int(m.group(1)), int(m.group(2))
     assert created <= 2 * p + 4 and reused >= nwin, r.stdout
@@ -187,8 +189,8 @@ def test_handle_budget_bounds_hbm_under_flink_copies(oracle_mod, tmp_path):
     initial value, the partial the combine drops is never released, and every emission is
     copied (sized from the summary's vertex count) and dropped after the sink reads it. Dropped
     summaries return their handles only when the modelled finalizer runs, which the pool's byte
-    budget triggers (System.gc() + System.runFinalization() in HandlePool.java). The handed-out
-    HBM stays within the budget plus one table, the finalizer runs repeatedly, the handles the
+    budget triggers (System.gc() + System.runFinalization() in HandlePool.java). The HBM the pool
+    accounts (handed out + pooled) stays within the budget plus one table, the finalizer runs repeatedly, the handles the
     pool holds stay bounded, and the final summary equals the oracle."""
     import numpy as np
     W, nw = 1024, 1000
@@ -202,7 +204,7 @@ def test_handle_budget_bounds_hbm_under_flink_copies(oracle_mod, tmp_path):
     st = json.loads(r.stdout.strip().splitlines()[-1])
     assert st["windows"] == nw
     default_table = (1 << 18) * 20  # hint 2^16 -> 2^18 slots x (16 B slot + 4 B vertex list)
-    assert st["peak_outstanding"] <= budget + default_table, st
+    assert st["peak_total"] <= budget + default_table, st  # handed out + pooled
     assert st["collections"] >= 10 and st["finalized"] >= nw, st  # ~2 dropped summaries per window
     assert st["max_queue"] <= 2 * nw // 10, st  # drained every few windows, not left to grow
     assert st["live_handles"] <= 64 + 1 + st["max_queue"], st  # pooled (<= kMaxFree) + the summary + the queue

@@ -116,6 +116,7 @@ def test_handle_pool_hbm_budget_by_construction():
     acq = re.search(r"\tlong acquire\(long hint\) \{(.*?)\n\t\}", pool, flags=re.S).group(1)
     assert "System.gc();" in acq and "System.runFinalization();" in acq
     assert "BUDGET_BYTES" in acq and "synchronized long acquire" not in pool  # not under the pool's lock
+    assert "total() + need > BUDGET_BYTES" in acq and "evictFor(need)" in acq
     assert acq.index("System.runFinalization();") < acq.index("GsNative.create(")
     assert "GsNative.tableCapacity(h)" in pool
     ser = _read(os.path.join(PKG, "GpuSummarySerializer.java"))

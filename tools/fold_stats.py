@@ -46,8 +46,11 @@ def main():
     ap.add_argument("cfg", choices=["r20", "bip", "rmat26"])
     ap.add_argument("--batches", type=int, default=16)
     ap.add_argument("--passes", type=int, default=2, help="the last pass is printed (the first sizes the table)")
+    ap.add_argument("--hint-log2", type=int, default=0, help="capacity hint (log2 vertices; 0: the bench's)")
     a = ap.parse_args()
     kind, hint, src, dst, nb = stream(a.cfg, a.batches)
+    if a.hint_log2:
+        hint = 1 << a.hint_log2
     B = 1 << 20
     s = gs.Summary(kind, capacity_hint=hint)
     keys = None
