@@ -118,9 +118,6 @@ struct FoldArgs {
 #ifndef GS_ROWS_TTAS
 #define GS_ROWS_TTAS 3  // other replicas' rows: re-read before the key CAS on both sides (experiment switch)
 #endif
-#ifndef GS_DIRECT_FRESH
-#define GS_DIRECT_FRESH 0  // direct hook of a freshly inserted larger-key endpoint (experiment switch)
-#endif
 #ifndef GS_COMBINE_ROUNDS
 #define GS_COMBINE_ROUNDS 2
 #endif
@@ -506,19 +503,36 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
     }
     ru = su;
     rv = sv;
-    // Direct hook of a vertex this thread just inserted under the other endpoint, when that one
-    // exists and has the smaller key (GS_DIRECT_FRESH): the fresh vertex is a singleton root, and
-    // any vertex of the other tree with a smaller key is a valid parent (links still only point
-    // to smaller keys, and the other tree's root stays the minimum), so no find of the other
-    // root is needed. Untracked folds only (a tracked record names the new parent as a root).
-    // One CAS on the fresh slot's link; if another lane hooked it first, the general path below.
+    // GS_SETTLE: this lane's fresh slots get their first link now (other lanes' hook CASes on
+    // them wait for it). A fresh vertex whose other endpoint is known with a smaller key hangs
+    // straight under it (both fresh: the larger under the smaller) -- the edge is then done by
+    // the insert alone; the shortcut below sees the parent/child pair and, signed, the parity.
     bool direct = false;
-    if (GS_DIRECT_FRESH && !TRACK && su != kNoSlot && sv != kNoSlot && su != sv && nu != nv) {
-      const bool u_hi = nu && kd < ks, v_hi = nv && ks < kd;
-      if (u_hi || v_hi) {
-        const uint32_t x = u_hi ? su : sv, y = u_hi ? sv : su;
-        const uint32_t desired = (y << 1) | (SIGNED ? (need & 1u) : 0u);
-        direct = atomicCAS(&t.tab[x].link, x << 1, desired) == (x << 1);
+    if (kSettle && (nu || nv)) {
+      const uint32_t par = SIGNED ? (need & 1u) : 0u;
+      const bool two = su != kNoSlot && sv != kNoSlot && su != sv;
+      uint32_t fu = su << 1, fv = sv << 1;  // first links: the slot itself, a root
+      if (two && nu && kd < ks) fu = (sv << 1) | par;       // u fresh, the larger key: under v
+      else if (two && nv && ks < kd) fv = (su << 1) | par;  // v fresh, the larger key: under u
+      if (nu) {
+        settle_slot(t, su, fu);
+        lu = fu;
+      }
+      if (nv && sv != su) {
+        settle_slot(t, sv, fv);
+        lv = fv;
+      }
+      direct = two && ((nu && (fu >> 1) == sv) || (nv && (fv >> 1) == su));
+      if (direct) {
+        GS_DBG(CTR_DBG_HOOKOK);
+        if (TRACK) {  // the insert was the join: its record {hi key, lo key, parity}
+          has_rec = true;
+          rec[0] = ks < kd ? kd : ks;
+          rec[1] = ks < kd ? ks : kd;
+          rec[2] = (int64_t)par;
+        }
+        if (nu && (fu >> 1) == sv) fresh0 = kNoSlot;  // no longer a root of its own
+        if (nv && (fv >> 1) == su) fresh1 = kNoSlot;
       }
     }
     if (!direct && su != kNoSlot && sv != kNoSlot && su != sv) {  // a self-loop adds its vertex, never a conflict

@@ -47,7 +47,7 @@ public class GpuSummarySerializer extends Serializer<GpuSummary> {
 	public GpuSummary copy(Kryo kryo, GpuSummary original) {
 		GpuSummary c = fresh(original.getClass());
 		original.flush();
-		c.sizeFor(GsNative.numVertices(original.handle()));
+		c.sizeFor(2 * GsNative.numVertices(original.handle()));  // (the combine charges each row as an edge)
 		GsNative.combine(c.handle(), original.handle());  // the verdict travels with the rows
 		return c;
 	}

@@ -28,10 +28,11 @@ static void die(const std::string& m) {
   std::exit(1);
 }
 
-// GpuSummarySerializer.copy: a fresh summary sized from the source's vertex count, combined into
+// GpuSummarySerializer.copy: a fresh summary sized from the source's vertex count (x 2: the
+// combine's capacity check charges each exported row as an edge), combined into
 static DisjointSetRef copy_of(DisjointSet& src, uint64_t default_hint) {
   auto c = std::make_shared<DisjointSet>(0, default_hint);
-  c->size_for(src.size());
+  c->size_for(2 * src.size());
   c->merge(src);
   return c;
 }

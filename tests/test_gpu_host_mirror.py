@@ -204,7 +204,9 @@ def test_handle_budget_bounds_hbm_under_flink_copies(oracle_mod, tmp_path):
     st = json.loads(r.stdout.strip().splitlines()[-1])
     assert st["windows"] == nw
     default_table = (1 << 18) * 20  # hint 2^16 -> 2^18 slots x (16 B slot + 4 B vertex list)
-    assert st["peak_total"] <= budget + default_table, st  # handed out + pooled
+    # handed out + pooled; a table that grows while handed out is seen at its release, so one
+    # more table's worth of slack than the create that may pass the budget
+    assert st["peak_total"] <= budget + 2 * default_table, st
     assert st["collections"] >= 10 and st["finalized"] >= nw, st  # ~2 dropped summaries per window
     assert st["max_queue"] <= 2 * nw // 10, st  # drained every few windows, not left to grow
     assert st["live_handles"] <= 64 + 1 + st["max_queue"], st  # pooled (<= kMaxFree) + the summary + the queue

@@ -121,7 +121,7 @@ def test_handle_pool_hbm_budget_by_construction():
     assert "GsNative.tableCapacity(h)" in pool
     ser = _read(os.path.join(PKG, "GpuSummarySerializer.java"))
     copy = re.search(r"public GpuSummary copy\(.*?\n\t\}", ser, flags=re.S).group(0)
-    assert "sizeFor(GsNative.numVertices(original.handle()))" in copy
+    assert "sizeFor(2 * GsNative.numVertices(original.handle()))" in copy
     assert copy.index("sizeFor(") < copy.index("c.handle()")
     for cls, p in (("GpuDisjointSet", "CC"), ("GpuCandidates", "SIGNED")):
         assert "HandlePool.%s.acquire(GpuSummary.hintFor(sized, image))" % p in _read(os.path.join(PKG, cls + ".java"))
