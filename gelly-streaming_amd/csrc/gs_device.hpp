@@ -114,21 +114,6 @@ __host__ __device__ constexpr int ctr_index(int c) { return c * kCtrStride; }
 constexpr uint32_t kAuxPresent = 1u;  // reserved slot only: INT64_MIN is a vertex
 constexpr uint32_t kAuxNew = 2u;      // change tracking: inserted since the last emission
 constexpr uint32_t kAuxBig = 4u;      // change emission: a root whose absorbed list is too long to walk
-constexpr uint32_t kAuxSettled = 8u;  // GS_SETTLE: the inserter has written the slot's first link (word B)
-
-// Settled inserts (GS_SETTLE). The key CAS claims a slot as before; the winner then writes
-// the slot's word B = {link, aux} in ONE write-through store: its first link -- itself, or,
-// when the edge's other endpoint is already known with a smaller key, that endpoint (a
-// direct hook: a singleton root may hang under any vertex of a tree whose root has a
-// smaller key) -- with kAuxSettled. A hook CAS is 64-bit on word B and expects
-// kAuxSettled, so it cannot land on a slot whose first link is still to come (it waits
-// for the store instead): a fresh vertex needs one atomic, not a key CAS plus a hook CAS.
-// Other replicas' rows insert their hooked root and hang it under its new parent this way
-// (55 % of remote rows, each two atomics before), and so do a young table's inserts.
-#ifndef GS_SETTLE
-#define GS_SETTLE 0
-#endif
-constexpr bool kSettle = GS_SETTLE != 0;
 
 struct alignas(16) Slot {
   int64_t key;
@@ -178,44 +163,10 @@ __device__ __forceinline__ void load_slot(const Slot* p, int64_t& key, uint32_t&
   link = v.z;
 }
 
-// Both endpoints' first probes as L1-bypassing (sc1, L2-served) 16-B loads in flight together
-// (experiment switch GS_PROBE_SC1): a plain load may return a line the CU's L1 holds from
-// before another CU's insert, an EMPTY that the key CAS then has to settle.
-#ifndef GS_PROBE_SC1
-#define GS_PROBE_SC1 0
-#endif
-__device__ __forceinline__ void load_slot2_sc1(const Slot* pa, const Slot* pb, int64_t& ka, uint32_t& la, int64_t& kb,
-                                               uint32_t& lb) {
-  uint4 a, b;
-  asm volatile(
-      "global_load_dwordx4 %0, %2, off sc1\n\t"
-      "global_load_dwordx4 %1, %3, off sc1\n\t"
-      "s_waitcnt vmcnt(0)"
-      : "=&v"(a), "=&v"(b)
-      : "v"(pa), "v"(pb)
-      : "memory");
-  ka = (int64_t)(((uint64_t)a.y << 32) | a.x);
-  la = a.z;
-  kb = (int64_t)(((uint64_t)b.y << 32) | b.x);
-  lb = b.z;
-}
-
 __device__ __forceinline__ uint32_t load_link_fresh(const Slot* p) {
   return __hip_atomic_load(&p->link, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// word B of a slot: link | aux << 32
-__device__ __forceinline__ unsigned long long* word_b(const Table& t, uint32_t s) {
-  return reinterpret_cast<unsigned long long*>(&t.tab[s].link);
-}
-__device__ __forceinline__ unsigned long long pack_b(uint32_t link, uint32_t aux) {
-  return (unsigned long long)link | ((unsigned long long)aux << 32);
-}
-// GS_SETTLE: the inserter's first link (write-through: in memory, not in this XCD's L2, when it lands)
-__device__ __forceinline__ void settle_slot(const Table& t, uint32_t s, uint32_t link) {
-  __hip_atomic_store(word_b(t, s), pack_b(link, kAuxSettled | (t.mark_new ? kAuxNew : 0u)), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // A key read as EMPTY for an occupied slot is a stale line: settle it at the
 // memory-side atomic unit (rare path).
@@ -266,7 +217,7 @@ __device__ __forceinline__ uint32_t lookup_resolve(const Table& t, int64_t key, 
       if (old != (unsigned long long)kEmpty) GS_DBG(CTR_DBG_KCAS_LOST);
       if (old == (unsigned long long)kEmpty) {
         fresh = true;
-        if (!kSettle && t.mark_new) t.tab[h].aux = kAuxNew;  // only the inserting thread writes a fresh slot's aux
+        if (t.mark_new) t.tab[h].aux = kAuxNew;  // only the inserting thread writes a fresh slot's aux
         link = h << 1;  // table init: every slot is its own root
         return h;
       }
@@ -293,7 +244,7 @@ __device__ __forceinline__ uint32_t insert_finish(const Table& t, int64_t key, u
   if (tried && old != (unsigned long long)kEmpty) GS_DBG(CTR_DBG_KCAS_LOST);
   if (tried && old == (unsigned long long)kEmpty) {
     fresh = true;
-    if (!kSettle && t.mark_new) t.tab[h].aux = kAuxNew;
+    if (t.mark_new) t.tab[h].aux = kAuxNew;
     link = h << 1;
     return h;
   }
@@ -639,29 +590,8 @@ __device__ __forceinline__ bool hook(const Table& t, uint32_t a, uint32_t la, in
     const uint32_t desired = (lo << 1) | (SIGNED ? (need & 1u) : 0u);
     const bool own = GS_FRESH_HOOK_SKIP && first && (hi == fresh0 || hi == fresh1);
     first = false;
-    uint32_t old;
-    if (kSettle) {
-      // 64-bit CAS on {link, aux}: only a settled root is hooked, and its aux bits are kept. A
-      // root this thread inserted (own) was settled by it: {self, kAuxSettled [| kAuxNew]}.
-      unsigned long long w = own ? pack_b(expect, kAuxSettled | (t.mark_new ? kAuxNew : 0u))
-                                 : __hip_atomic_load(word_b(t, hi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (;;) {
-        if ((uint32_t)w != expect) break;  // moved: follow it (no CAS)
-        if (!((uint32_t)(w >> 32) & kAuxSettled)) {
-          // inserted by another lane whose first link is on its way: read it at the memory side
-          __builtin_amdgcn_s_sleep(1);
-          w = atomicOr(word_b(t, hi), 0ull);
-          continue;
-        }
-        const unsigned long long o = atomicCAS(word_b(t, hi), w, pack_b(desired, (uint32_t)(w >> 32)));
-        if (o == w) break;
-        w = o;  // aux bits or the link changed meanwhile: decide again on the live word
-      }
-      old = (uint32_t)w;
-    } else {
-      const uint32_t seen = own ? expect : load_link_fresh(t.tab + hi);
-      old = seen == expect ? atomicCAS(&t.tab[hi].link, expect, desired) : seen;
-    }
+    const uint32_t seen = own ? expect : load_link_fresh(t.tab + hi);
+    const uint32_t old = seen == expect ? atomicCAS(&t.tab[hi].link, expect, desired) : seen;
     if (old == expect) {
       GS_DBG(CTR_DBG_HOOKOK);
       if (TRACK) {

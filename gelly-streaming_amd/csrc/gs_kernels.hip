@@ -456,12 +456,8 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
   int64_t k0u = 0, k0v = 0;
   uint32_t l0u = 0, l0v = 0;
   if (valid) {
-    if (GS_PROBE_SC1) {
-      load_slot2_sc1(t.tab + hu, t.tab + hv, k0u, l0u, k0v, l0v);
-    } else {
-      load_slot(t.tab + hu, k0u, l0u);
-      load_slot(t.tab + hv, k0v, l0v);
-    }
+    load_slot(t.tab + hu, k0u, l0u);
+    load_slot(t.tab + hv, k0v, l0v);
   }
   uint32_t ru = 0, rv = 0, lu = 0, lv = 0;
   int64_t kru = 0, krv = 0;
@@ -503,39 +499,7 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
     }
     ru = su;
     rv = sv;
-    // GS_SETTLE: this lane's fresh slots get their first link now (other lanes' hook CASes on
-    // them wait for it). A fresh vertex whose other endpoint is known with a smaller key hangs
-    // straight under it (both fresh: the larger under the smaller) -- the edge is then done by
-    // the insert alone; the shortcut below sees the parent/child pair and, signed, the parity.
-    bool direct = false;
-    if (kSettle && (nu || nv)) {
-      const uint32_t par = SIGNED ? (need & 1u) : 0u;
-      const bool two = su != kNoSlot && sv != kNoSlot && su != sv;
-      uint32_t fu = su << 1, fv = sv << 1;  // first links: the slot itself, a root
-      if (two && nu && kd < ks) fu = (sv << 1) | par;       // u fresh, the larger key: under v
-      else if (two && nv && ks < kd) fv = (su << 1) | par;  // v fresh, the larger key: under u
-      if (nu) {
-        settle_slot(t, su, fu);
-        lu = fu;
-      }
-      if (nv && sv != su) {
-        settle_slot(t, sv, fv);
-        lv = fv;
-      }
-      direct = two && ((nu && (fu >> 1) == sv) || (nv && (fv >> 1) == su));
-      if (direct) {
-        GS_DBG(CTR_DBG_HOOKOK);
-        if (TRACK) {  // the insert was the join: its record {hi key, lo key, parity}
-          has_rec = true;
-          rec[0] = ks < kd ? kd : ks;
-          rec[1] = ks < kd ? ks : kd;
-          rec[2] = (int64_t)par;
-        }
-        if (nu && (fu >> 1) == sv) fresh0 = kNoSlot;  // no longer a root of its own
-        if (nv && (fv >> 1) == su) fresh1 = kNoSlot;
-      }
-    }
-    if (!direct && su != kNoSlot && sv != kNoSlot && su != sv) {  // a self-loop adds its vertex, never a conflict
+    if (su != kNoSlot && sv != kNoSlot && su != sv) {  // a self-loop adds its vertex, never a conflict
       const uint32_t pu = lu >> 1, pv = lv >> 1;
       if (pu == pv || pu == sv || pv == su) {  // shared parent, or parent/child
         GS_DBG(CTR_DBG_SHORT);

@@ -5,8 +5,6 @@ set -o pipefail
 O=gpurun_out/${1:-r05f}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
-GS_LIB_VARIANT=settle timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests_settle.txt 2>&1
-rc=$?; tail -2 $O/gpu_tests_settle.txt; [ $rc = 0 ] || exit $rc
 for v in base settle; do
   if [ $v = base ]; then E="X=1"; else E="GS_LIB_VARIANT=$v"; fi
   env $E timeout -k 10 200 python tools/rank_replay.py --row-stats --reps 2 --lag 2 > $O/replay_$v.txt 2>&1 || exit 1
@@ -27,5 +25,7 @@ for v in base settle; do
   env $E timeout -k 10 120 python tools/fold_stats.py bip > $O/bip_times_$v.txt 2>&1 || exit 1
   env $E timeout -k 10 120 python tools/fold_stats.py r20 > $O/r20_times_$v.txt 2>&1 || exit 1
 done
-bash tools/r05_tablesize.sh ${1:-r05f}_ts
-echo "rc=$?"
+bash tools/r05_tablesize.sh ${1:-r05f}_ts || exit 1
+GS_LIB_VARIANT=settle timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests_settle.txt 2>&1
+rc=$?; tail -2 $O/gpu_tests_settle.txt
+echo "rc=$rc"
