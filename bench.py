@@ -380,6 +380,9 @@ def bench_bip(args):
                 "bytes_per_edge": BYTES_PER_EDGE_SPARSE, "edges_per_launch": int(per_launch),
                 "fold_avg_us": round(fold_avg_ms * 1e3, 2), "fold_launches": int(nf)}
         roof.update(extra)
+        col = summ.colouring()
+        roof["atomic_floor"] = atomic_floor(summ.num_vertices(), len(np.unique(col[1])) if col[0] else 0,
+                                            el * 1e3 / args.steps)
     if args.profile_only:  # profiling run: the timed steps only
         if group is not None:
             group.close()
@@ -742,6 +745,21 @@ def bench_dropin(args):
     print(json.dumps(line), flush=True)
 
 
+ATOMIC_CAS64_PER_S = 26.07e9  # random 64-bit CAS over a 2 GiB table (profiles/r01_calib_atomic.log)
+
+
+def atomic_floor(vertices, components, step_ms):
+    """The memory-side atomics a pass cannot avoid: one key CAS per vertex
+    inserted and one hook CAS per union that joins two trees (vertices - components), at the
+    calibrated random-CAS rate. A young table's micro-batches are bound by these, not by the
+    read-request rate the steady batches run at."""
+    n = 2 * int(vertices) - int(components)
+    floor_ms = n / ATOMIC_CAS64_PER_S * 1e3
+    return {"atomics_min_per_step": n, "vertices": int(vertices), "components": int(components),
+            "ceiling_per_s": ATOMIC_CAS64_PER_S, "floor_ms": round(floor_ms, 4),
+            "floor_frac_of_step": round(floor_ms / step_ms, 4), "source": "profiles/r01_calib_atomic.log"}
+
+
 def rccl_setting():
     """config.rccl: the channel cap every communicator of this process was created with (the env
     RCCL reads at communicator creation; None = RCCL's default)."""
@@ -943,6 +961,10 @@ def main():
         if grouped:
             roof["note"] = ("exchange path: fold launches include the other ranks' gathered rows (side stream); "
                             "achieved assumes 2^20 own edges per launch")
+        else:  # the label pass's output of the profile step: its distinct labels are the components
+            nl = int(nlabels[0])
+            roof["atomic_floor"] = atomic_floor(nl, int(torch.unique(out_l[:nl]).numel()),
+                                                elapsed * 1e3 / args.steps)
 
     # Per-phase device time of the exchange protocol, one extra untimed
     # step with timing events around each phase (gs_group_set_phase_timing): the N > 1

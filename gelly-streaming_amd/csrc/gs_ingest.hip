@@ -288,7 +288,7 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
                                            int64_t* __restrict__ dst, uint64_t cap,
                                            unsigned long long* __restrict__ bad, bool aligned, uint64_t tile,
                                            unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat,
-                                           unsigned long long lb_timeout);
+                                           unsigned long long lb_timeout, unsigned long long selfcount);
 
 // Single pass (GS_PARSE_FUSED, default): no k_count_lines pass and no scan. Every block
 // counts its tile's '\n' from the masks it builds anyway and finds the count before its
@@ -342,9 +342,26 @@ __device__ __forceinline__ uint32_t nl_count16(const uint4& v) {
 // per round); publishes the tile's inclusive count. agg = the tile's own '\n' count.
 // Between unsuccessful rounds the wave backs off (s_sleep 8 -> 64): every waiting wave
 // re-reading 64 status words at once slowed the other blocks' staging loads.
+// Bounded self-count (selfcount ticks, GS_PARSE_SELFCOUNT_US): once a round has waited that
+// long, the wave counts the '\n' of every predecessor in its window that has published nothing
+// yet (the whole wave reads that 16 KiB tile: 16 loads of 16 B per lane) and uses the count as
+// the tile's aggregate -- what the tile itself publishes from the same bytes. The waits are for
+// tiles of an XCD that has fallen behind in dispatch; counting one costs
+// a tile read instead of waiting for that XCD. Aligned texts only.
+__device__ __forceinline__ unsigned long long self_count_tile(const uint8_t* __restrict__ text, int64_t tp) {
+  const uint4* v = reinterpret_cast<const uint4*>(text + (uint64_t)tp * kTile);
+  unsigned long long c = 0;
+#pragma unroll 4
+  for (uint32_t q = threadIdx.x & 63; q < kTile / 16; q += 64) c += nl_count16(v[q]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+  return c;
+}
+
 __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restrict__ text, unsigned long long* status,
                                                         unsigned long long* pstat, uint64_t tile, unsigned long long agg,
-                                                        bool published, unsigned long long lb_timeout) {
+                                                        bool published, unsigned long long lb_timeout,
+                                                        unsigned long long selfcount, bool aligned) {
   const int lane = threadIdx.x & 63;
   if (tile == 0) {
     if (lane == 0) __hip_atomic_store(pstat, kStP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -365,12 +382,24 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
     const unsigned long long wa =
         ti >= 0 ? __hip_atomic_load(status + ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     const bool has_p = (wp & kStP) != 0;
-    const unsigned long long w = has_p ? wp : wa;
-    const unsigned long long pm = __ballot(has_p), am = __ballot(has_p || st_has_agg(wa));
+    unsigned long long w = has_p ? wp : wa;
+    const unsigned long long pm = __ballot(has_p);
+    unsigned long long am = __ballot(has_p || st_has_agg(wa));
     const int j = pm ? __ffsll((long long)pm) - 1 : 64;  // nearest final prefix in this window
     const unsigned long long need = j >= 64 ? ~0ull : ((2ull << j) - 1ull);  // lanes 0..j
+    if ((am & need) != need && aligned && wall_clock64() - t_start > selfcount) {
+      // bounded self-count of the silent predecessors (wave-uniform loop over their lanes)
+      unsigned long long miss = need & ~am & __ballot(ti >= 0);
+      while (miss) {
+        const int l = __ffsll((long long)miss) - 1;
+        miss &= miss - 1;
+        const unsigned long long c = self_count_tile(text, base - l);
+        if (lane == l) w = kStA | c;
+      }
+      am = need;
+    }
     if ((am & need) == need) {
-      unsigned long long v = lane <= j ? (has_p ? (w & kStVal) : st_agg(w)) : 0ull;
+      unsigned long long v = lane <= j ? ((w & kStP) ? (w & kStVal) : st_agg(w)) : 0ull;
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
       excl += v;
@@ -409,8 +438,9 @@ __global__ __launch_bounds__(256) void k_parse_fused(const uint8_t* __restrict__
                                                      int64_t* __restrict__ src, int64_t* __restrict__ dst, uint64_t cap,
                                                      unsigned long long* __restrict__ bad, bool aligned,
                                                      unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat,
-                                                     unsigned long long lb_timeout) {
-  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, blockIdx.x, status, pstat, lb_timeout);
+                                                     unsigned long long lb_timeout, unsigned long long selfcount) {
+  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, blockIdx.x, status, pstat, lb_timeout,
+                   selfcount);
 }
 
 // One tile per block (44 VGPRs, 8 blocks per CU).
@@ -418,7 +448,8 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
                                                const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                                int64_t* __restrict__ dst, uint64_t cap,
                                                unsigned long long* __restrict__ bad, bool aligned, uint64_t tile0) {
-  parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile0 + blockIdx.x, nullptr, nullptr, 0ull);
+  parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile0 + blockIdx.x, nullptr, nullptr, 0ull,
+                    0ull);
 }
 
 template <bool FUSED>
@@ -427,7 +458,7 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
                                            int64_t* __restrict__ dst, uint64_t cap,
                                            unsigned long long* __restrict__ bad, bool aligned, uint64_t tile,
                                            unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat,
-                                           unsigned long long lb_timeout) {
+                                           unsigned long long lb_timeout, unsigned long long selfcount) {
   constexpr uint32_t kSeg = kTile / 256;  // bytes per thread in the line-start scan
   constexpr uint32_t kExtra = 2;          // '\n' masks past the tile: lines that cross its end
   constexpr uint32_t kSlots = (kTile + kOver + 4095) / 4096;
@@ -603,7 +634,7 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
     if (wid == 0) {
       const unsigned long long e =
           look_back(text, status, pstat, tile, (unsigned long long)wnl[0] + wnl[1] + wnl[2] + wnl[3], early,
-                    lb_timeout);
+                    lb_timeout, selfcount, aligned);
       if (lane == 0) pre_sh = e;
     }
     __syncthreads();
@@ -667,8 +698,12 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
     // counts the '\n' before its tile itself (default ~50 ms; 0: at once)
     const char* lbe = getenv("GS_PARSE_LB_TIMEOUT_US");
     const unsigned long long lb_timeout = lbe ? 100ull * strtoull(lbe, nullptr, 10) : 5000000ull;
+    // GS_PARSE_SELFCOUNT_US (experiment knob): the bounded self-count of silent predecessors after
+    // that many microseconds of waiting (unset: never)
+    const char* sce = getenv("GS_PARSE_SELFCOUNT_US");
+    const unsigned long long selfcount = sce ? 100ull * strtoull(sce, nullptr, 10) : ~0ull;
     hipLaunchKernelGGL(k_parse_fused, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, src, dst,
-                       (uint64_t)cap, s.bad, aligned, agg, pre, lb_timeout);
+                       (uint64_t)cap, s.bad, aligned, agg, pre, lb_timeout, selfcount);
     if (kev1 && hipEventRecord(kev1, st) != hipSuccess) return -1;
     hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
                        s.bad, s.res, host_res, seq, pre);
