@@ -348,6 +348,12 @@ __device__ __forceinline__ uint32_t nl_count16(const uint4& v) {
 // the tile's aggregate -- what the tile itself publishes from the same bytes. The waits are for
 // tiles of an XCD that has fallen behind in dispatch; counting one costs
 // a tile read instead of waiting for that XCD. Aligned texts only.
+#ifndef GS_LB_FALLBACK16
+#define GS_LB_FALLBACK16 1  // 0: the fallback counts one byte per lane and load (experiment switch)
+#endif
+#ifndef GS_LB_SELFCOUNT
+#define GS_LB_SELFCOUNT 1  // 0: no self-count code in the look-back (experiment switch)
+#endif
 __device__ __forceinline__ unsigned long long self_count_tile(const uint8_t* __restrict__ text, int64_t tp) {
   const uint4* v = reinterpret_cast<const uint4*>(text + (uint64_t)tp * kTile);
   unsigned long long c = 0;
@@ -387,7 +393,7 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
     unsigned long long am = __ballot(has_p || st_has_agg(wa));
     const int j = pm ? __ffsll((long long)pm) - 1 : 64;  // nearest final prefix in this window
     const unsigned long long need = j >= 64 ? ~0ull : ((2ull << j) - 1ull);  // lanes 0..j
-    if ((am & need) != need && aligned && wall_clock64() - t_start > selfcount) {
+    if (GS_LB_SELFCOUNT && (am & need) != need && aligned && wall_clock64() - t_start > selfcount) {
       // bounded self-count of the silent predecessors (wave-uniform loop over their lanes)
       unsigned long long miss = need & ~am & __ballot(ti >= 0);
       while (miss) {
@@ -412,12 +418,16 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
       // and load made a late tile of a large text millions of dependent loads)
       unsigned long long c = 0;
       const uint64_t end = tile * kTile;
+#if GS_LB_FALLBACK16
       const uint64_t head = min(end, (uint64_t)((16u - ((uintptr_t)text & 15u)) & 15u));
       for (uint64_t q = (uint64_t)lane; q < head; q += 64) c += text[q] == '\n';
       const uint4* v16 = reinterpret_cast<const uint4*>(text + head);
       const uint64_t n16 = (end - head) / 16;
       for (uint64_t q = (uint64_t)lane; q < n16; q += 64) c += nl_count16(v16[q]);
       for (uint64_t q = head + 16 * n16 + (uint64_t)lane; q < end; q += 64) c += text[q] == '\n';
+#else
+      for (uint64_t q = (uint64_t)lane; q < end; q += 64) c += text[q] == '\n';
+#endif
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
       excl = c;
