@@ -322,8 +322,6 @@ struct gs_group {
   uint64_t ramp_edges = 1ull << 22, ramp_batch = 1ull << 20;  // gs_group_set_ramp
   uint64_t done = 0;    // exchanges whose data half has been issued
   int data_lag = 2;     // exchanges between an exchange's own fold and its data half (GS_GROUP_DATA_LAG: 1..kLag)
-  bool eager = true;    // GS_GROUP_EAGER (default 1): data halves issued as soon as their counts land, the host
-                        // blocking only when kLag exchanges are outstanding (data_lag then unused)
   uint64_t api_seen = 0;  // h->api_calls at the previous fold call (lane ordering)
   // statistics
   uint64_t exchanges = 0, rows_received = 0, live_received = 0;
@@ -515,7 +513,6 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   if (const char* m = getenv("GS_GROUP_LANES")) g->no_lanes = atoi(m) == 0;
   if (const char* m = getenv("GS_GROUP_SIDE")) g->no_side = atoi(m) == 0;
   if (const char* m = getenv("GS_GROUP_DATA_LAG")) g->data_lag = std::min(kLag, std::max(1, atoi(m)));
-  if (const char* m = getenv("GS_GROUP_EAGER")) g->eager = atoi(m) != 0;
   auto bail = [&](int code) {
     gs_group_destroy(g);
     return code;
@@ -578,10 +575,10 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   const int d = (int)(b % gs::kDeltaSets), k = (int)(b % kLag);  // delta set, buffer set
   g->hp_calls++;
   g->own_edges += n;
-  // data lag kLag: the data half of exchange b - kLag, issued first, so buffer set k is
-  // released (events recorded) before this exchange reuses it. A shorter fixed lag issues it
-  // at the end of the call (below); the eager schedule after this call's own folds.
-  if (!g->eager && g->data_lag == kLag && b >= (uint64_t)kLag)
+  // data lag kLag: the data half of exchange b - kLag (its counts landed long ago),
+  // issued first, so buffer set k is released (events recorded) before this exchange
+  // reuses it. A shorter lag issues it at the end of the call (below).
+  if (g->data_lag == kLag && b >= (uint64_t)kLag)
     if (int rc = finish_data(g, b - kLag)) return rc;
   HostTimer ht(g->hostprof ? &g->hp[0] : nullptr);
   // The own fold records into delta set d. The summary stream only waits for the
@@ -643,12 +640,6 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
         evs[nev++] = g->folded[d][i];
       }
   }
-  // Eager schedule: the own folds of this exchange are queued before the host may block, for
-  // the data half of exchange b - kLag whose buffer set k the stage below reuses -- the lanes
-  // keep three exchanges of folds while the host waits for those counts.
-  if (g->eager && b >= (uint64_t)kLag)
-    for (uint64_t e = g->done; e <= b - kLag; ++e)
-      if (int rc = finish_data(g, e)) return rc;
   ht.lap(g->hostprof ? &g->hp[1] : nullptr);
   // communication stream C: stage set d behind the fold, once the remote fold of
   // exchange b - kLag has read cnt_recv[k] (it ran behind the data collective that
@@ -675,18 +666,8 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   // every rank learns the others' hooks kLag - L exchanges sooner, so fewer of its own
   // hooks duplicate theirs. (The stage above reused buffer set k
   // after the data half of exchange b - kLag, issued in call b - kLag + L < b.)
-  if (!g->eager && g->data_lag < kLag && b >= (uint64_t)g->data_lag)
+  if (g->data_lag < kLag && b >= (uint64_t)g->data_lag)
     if (int rc = finish_data(g, b - g->data_lag)) return rc;
-  // Eager schedule (round 5): every earlier exchange whose gathered counts have already landed
-  // gets its data half now, oldest first, without waiting for any. A fixed lag of 2 made the host
-  // wait in every call for the counts of exchange b - 2, which land some 250 us after its folds
-  // (stage, count collective and headers queue behind them on the count stream): by then the
-  // lanes had run dry, 2.3 ms of idle GPU per one-rank step (profiles/r05_exch_trace.txt). Now
-  // the host blocks only for buffer reuse, kLag exchanges back (above).
-  if (g->eager)
-    while (g->done < b && __atomic_load_n(&g->hdr((int)(g->done % kLag))[g->nranks], __ATOMIC_ACQUIRE) ==
-                              (long long)g->done)
-      if (int rc = finish_data(g, g->done)) return rc;
   return GS_OK;
 }
 
