@@ -767,6 +767,17 @@ def rccl_setting():
     return {"NCCL_MAX_NCHANNELS": int(v) if v else None}
 
 
+def native_stdout_to_stderr():
+    """RCCL prints a version banner ("RCCL version : ...", "Librccl path : ...") on the process's
+    stdout when a communicator is created, ahead of the one JSON line the contract allows on
+    stdout. Native code gets fd 1 pointed at stderr; this script's own prints keep the real
+    stdout."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    sys.stdout = os.fdopen(real, "w", buffering=1)
+
+
 def main():
     args = parse()
     if args.rccl_max_channels > 0:
@@ -777,6 +788,7 @@ def main():
     rc = self_launch(args)
     if rc is not None:  # this process only launched the ranks
         sys.exit(rc)
+    native_stdout_to_stderr()  # in the rank processes (self_launch's children inherit the real stdout)
     if args.launch_check:
         return launch_check(args)
     world, rank, local = check_world(args)

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -288,7 +289,7 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
                                            int64_t* __restrict__ dst, uint64_t cap,
                                            unsigned long long* __restrict__ bad, bool aligned, uint64_t tile,
                                            unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat,
-                                           unsigned long long lb_timeout, unsigned long long selfcount);
+                                           unsigned long long lb_timeout);
 
 // Single pass (GS_PARSE_FUSED, default): no k_count_lines pass and no scan. Every block
 // counts its tile's '\n' from the masks it builds anyway and finds the count before its
@@ -312,6 +313,12 @@ constexpr unsigned long long kStP = 1ull << 63, kStA = 1ull << 62, kStVal = (1ul
 // (1 << kStWaveShift) | (its count) to the tile's status word, and the aggregate is
 // complete once all four waves have added. (The look-back's waits are for predecessors'
 // aggregates; this moves them a staging-and-scan earlier.)
+#ifndef GS_LB_WIN2
+#define GS_LB_WIN2 0
+#endif
+#ifndef GS_PARSE_DYN
+#define GS_PARSE_DYN 0
+#endif
 #ifndef GS_PARSE_EARLY
 #define GS_PARSE_EARLY 1  // 0: aggregates published after the scan (experiment switch)
 #endif
@@ -342,32 +349,35 @@ __device__ __forceinline__ uint32_t nl_count16(const uint4& v) {
 // per round); publishes the tile's inclusive count. agg = the tile's own '\n' count.
 // Between unsuccessful rounds the wave backs off (s_sleep 8 -> 64): every waiting wave
 // re-reading 64 status words at once slowed the other blocks' staging loads.
-// Bounded self-count (selfcount ticks, GS_PARSE_SELFCOUNT_US): once a round has waited that
-// long, the wave counts the '\n' of every predecessor in its window that has published nothing
-// yet (the whole wave reads that 16 KiB tile: 16 loads of 16 B per lane) and uses the count as
-// the tile's aggregate -- what the tile itself publishes from the same bytes. The waits are for
-// tiles of an XCD that has fallen behind in dispatch; counting one costs
-// a tile read instead of waiting for that XCD. Aligned texts only.
-#ifndef GS_LB_FALLBACK16
-#define GS_LB_FALLBACK16 1  // 0: the fallback counts one byte per lane and load (experiment switch)
-#endif
-#ifndef GS_LB_SELFCOUNT
-#define GS_LB_SELFCOUNT 1  // 0: no self-count code in the look-back (experiment switch)
-#endif
-__device__ __forceinline__ unsigned long long self_count_tile(const uint8_t* __restrict__ text, int64_t tp) {
-  const uint4* v = reinterpret_cast<const uint4*>(text + (uint64_t)tp * kTile);
+// The look-back's fallback: every '\n' before the tile, counted by the waiting wave with 4 B per
+// lane and load (one byte per lane and load made a late tile of a large text millions
+// of loads). 4 B, not 16: the 16-B loop took the parse kernel from 58 to 69 VGPRs (73 out of
+// line, the call's ABI), 8 -> 7 waves per SIMD, and the whole parse 3-7 % slower
+// (profiles/r05_ingest_ab.txt); one word per lane keeps it at 64 VGPRs, 8 waves.
+__device__ __forceinline__ unsigned long long count_nl_before(const uint8_t* __restrict__ text, uint64_t end) {
+  const uint32_t lane = threadIdx.x & 63;
   unsigned long long c = 0;
-#pragma unroll 4
-  for (uint32_t q = threadIdx.x & 63; q < kTile / 16; q += 64) c += nl_count16(v[q]);
+  const uint64_t head = min(end, (uint64_t)((4u - ((uintptr_t)text & 3u)) & 3u));
+  for (uint64_t q = lane; q < head; q += 64) c += text[q] == '\n';
+  const uint32_t* v4 = reinterpret_cast<const uint32_t*>(text + head);
+  const uint64_t n4 = (end - head) / 4;
+  for (uint64_t q = lane; q < n4; q += 64) {
+    const uint32_t x = v4[q] ^ 0x0A0A0A0Au;  // as nl_count16, on one word
+    c += __popc(~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu));
+  }
+  for (uint64_t q = head + 4 * n4 + lane; q < end; q += 64) c += text[q] == '\n';
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
   return c;
 }
 
+#ifdef GS_LB_STATS  // experiment: look-back statistics (blocks, -, sleeps, windows, ticks waited, ticks before)
+__device__ unsigned long long g_lbs[8];
+#define GS_LBS(i, v) atomicAdd(&g_lbs[i], (unsigned long long)(v))
+#endif
 __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restrict__ text, unsigned long long* status,
                                                         unsigned long long* pstat, uint64_t tile, unsigned long long agg,
-                                                        bool published, unsigned long long lb_timeout,
-                                                        unsigned long long selfcount, bool aligned) {
+                                                        bool published, unsigned long long lb_timeout) {
   const int lane = threadIdx.x & 63;
   if (tile == 0) {
     if (lane == 0) __hip_atomic_store(pstat, kStP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -381,6 +391,35 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
   int64_t base = (int64_t)tile - 1;
   const unsigned long long t_start = wall_clock64();
   int backoff = 0;
+  unsigned wins = 0;
+#if GS_LB_WIN2
+  for (;;) {  // experiment: 128 predecessors per round (two words per lane and array)
+    const int64_t ta = base - lane, tb = base - 64 - lane;
+    const unsigned long long wpa =
+        ta >= 0 ? __hip_atomic_load(pstat + ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kStP;
+    const unsigned long long waa =
+        ta >= 0 ? __hip_atomic_load(status + ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const unsigned long long wpb =
+        tb >= 0 ? __hip_atomic_load(pstat + tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kStP;
+    const unsigned long long wab =
+        tb >= 0 ? __hip_atomic_load(status + tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const bool pa = (wpa & kStP) != 0, pb = (wpb & kStP) != 0;
+    const unsigned long long pma = __ballot(pa), pmb = __ballot(pb);
+    const unsigned long long ama = __ballot(pa || st_has_agg(waa)), amb = __ballot(pb || st_has_agg(wab));
+    const int j = pma ? __ffsll((long long)pma) - 1 : (pmb ? 64 + __ffsll((long long)pmb) - 1 : 128);
+    const unsigned long long needa = j >= 64 ? ~0ull : ((2ull << j) - 1ull);
+    const unsigned long long needb = j < 64 ? 0ull : (j >= 128 ? ~0ull : ((2ull << (j - 64)) - 1ull));
+    if ((ama & needa) == needa && (amb & needb) == needb) {
+      unsigned long long v = lane <= j ? (pa ? (wpa & kStVal) : st_agg(waa)) : 0ull;
+      if (j >= 64 && lane + 64 <= j) v += pb ? (wpb & kStVal) : st_agg(wab);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+      excl += v;
+      if (j < 128) break;
+      base -= 128;
+      continue;
+    }
+#else
   for (;;) {
     const int64_t ti = base - lane;  // lane 0: the nearest predecessor
     const unsigned long long wp =
@@ -388,49 +427,23 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
     const unsigned long long wa =
         ti >= 0 ? __hip_atomic_load(status + ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     const bool has_p = (wp & kStP) != 0;
-    unsigned long long w = has_p ? wp : wa;
-    const unsigned long long pm = __ballot(has_p);
-    unsigned long long am = __ballot(has_p || st_has_agg(wa));
+    const unsigned long long w = has_p ? wp : wa;
+    const unsigned long long pm = __ballot(has_p), am = __ballot(has_p || st_has_agg(wa));
     const int j = pm ? __ffsll((long long)pm) - 1 : 64;  // nearest final prefix in this window
     const unsigned long long need = j >= 64 ? ~0ull : ((2ull << j) - 1ull);  // lanes 0..j
-    if (GS_LB_SELFCOUNT && (am & need) != need && aligned && wall_clock64() - t_start > selfcount) {
-      // bounded self-count of the silent predecessors (wave-uniform loop over their lanes)
-      unsigned long long miss = need & ~am & __ballot(ti >= 0);
-      while (miss) {
-        const int l = __ffsll((long long)miss) - 1;
-        miss &= miss - 1;
-        const unsigned long long c = self_count_tile(text, base - l);
-        if (lane == l) w = kStA | c;
-      }
-      am = need;
-    }
     if ((am & need) == need) {
-      unsigned long long v = lane <= j ? ((w & kStP) ? (w & kStVal) : st_agg(w)) : 0ull;
+      unsigned long long v = lane <= j ? (has_p ? (w & kStVal) : st_agg(w)) : 0ull;
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
       excl += v;
       if (j < 64) break;
       base -= 64;  // the whole window was own counts: continue further back
+      ++wins;
       continue;
     }
-    if (wall_clock64() - t_start > lb_timeout) {  // ~50 ms (100 MHz clock) by default: count it directly
-      // every '\n' before the tile, 16 bytes per lane and load (one byte per lane
-      // and load made a late tile of a large text millions of dependent loads)
-      unsigned long long c = 0;
-      const uint64_t end = tile * kTile;
-#if GS_LB_FALLBACK16
-      const uint64_t head = min(end, (uint64_t)((16u - ((uintptr_t)text & 15u)) & 15u));
-      for (uint64_t q = (uint64_t)lane; q < head; q += 64) c += text[q] == '\n';
-      const uint4* v16 = reinterpret_cast<const uint4*>(text + head);
-      const uint64_t n16 = (end - head) / 16;
-      for (uint64_t q = (uint64_t)lane; q < n16; q += 64) c += nl_count16(v16[q]);
-      for (uint64_t q = head + 16 * n16 + (uint64_t)lane; q < end; q += 64) c += text[q] == '\n';
-#else
-      for (uint64_t q = (uint64_t)lane; q < end; q += 64) c += text[q] == '\n';
 #endif
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
-      excl = c;
+    if (wall_clock64() - t_start > lb_timeout) {  // ~50 ms (100 MHz clock) by default: count it directly
+      excl = count_nl_before(text, tile * kTile);
       break;
     }
     if (backoff < 3) {
@@ -441,6 +454,16 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
     ++backoff;
   }
   if (lane == 0) __hip_atomic_store(pstat + tile, kStP | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef GS_LB_STATS
+  if (lane == 0) {
+    GS_LBS(0, 1);
+    GS_LBS(2, backoff);
+    GS_LBS(3, wins);
+    GS_LBS(4, wall_clock64() - t_start);
+    GS_LBS(6, backoff > 0 ? 1 : 0);
+  }
+#endif
+  (void)wins;
   return excl;
 }
 
@@ -448,9 +471,16 @@ __global__ __launch_bounds__(256) void k_parse_fused(const uint8_t* __restrict__
                                                      int64_t* __restrict__ src, int64_t* __restrict__ dst, uint64_t cap,
                                                      unsigned long long* __restrict__ bad, bool aligned,
                                                      unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat,
-                                                     unsigned long long lb_timeout, unsigned long long selfcount) {
-  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, blockIdx.x, status, pstat, lb_timeout,
-                   selfcount);
+                                                     unsigned long long lb_timeout, unsigned* __restrict__ tctr) {
+#if GS_PARSE_DYN  // experiment: tiles numbered in the order blocks start (a predecessor is always running)
+  __shared__ unsigned tile_sh;
+  if (threadIdx.x == 0) tile_sh = atomicAdd(tctr, 1u);
+  __syncthreads();
+  const uint64_t tile = tile_sh;
+#else
+  const uint64_t tile = blockIdx.x;
+#endif
+  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, tile, status, pstat, lb_timeout);
 }
 
 // One tile per block (44 VGPRs, 8 blocks per CU).
@@ -458,8 +488,7 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
                                                const uint64_t* __restrict__ tile_pre, int64_t* __restrict__ src,
                                                int64_t* __restrict__ dst, uint64_t cap,
                                                unsigned long long* __restrict__ bad, bool aligned, uint64_t tile0) {
-  parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile0 + blockIdx.x, nullptr, nullptr, 0ull,
-                    0ull);
+  parse_tile<false>(text, len, sep, tile_pre, src, dst, cap, bad, aligned, tile0 + blockIdx.x, nullptr, nullptr, 0ull);
 }
 
 template <bool FUSED>
@@ -468,7 +497,7 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
                                            int64_t* __restrict__ dst, uint64_t cap,
                                            unsigned long long* __restrict__ bad, bool aligned, uint64_t tile,
                                            unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat,
-                                           unsigned long long lb_timeout, unsigned long long selfcount) {
+                                           unsigned long long lb_timeout) {
   constexpr uint32_t kSeg = kTile / 256;  // bytes per thread in the line-start scan
   constexpr uint32_t kExtra = 2;          // '\n' masks past the tile: lines that cross its end
   constexpr uint32_t kSlots = (kTile + kOver + 4095) / 4096;
@@ -480,6 +509,9 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
   __shared__ uint32_t wnl[4];
   const uint64_t t0 = tile * kTile;
   const uint64_t staged_end = min(len, t0 + kTile + kOver);
+#ifdef GS_LB_STATS
+  const unsigned long long blk_start = wall_clock64();
+#endif
   // stage [t0, staged_end) at lds[kLds0..] with 16-B stores; lds[kLds0 - 1] = byte t0 - 1.
   // Every thread's global loads (five 16-B slots, 4 KiB apart) are issued before any is
   // waited for; named registers, not an array (an indexed array of them went to scratch).
@@ -587,6 +619,11 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
       }
     }
 #endif
+#ifdef GS_PARSE_FLOOR  // experiment: no field parse (the kernel's floor without the SWAR work)
+    a = so;
+    d = e;
+    return e >= 0;
+#endif
     uint64_t q = t0 + (uint64_t)so;
     a = 0;
     d = 0;
@@ -641,10 +678,18 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
       k = 2;
     }
     __shared__ unsigned long long pre_sh;
+#ifdef GS_PARSE_NOLB  // experiment: no look-back (wrong line numbers; the kernel's cost without it)
+    if (threadIdx.x == 0) pre_sh = 0;
+    if (false) {
+#else
     if (wid == 0) {
+#endif
+#ifdef GS_LB_STATS
+      if (lane == 0) GS_LBS(5, wall_clock64() - blk_start);
+#endif
       const unsigned long long e =
           look_back(text, status, pstat, tile, (unsigned long long)wnl[0] + wnl[1] + wnl[2] + wnl[3], early,
-                    lb_timeout, selfcount, aligned);
+                    lb_timeout);
       if (lane == 0) pre_sh = e;
     }
     __syncthreads();
@@ -708,13 +753,22 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
     // counts the '\n' before its tile itself (default ~50 ms; 0: at once)
     const char* lbe = getenv("GS_PARSE_LB_TIMEOUT_US");
     const unsigned long long lb_timeout = lbe ? 100ull * strtoull(lbe, nullptr, 10) : 5000000ull;
-    // GS_PARSE_SELFCOUNT_US (experiment knob): the bounded self-count of silent predecessors after
-    // that many microseconds of waiting (unset: never)
-    const char* sce = getenv("GS_PARSE_SELFCOUNT_US");
-    const unsigned long long selfcount = sce ? 100ull * strtoull(sce, nullptr, 10) : ~0ull;
     hipLaunchKernelGGL(k_parse_fused, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, src, dst,
-                       (uint64_t)cap, s.bad, aligned, agg, pre, lb_timeout, selfcount);
+                       (uint64_t)cap, s.bad, aligned, agg, pre, lb_timeout,
+                       reinterpret_cast<unsigned*>(agg + s.tiles_cap - 1));  // (zeroed by the fill, never a tile's word)
     if (kev1 && hipEventRecord(kev1, st) != hipSuccess) return -1;
+#ifdef GS_LB_STATS
+    {
+      unsigned long long v[8] = {};
+      if (hipStreamSynchronize(st) == hipSuccess && hipMemcpyFromSymbol(v, HIP_SYMBOL(g_lbs), sizeof v) == hipSuccess) {
+        const double b = (double)(v[0] ? v[0] : 1);
+        fprintf(stderr, "LBSTATS tiles %llu sleeps/blk %.2f windows/blk %.3f wait_us/blk %.2f before_us/blk %.2f "
+                "blocks_slept %.3f\n", v[0], v[2] / b, v[3] / b, v[4] / b / 100.0, v[5] / b / 100.0, v[6] / b);
+        unsigned long long z[8] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lbs), z, sizeof z);
+      }
+    }
+#endif
     hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
                        s.bad, s.res, host_res, seq, pre);
     return hipGetLastError() == hipSuccess ? 0 : -1;

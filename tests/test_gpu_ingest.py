@@ -270,18 +270,3 @@ def test_parse_lookback_fallback_counts_directly(gs, oracle_mod, offset, monkeyp
         assert (n, b) == (en, eb), (nlines, offset, n, b, en, eb)
         assert np.array_equal(s, es) and np.array_equal(d, ed)
 
-
-@pytest.mark.parametrize("offset", [0, 5])
-def test_parse_bounded_self_count(gs, oracle_mod, offset, monkeypatch):
-    """The look-back's bounded self-count (GS_PARSE_SELFCOUNT_US): a wave whose predecessors
-    have published nothing counts their '\\n' itself and uses the counts as their aggregates.
-    At 0 us every waiting round self-counts its silent predecessors; the parse stays the
-    oracle's (aligned texts; an unaligned one never self-counts)."""
-    rng = np.random.default_rng(23 + offset)
-    monkeypatch.setenv("GS_PARSE_SELFCOUNT_US", "0")
-    for nlines in (5000, 200000):
-        text = _random_text(rng, nlines, 0)
-        es, ed, en, eb = oracle_mod.parse_edges(text, 0)
-        s, d, n, b = _gpu_parse(gs, text, 0, offset)
-        assert (n, b) == (en, eb), (nlines, offset, n, b, en, eb)
-        assert np.array_equal(s, es) and np.array_equal(d, ed)
