@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "gs_ingest.h"
 #include "gs_ingest.hpp"
@@ -313,6 +314,9 @@ constexpr unsigned long long kStP = 1ull << 63, kStA = 1ull << 62, kStVal = (1ul
 // (1 << kStWaveShift) | (its count) to the tile's status word, and the aggregate is
 // complete once all four waves have added. (The look-back's waits are for predecessors'
 // aggregates; this moves them a staging-and-scan earlier.)
+#ifndef GS_PARSE_REGMASK
+#define GS_PARSE_REGMASK 1  // '\n' masks from the staging registers (0: from LDS after staging; experiment switch)
+#endif
 #ifndef GS_LB_WIN2
 #define GS_LB_WIN2 0
 #endif
@@ -345,6 +349,35 @@ __device__ __forceinline__ uint32_t nl_count16(const uint4& v) {
   return c;
 }
 
+// '\n' mask of 16 bytes held in registers (bit j: byte j), exact: the zero-byte test of
+// w ^ 0x0A0A0A0A leaves bit 8 b + 7 of a word for a '\n' in its byte b, and one multiply by
+// 2^0 + 2^7 + 2^14 + 2^21 gathers the four bits into bits 21..24 (no two partial products
+// share a bit, so nothing carries)
+__device__ __forceinline__ uint32_t nl_mask16(const uint4& v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = w[k] ^ 0x0A0A0A0Au;
+    const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+    m |= ((((t >> 7) * 0x00204081u) >> 21) & 0xFu) << (4 * k);
+  }
+  return m;
+}
+
+// Inclusive prefix sum over the 64 lanes of a wave with DPP (no LDS round trips: __shfl_up is
+// a ds_bpermute per step): row_shr 1, 2, 4, 8 within each row of 16 lanes, then row_bcast 15
+// and 31 carry the rows' totals upward
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 // Wave 0 of tile `tile`: '\n' before the tile (decoupled look-back over 64 predecessors
 // per round); publishes the tile's inclusive count. agg = the tile's own '\n' count.
 // Between unsuccessful rounds the wave backs off (s_sleep 8 -> 64): every waiting wave
@@ -371,9 +404,9 @@ __device__ __forceinline__ unsigned long long count_nl_before(const uint8_t* __r
   return c;
 }
 
-#ifdef GS_LB_STATS  // experiment: look-back statistics (blocks, -, sleeps, windows, ticks waited, ticks before)
-__device__ unsigned long long g_lbs[8];
-#define GS_LBS(i, v) atomicAdd(&g_lbs[i], (unsigned long long)(v))
+#ifdef GS_LB_STATS  // experiment: per-tile look-back statistics {ticks before, ticks waited, sleeps, windows}
+constexpr uint32_t kLbsTiles = 65536;
+__device__ uint32_t g_lbt[kLbsTiles][8];  // + [4] staged, [5] masks, [6] scanned, [7] loads landed (wave 0)
 #endif
 __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restrict__ text, unsigned long long* status,
                                                         unsigned long long* pstat, uint64_t tile, unsigned long long agg,
@@ -455,12 +488,10 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
   }
   if (lane == 0) __hip_atomic_store(pstat + tile, kStP | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef GS_LB_STATS
-  if (lane == 0) {
-    GS_LBS(0, 1);
-    GS_LBS(2, backoff);
-    GS_LBS(3, wins);
-    GS_LBS(4, wall_clock64() - t_start);
-    GS_LBS(6, backoff > 0 ? 1 : 0);
+  if (lane == 0 && tile < kLbsTiles) {
+    g_lbt[tile][1] = (uint32_t)(wall_clock64() - t_start);
+    g_lbt[tile][2] = (uint32_t)backoff;
+    g_lbt[tile][3] = wins;
   }
 #endif
   (void)wins;
@@ -529,13 +560,32 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
   // one-pass: a tile wholly inside the (aligned) text publishes its '\n' count from the
   // staged registers (slots 0-3 are exactly its 16 KiB), wave by wave, right away
   const bool early = GS_PARSE_EARLY && FUSED && tile != 0 && aligned && t0 + kTile <= len;
+  // a tile whose staged bytes all lie inside the (aligned) text: every thread's '\n' masks
+  // of its five slots straight from the registers (no LDS read-back and one barrier less);
+  // the count the early aggregate publishes is theirs
+  const bool regmask = GS_PARSE_REGMASK && aligned && staged_end == t0 + kTile + kOver;
+  uint16_t* m16 = reinterpret_cast<uint16_t*>(nlm);
+  uint32_t mk0 = 0, mk1 = 0, mk2 = 0, mk3 = 0;
+  if (regmask) {
+    mk0 = nl_mask16(v0);
+    mk1 = nl_mask16(v1);
+    mk2 = nl_mask16(v2);
+    mk3 = nl_mask16(v3);
+    m16[threadIdx.x] = (uint16_t)mk0;
+    m16[256 + threadIdx.x] = (uint16_t)mk1;
+    m16[512 + threadIdx.x] = (uint16_t)mk2;
+    m16[768 + threadIdx.x] = (uint16_t)mk3;
+    if (threadIdx.x < 4 * kExtra) m16[1024 + threadIdx.x] = (uint16_t)nl_mask16(v4);
+  }
   if (early) {
-    uint32_t c = nl_count16(v0) + nl_count16(v1) + nl_count16(v2) + nl_count16(v3);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((threadIdx.x & 63u) == 0)
+    uint32_t c = regmask ? __popc(mk0) + __popc(mk1) + __popc(mk2) + __popc(mk3)
+                         : nl_count16(v0) + nl_count16(v1) + nl_count16(v2) + nl_count16(v3);
+    c = __builtin_amdgcn_readlane(wave_incl_sum(c), 63);
+    if ((threadIdx.x & 63u) == 0) {
       __hip_atomic_fetch_add(status + tile, (1ull << kStWaveShift) | (unsigned long long)c, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+      wnl[threadIdx.x >> 6] = c;  // (the look-back's aggregate: this wave's quarter of the tile)
+    }
   }
   auto put = [&](bool f, uint32_t i, const uint4& v) {
     if (f) {
@@ -544,12 +594,21 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
       for (uint64_t q = t0 + i; q < t0 + i + 16 && q < staged_end; ++q) lds[kLds0 + (q - t0)] = text[q];
     }
   };
+#ifdef GS_LB_STATS
+  if (threadIdx.x == 0 && tile < kLbsTiles) {
+    const uint32_t x = v0.x ^ v1.x ^ v2.x ^ v3.x ^ v4.x;  // the loads have landed (for this wave)
+    g_lbt[tile][7] = (uint32_t)(wall_clock64() - blk_start) | (x & 0u);
+  }
+#endif
   put(f0, i0, v0);
   put(f1, i0 + 4096u, v1);
   put(f2, i0 + 8192u, v2);
   put(f3, i0 + 12288u, v3);
   put(f4, i0 + 16384u, v4);
   __syncthreads();
+#ifdef GS_LB_STATS
+  if (threadIdx.x == 0 && tile < kLbsTiles) g_lbt[tile][4] = (uint32_t)(wall_clock64() - blk_start);
+#endif
   // (1) each thread's 64-byte segment: its '\n' mask (to LDS: a line's end may lie in a
   //     later segment) and its line starts (byte p - 1 is '\n', or p == 0); a block
   //     scan of the start counts numbers the lines.
@@ -559,11 +618,15 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
   const uint64_t vend = staged_end == len ? len - t0 : ~0ull;  // the text ends inside the staged bytes
   // 16-bit chunk masks written as the u16 quarters of nlm (little endian: nlm[q] is
   // then segment q's 64-bit mask); 4 chunks per thread + the kExtra segments' chunks
-  uint16_t* m16 = reinterpret_cast<uint16_t*>(nlm);
+  if (!regmask) {  // (block-uniform) the text's last tiles, unaligned texts: from LDS, with the end rule
 #pragma unroll
-  for (uint32_t r = 0; r < 4; ++r) m16[r * 256 + threadIdx.x] = (uint16_t)chunk_nl_mask(L, r * 256 + threadIdx.x, vend);
-  if (threadIdx.x < 4 * kExtra) m16[1024 + threadIdx.x] = (uint16_t)chunk_nl_mask(L, 1024 + threadIdx.x, vend);
-  __syncthreads();
+    for (uint32_t r = 0; r < 4; ++r) m16[r * 256 + threadIdx.x] = (uint16_t)chunk_nl_mask(L, r * 256 + threadIdx.x, vend);
+    if (threadIdx.x < 4 * kExtra) m16[1024 + threadIdx.x] = (uint16_t)chunk_nl_mask(L, 1024 + threadIdx.x, vend);
+    __syncthreads();
+  }
+#ifdef GS_LB_STATS
+  if (threadIdx.x == 0 && tile < kLbsTiles) g_lbt[tile][5] = (uint32_t)(wall_clock64() - blk_start);
+#endif
   const uint64_t nl = nlm[threadIdx.x];
   // bit j: a line starts at seg + j (byte seg + j - 1 is '\n': the previous segment's top bit)
   const bool prev_nl = threadIdx.x == 0 ? L[-1] == '\n' : (nlm[threadIdx.x - 1] >> 63) != 0;
@@ -572,20 +635,17 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
   if (valid < 64) mine &= (1ull << valid) - 1ull;
   const uint32_t c = __popcll(mine);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t x = c;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
+  const uint32_t x = wave_incl_sum(c);
   if (lane == 63) wsum[wid] = x;
-  if (FUSED) {  // the tile's own '\n' (its bytes only): the look-back's aggregate
-    uint32_t cn = __popcll(valid >= 64 ? nl : (nl & ((1ull << valid) - 1ull)));
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) cn += __shfl_xor(cn, o, 64);
-    if (lane == 0) wnl[wid] = cn;
+  if (FUSED && !early) {  // the tile's own '\n' (its bytes only): the look-back's aggregate (early: counted above)
+    const uint32_t cn = __popcll(valid >= 64 ? nl : (nl & ((1ull << valid) - 1ull)));
+    const uint32_t tot = __builtin_amdgcn_readlane(wave_incl_sum(cn), 63);
+    if (lane == 0) wnl[wid] = tot;
   }
   __syncthreads();
+#ifdef GS_LB_STATS
+  if (threadIdx.x == 0 && tile < kLbsTiles) g_lbt[tile][6] = (uint32_t)(wall_clock64() - blk_start);
+#endif
   uint32_t wbase = 0;
   for (int q = 0; q < 4; ++q)
     if (q < wid) wbase += wsum[q];
@@ -685,7 +745,7 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
     if (wid == 0) {
 #endif
 #ifdef GS_LB_STATS
-      if (lane == 0) GS_LBS(5, wall_clock64() - blk_start);
+      if (lane == 0 && tile < kLbsTiles) g_lbt[tile][0] = (uint32_t)(wall_clock64() - blk_start);
 #endif
       const unsigned long long e =
           look_back(text, status, pstat, tile, (unsigned long long)wnl[0] + wnl[1] + wnl[2] + wnl[3], early,
@@ -731,6 +791,37 @@ __global__ void k_parse_result(const uint64_t* tile_pre, const uint64_t* tile_cn
   }
 }
 
+// The one-pass parse's result (as k_parse_result, from the last tile's prefix word) and the
+// reset of the status words it used, for the next parse: the aggregate and prefix words of
+// its tiles and the ticket word. One launch instead of a fill before the parse and a result
+// kernel after it. Block 0 reads the last prefix before it clears it; nothing else reads
+// the words once k_parse_fused has finished (stream order).
+__global__ __launch_bounds__(256) void k_parse_finish(unsigned long long* agg, unsigned long long* pre,
+                                                      uint64_t tiles, uint64_t tiles_cap, const uint8_t* text,
+                                                      uint64_t len, unsigned long long* bad, uint64_t* res,
+                                                      unsigned long long* host, unsigned long long seq) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint64_t nl = pre[tiles - 1] & kStVal;
+    const uint64_t lines = nl + (text[len - 1] != '\n' ? 1u : 0u);
+    const uint64_t b = *bad;
+    *bad = ~0ull;
+    res[0] = lines;
+    res[1] = b;
+    pre[tiles - 1] = 0;
+    agg[tiles_cap - 1] = 0;
+    if (host) {
+      __hip_atomic_store(host + 1, (unsigned long long)lines, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(host + 2, (unsigned long long)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(host, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tiles; i += stride) {
+    agg[i] = 0;
+    if (i + 1 < tiles) pre[i] = 0;
+  }
+}
+
 int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, int64_t* src, int64_t* dst, size_t cap,
                        ParseScratch& s, unsigned long long* host_res, unsigned long long seq, bool fused,
                        hipEvent_t kev0, hipEvent_t kev1) {
@@ -740,10 +831,13 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
   if (tiles > s.tiles_cap) return -1;
   const bool aligned = ((uintptr_t)text & 15u) == 0;
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
-  if (fused) {  // aggregate words (s.tile_cnt) and prefix words (s.tile_pre) zeroed, then one pass
-    // one fill: the aggregate words and the prefix words are adjacent (tile_pre = tile_cnt
-    // + tiles_cap); `bad` is reset by the previous parse's k_parse_result
-    if (hipMemsetAsync(s.tile_cnt, 0, (s.tiles_cap + tiles) * 8, st) != hipSuccess) return -1;
+  const bool st_zero = s.st_zero;
+  s.st_zero = false;  // until this call has queued a k_parse_finish
+  if (fused) {  // aggregate words (s.tile_cnt) and prefix words (s.tile_pre) zero, then one pass
+    // the previous one-pass parse's k_parse_finish left them zero; else one fill (the
+    // aggregate words and the prefix words are adjacent: tile_pre = tile_cnt + tiles_cap);
+    // `bad` is reset by the previous parse's k_parse_result / k_parse_finish
+    if (!st_zero && hipMemsetAsync(s.tile_cnt, 0, (s.tiles_cap + s.tiles_cap) * 8, st) != hipSuccess) return -1;
     if (!s.bad_ready && hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess) return -1;
     s.bad_ready = true;
     unsigned long long* agg = reinterpret_cast<unsigned long long*>(s.tile_cnt);
@@ -758,20 +852,37 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
                        reinterpret_cast<unsigned*>(agg + s.tiles_cap - 1));  // (zeroed by the fill, never a tile's word)
     if (kev1 && hipEventRecord(kev1, st) != hipSuccess) return -1;
 #ifdef GS_LB_STATS
-    {
-      unsigned long long v[8] = {};
-      if (hipStreamSynchronize(st) == hipSuccess && hipMemcpyFromSymbol(v, HIP_SYMBOL(g_lbs), sizeof v) == hipSuccess) {
-        const double b = (double)(v[0] ? v[0] : 1);
-        fprintf(stderr, "LBSTATS tiles %llu sleeps/blk %.2f windows/blk %.3f wait_us/blk %.2f before_us/blk %.2f "
-                "blocks_slept %.3f\n", v[0], v[2] / b, v[3] / b, v[4] / b / 100.0, v[5] / b / 100.0, v[6] / b);
-        unsigned long long z[8] = {};
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lbs), z, sizeof z);
+    if (tiles > 4096 && tiles <= kLbsTiles) {  // the large parses only: per-tile figures, summarised
+      static uint32_t v[kLbsTiles][8];
+      if (hipStreamSynchronize(st) == hipSuccess &&
+          hipMemcpyFromSymbol(v, HIP_SYMBOL(g_lbt), tiles * 32) == hipSuccess) {
+        double sum[8] = {};
+        uint32_t slept = 0;
+        std::vector<uint32_t> w(tiles), b(tiles);
+        for (uint64_t q = 0; q < tiles; ++q) {
+          for (int c = 0; c < 8; ++c) sum[c] += v[q][c];
+          slept += v[q][2] > 0;
+          b[q] = v[q][0];
+          w[q] = v[q][1];
+        }
+        std::sort(w.begin(), w.end());
+        std::sort(b.begin(), b.end());
+        const double n = (double)tiles;
+        fprintf(stderr, "LBSTATS tiles %llu before_us avg %.2f p50 %.2f p90 %.2f | wait_us avg %.2f p50 %.2f p90 %.2f "
+                "p99 %.2f | sleeps/blk %.2f slept %.3f windows/blk %.3f\n", (unsigned long long)tiles,
+                sum[0] / n / 100, b[tiles / 2] / 100.0, b[tiles * 9 / 10] / 100.0, sum[1] / n / 100,
+                w[tiles / 2] / 100.0, w[tiles * 9 / 10] / 100.0, w[tiles * 99 / 100] / 100.0, sum[2] / n, slept / n,
+                sum[3] / n);
+        fprintf(stderr, "LBPHASES landed %.2f staged %.2f masks %.2f scanned %.2f parsed %.2f (us after block start)\n",
+                sum[7] / n / 100, sum[4] / n / 100, sum[5] / n / 100, sum[6] / n / 100, sum[0] / n / 100);
       }
     }
 #endif
-    hipLaunchKernelGGL(k_parse_result, dim3(1), dim3(64), 0, st, s.tile_pre, s.tile_cnt, tiles, t, (uint64_t)len,
-                       s.bad, s.res, host_res, seq, pre);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    hipLaunchKernelGGL(k_parse_finish, dim3((unsigned)std::min<uint64_t>(64, (tiles + 255) / 256)), dim3(256), 0, st,
+                       agg, pre, tiles, s.tiles_cap, t, (uint64_t)len, s.bad, s.res, host_res, seq);
+    if (hipGetLastError() != hipSuccess) return -1;
+    s.st_zero = true;
+    return 0;
   }
   hipLaunchKernelGGL(k_count_lines, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, s.tile_cnt, aligned,
                      (uint64_t)0);
@@ -820,6 +931,7 @@ int parse_scratch_init(ParseScratch& s, void* mem, size_t max_len) {
   s.cub_bytes = cub;
   s.tiles_cap = tiles;
   s.bad_ready = false;
+  s.st_zero = false;
   return 0;
 }
 

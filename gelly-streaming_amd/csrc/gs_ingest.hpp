@@ -15,6 +15,7 @@ struct ParseScratch {
   size_t cub_bytes = 0;
   uint64_t tiles_cap = 0;
   bool bad_ready = false;  // `bad` holds ~0 (k_parse_result resets it after every parse)
+  bool st_zero = false;    // the one-pass status words are zero (the last one-pass parse's k_parse_finish cleared them)
 };
 
 // Device bytes needed to parse up to max_len bytes of text.
