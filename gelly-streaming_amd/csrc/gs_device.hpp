@@ -152,8 +152,21 @@ struct Delta {
   uint32_t* lnv = nullptr;   // resident window server: the block's new vertices of the window (LDS)
 };
 
+// Home slot of an id. Ids that differ only in their low 3 bits share one 128-B line of 8
+// slots: the line from a Fibonacci hash of key >> 3, the slot within it from key & 7. Dense
+// id ranges (config 4's first-appearance ids, ids assigned in order) then fill whole lines,
+// and the table's working set is their 16 B per id instead of a line per id: config 4
+// 0.893-0.902 -> 0.774-0.802 ms/step; random 64-bit ids (configs 2, 3, 5) place as before
+// (profiles/r05_hash_line_ab.txt). GS_HASH_LINE=0: the plain Fibonacci hash of the id.
+#ifndef GS_HASH_LINE
+#define GS_HASH_LINE 1
+#endif
 __device__ __forceinline__ uint32_t hash_slot(int64_t key, int shift) {
+#if GS_HASH_LINE
+  return ((uint32_t)((((uint64_t)key >> 3) * 0x9E3779B97F4A7C15ull) >> (shift + 3)) << 3) | (uint32_t)(key & 7);
+#else
   return (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ull) >> shift);
+#endif
 }
 
 __device__ __forceinline__ void load_slot(const Slot* p, int64_t& key, uint32_t& link) {
