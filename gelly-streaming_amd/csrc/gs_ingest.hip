@@ -317,12 +317,6 @@ constexpr unsigned long long kStP = 1ull << 63, kStA = 1ull << 62, kStVal = (1ul
 #ifndef GS_PARSE_REGMASK
 #define GS_PARSE_REGMASK 1  // '\n' masks from the staging registers (0: from LDS after staging; experiment switch)
 #endif
-#ifndef GS_LB_WIN2
-#define GS_LB_WIN2 0
-#endif
-#ifndef GS_PARSE_DYN
-#define GS_PARSE_DYN 0
-#endif
 #ifndef GS_PARSE_EARLY
 #define GS_PARSE_EARLY 1  // 0: aggregates published after the scan (experiment switch)
 #endif
@@ -425,34 +419,6 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
   const unsigned long long t_start = wall_clock64();
   int backoff = 0;
   unsigned wins = 0;
-#if GS_LB_WIN2
-  for (;;) {  // experiment: 128 predecessors per round (two words per lane and array)
-    const int64_t ta = base - lane, tb = base - 64 - lane;
-    const unsigned long long wpa =
-        ta >= 0 ? __hip_atomic_load(pstat + ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kStP;
-    const unsigned long long waa =
-        ta >= 0 ? __hip_atomic_load(status + ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-    const unsigned long long wpb =
-        tb >= 0 ? __hip_atomic_load(pstat + tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kStP;
-    const unsigned long long wab =
-        tb >= 0 ? __hip_atomic_load(status + tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-    const bool pa = (wpa & kStP) != 0, pb = (wpb & kStP) != 0;
-    const unsigned long long pma = __ballot(pa), pmb = __ballot(pb);
-    const unsigned long long ama = __ballot(pa || st_has_agg(waa)), amb = __ballot(pb || st_has_agg(wab));
-    const int j = pma ? __ffsll((long long)pma) - 1 : (pmb ? 64 + __ffsll((long long)pmb) - 1 : 128);
-    const unsigned long long needa = j >= 64 ? ~0ull : ((2ull << j) - 1ull);
-    const unsigned long long needb = j < 64 ? 0ull : (j >= 128 ? ~0ull : ((2ull << (j - 64)) - 1ull));
-    if ((ama & needa) == needa && (amb & needb) == needb) {
-      unsigned long long v = lane <= j ? (pa ? (wpa & kStVal) : st_agg(waa)) : 0ull;
-      if (j >= 64 && lane + 64 <= j) v += pb ? (wpb & kStVal) : st_agg(wab);
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-      excl += v;
-      if (j < 128) break;
-      base -= 128;
-      continue;
-    }
-#else
   for (;;) {
     const int64_t ti = base - lane;  // lane 0: the nearest predecessor
     const unsigned long long wp =
@@ -474,7 +440,6 @@ __device__ __forceinline__ unsigned long long look_back(const uint8_t* __restric
       ++wins;
       continue;
     }
-#endif
     if (wall_clock64() - t_start > lb_timeout) {  // ~50 ms (100 MHz clock) by default: count it directly
       excl = count_nl_before(text, tile * kTile);
       break;
@@ -502,16 +467,8 @@ __global__ __launch_bounds__(256) void k_parse_fused(const uint8_t* __restrict__
                                                      int64_t* __restrict__ src, int64_t* __restrict__ dst, uint64_t cap,
                                                      unsigned long long* __restrict__ bad, bool aligned,
                                                      unsigned long long* __restrict__ status, unsigned long long* __restrict__ pstat,
-                                                     unsigned long long lb_timeout, unsigned* __restrict__ tctr) {
-#if GS_PARSE_DYN  // experiment: tiles numbered in the order blocks start (a predecessor is always running)
-  __shared__ unsigned tile_sh;
-  if (threadIdx.x == 0) tile_sh = atomicAdd(tctr, 1u);
-  __syncthreads();
-  const uint64_t tile = tile_sh;
-#else
-  const uint64_t tile = blockIdx.x;
-#endif
-  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, tile, status, pstat, lb_timeout);
+                                                     unsigned long long lb_timeout) {
+  parse_tile<true>(text, len, sep, nullptr, src, dst, cap, bad, aligned, blockIdx.x, status, pstat, lb_timeout);
 }
 
 // One tile per block (44 VGPRs, 8 blocks per CU).
@@ -793,7 +750,7 @@ __global__ void k_parse_result(const uint64_t* tile_pre, const uint64_t* tile_cn
 
 // The one-pass parse's result (as k_parse_result, from the last tile's prefix word) and the
 // reset of the status words it used, for the next parse: the aggregate and prefix words of
-// its tiles and the ticket word. One launch instead of a fill before the parse and a result
+// its tiles. One launch instead of a fill before the parse and a result
 // kernel after it. Block 0 reads the last prefix before it clears it; nothing else reads
 // the words once k_parse_fused has finished (stream order).
 __global__ __launch_bounds__(256) void k_parse_finish(unsigned long long* agg, unsigned long long* pre,
@@ -808,7 +765,6 @@ __global__ __launch_bounds__(256) void k_parse_finish(unsigned long long* agg, u
     res[0] = lines;
     res[1] = b;
     pre[tiles - 1] = 0;
-    agg[tiles_cap - 1] = 0;
     if (host) {
       __hip_atomic_store(host + 1, (unsigned long long)lines, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(host + 2, (unsigned long long)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -848,8 +804,7 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
     const char* lbe = getenv("GS_PARSE_LB_TIMEOUT_US");
     const unsigned long long lb_timeout = lbe ? 100ull * strtoull(lbe, nullptr, 10) : 5000000ull;
     hipLaunchKernelGGL(k_parse_fused, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, src, dst,
-                       (uint64_t)cap, s.bad, aligned, agg, pre, lb_timeout,
-                       reinterpret_cast<unsigned*>(agg + s.tiles_cap - 1));  // (zeroed by the fill, never a tile's word)
+                       (uint64_t)cap, s.bad, aligned, agg, pre, lb_timeout);
     if (kev1 && hipEventRecord(kev1, st) != hipSuccess) return -1;
 #ifdef GS_LB_STATS
     if (tiles > 4096 && tiles <= kLbsTiles) {  // the large parses only: per-tile figures, summarised
