@@ -270,3 +270,29 @@ def test_parse_lookback_fallback_counts_directly(gs, oracle_mod, offset, monkeyp
         assert (n, b) == (en, eb), (nlines, offset, n, b, en, eb)
         assert np.array_equal(s, es) and np.array_equal(d, ed)
 
+
+
+def test_parse_sequence_reuses_cleared_status_words(gs, oracle_mod):
+    """The one-pass parse leaves its tiles' status words zero for the next parse (k_parse_finish
+    clears them with the result), so parses after the first run without a fill. A sequence of
+    texts of different tile counts on one cached scratch -- large, small, large again, unaligned,
+    malformed, empty, large -- must each equal the oracle: a status word left over from a longer
+    parse would hand a later tile a wrong line number."""
+    rng = np.random.default_rng(0x5EC)
+    sizes = [(150000, 0), (2000, 0), (150000, 3), (40000, 1), (0, 0), (160000, 0), (700, 5)]
+    for nlines, offset in sizes:
+        text = _random_text(rng, nlines, 0) if nlines else b""
+        es, ed, en, eb = oracle_mod.parse_edges(text, 0)
+        s, d, n, b = _gpu_parse(gs, text, 0, offset)
+        assert (n, b) == (en, eb), (nlines, offset, n, b, en, eb)
+        assert np.array_equal(s, es) and np.array_equal(d, ed), (nlines, offset)
+    # the host text path (gs_fold_text, the summary's own scratch), texts of different sizes
+    for nlines in (60000, 900, 60000):
+        a = rng.integers(-(10 ** 12), 10 ** 12, nlines)
+        b = rng.integers(0, 5000, nlines)
+        text = b"\n".join(b"%d %d" % (int(x), int(y)) for x, y in zip(a, b)) + b"\n"
+        es, ed, en, eb = oracle_mod.parse_edges(text, 0)
+        assert eb == -1 and en == nlines
+        with gs.Summary("cc", capacity_hint=1 << 16) as summ:
+            assert summ.fold_text(text) == nlines
+            assert summ.num_vertices() == len(np.unique(np.concatenate([es, ed])))
