@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "gs_fold_records_counted_device", "gs_reset_config", "gs_wait_event", "gs_wait_stream", "gs_fold_device_after",
     "gs_fold_parity", "gs_set_window_server", "gs_window_server_stats", "gs_set_batch_dedup",
     "gs_digest", "gs_group_comm_ranks", "gs_group_set_phase_timing", "gs_group_phase_stats",
+    "gs_group_set_comm_api", "gs_testing_set", "gs_testing_get", "gs_hbm_bytes", "gs_create_bytes",
 )
 
 FAIL_BIT = 1 << 62  # count words: a failed signed verdict (GS_FAIL_BIT)
@@ -165,8 +166,100 @@ def lib():
     L.gs_group_comm_ranks.argtypes = [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
     L.gs_group_set_phase_timing.argtypes = [_vp, ctypes.c_int]
     L.gs_group_phase_stats.argtypes = [_vp, ctypes.POINTER(ctypes.c_double)]
+    L.gs_group_set_comm_api.argtypes = [_vp]
+    L.gs_hbm_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(_u64)]
+    L.gs_create_bytes.argtypes = [ctypes.c_int, _u64, ctypes.POINTER(_u64)]
+    L.gs_testing_set.argtypes = [ctypes.c_int, _i64]
+    L.gs_testing_get.argtypes = [ctypes.c_int]
+    L.gs_testing_get.restype = _i64
     _lib = L
     return L
+
+
+def hbm_bytes(device=0):
+    """gs_hbm_bytes: device memory held by every live summary / group of this process."""
+    b = _u64()
+    _check(lib().gs_hbm_bytes(int(device), ctypes.byref(b)))
+    return b.value
+
+
+def create_bytes(kind, capacity_hint):
+    """gs_create_bytes: the device bytes gs_create(kind, capacity_hint) allocates."""
+    b = _u64()
+    k = {"cc": KIND_CC, "signed": KIND_SIGNED}[kind] if isinstance(kind, str) else int(kind)
+    _check(lib().gs_create_bytes(k, int(capacity_hint), ctypes.byref(b)))
+    return b.value
+
+
+# ---------------------------------------------------------------- test controls
+# include/gs_testing.h: private knobs the tests use (the product reads no environment)
+TESTING_KNOBS = {"server_idle_us": 0, "changes_walk_max": 1, "parse_lb_timeout_us": 2, "group_self_apply": 3,
+                 "group_data_lag": 4}
+
+
+def testing_set(knob, value):
+    """gs_testing_set: a test knob (name of TESTING_KNOBS) to `value`; None or < 0
+    restores the product value."""
+    _check(lib().gs_testing_set(TESTING_KNOBS[knob], -1 if value is None else int(value)))
+
+
+def testing_get(knob):
+    return lib().gs_testing_get(TESTING_KNOBS[knob])
+
+
+class testing:
+    """Context manager: `with gsamd.testing(server_idle_us=100): ...` sets test knobs
+    and restores the product values on exit."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            testing_set(k, v)
+        return self
+
+    def __exit__(self, *a):
+        for k in self.knobs:
+            testing_set(k, None)
+
+
+FAKE_COMM_PATH = os.path.join(_HERE, "host", "bin", "libgs_fakecomm.so")
+_fake = None
+
+
+def fake_comm():
+    """The in-process collectives emulation (tests/cpp/gs_fake_comm.cpp; test
+    infrastructure, built by the host Makefile)."""
+    global _fake
+    if _fake is None:
+        lib()  # (torch's HIP runtime first)
+        if not os.path.exists(FAKE_COMM_PATH):
+            raise ImportError("libgs_fakecomm.so not built (%s); run __graft_entry__.build()" % FAKE_COMM_PATH)
+        F = ctypes.CDLL(FAKE_COMM_PATH)
+        F.gs_fake_comm_api.restype = _vp
+        F.gs_fake_comm_last_error.restype = ctypes.c_int
+        F.gs_fake_comm_order_hash.restype = _u64
+        _fake = F
+    return _fake
+
+
+def use_comm_emulation(on=True):
+    """gs_group_set_comm_api: groups created afterwards run their collectives through the
+    in-process emulation (N rank threads on one GPU; it fails a collective whose ranks
+    issued the communicators' collectives in different orders) -- or RCCL again (False)."""
+    _check(lib().gs_group_set_comm_api(fake_comm().gs_fake_comm_api() if on else None))
+
+
+class comm_emulation:
+    """Context manager around use_comm_emulation(True)."""
+
+    def __enter__(self):
+        use_comm_emulation(True)
+        return self
+
+    def __exit__(self, *a):
+        use_comm_emulation(False)
 
 
 def _check(rc):

@@ -9,7 +9,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <mutex>
+#include <unordered_map>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -19,6 +22,12 @@
 #include "gs_ingest.h"
 #include "gs_internal.hpp"
 
+// Young-table head chunk (fold_device_impl): log2 of the edges of an empty table's first
+// fold that go alone (0: off)
+#ifndef GS_YOUNG_HEAD_LOG2
+#define GS_YOUNG_HEAD_LOG2 14
+#endif
+
 namespace gsi {
 
 thread_local std::string g_err;
@@ -26,6 +35,45 @@ thread_local std::string g_err;
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
+}
+
+// Device-memory accounting (gs_hbm_bytes): every allocation of summary / group state
+// goes through dmalloc, which remembers its size and device.
+std::atomic<uint64_t> g_hbm[kMaxDevices];
+std::mutex g_alloc_mu;
+std::unordered_map<void*, std::pair<int, size_t>> g_allocs;
+
+hipError_t dmalloc(void** p, size_t bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const hipError_t e = dmalloc(p, bytes);
+  if (e == hipSuccess && *p) {
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    g_allocs[*p] = {dev, bytes};
+    if (dev >= 0 && dev < kMaxDevices) g_hbm[dev] += bytes;
+  }
+  return e;
+}
+
+hipError_t dfree(void* p) {
+  if (!p) return hipSuccess;
+  {
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    auto it = g_allocs.find(p);
+    if (it != g_allocs.end()) {
+      if (it->second.first >= 0 && it->second.first < kMaxDevices) g_hbm[it->second.first] -= it->second.second;
+      g_allocs.erase(it);
+    }
+  }
+  return dfree(p);
+}
+
+// include/gs_testing.h: process-wide test knobs, -1 = unset (the product value)
+std::atomic<int64_t> g_testing[GS_TESTING_KNOBS] = {{-1}, {-1}, {-1}, {-1}, {-1}};
+
+int64_t testing_value(int knob, int64_t product) {
+  const int64_t v = g_testing[knob].load(std::memory_order_relaxed);
+  return v < 0 ? product : v;
 }
 
 namespace {
@@ -106,7 +154,7 @@ int wait_x_consumer(gs_summary* h) {
 // Combine scratch of at least `rows` rows (v, label, parity), allocated on growth only.
 int ensure_x(gs_summary* h, uint64_t rows) {
   if (!h->x_cnt) {
-    GS_HIP(hipMalloc(&h->x_cnt, 16));
+    GS_HIP(dmalloc(&h->x_cnt, 16));
     GS_HIP(hipEventCreateWithFlags(&h->x_ready, hipEventDisableTiming));
     GS_HIP(hipEventCreateWithFlags(&h->x_used, hipEventDisableTiming));
   }
@@ -114,16 +162,16 @@ int ensure_x(gs_summary* h, uint64_t rows) {
   if (h->x_v) {
     if (int rc = wait_x_consumer(h)) return rc;
     GS_HIP(hipStreamSynchronize(h->stream));
-    (void)hipFree(h->x_v);
-    (void)hipFree(h->x_l);
-    (void)hipFree(h->x_p);
+    (void)dfree(h->x_v);
+    (void)dfree(h->x_l);
+    (void)dfree(h->x_p);
     h->x_v = h->x_l = nullptr;
     h->x_p = nullptr;
   }
   const uint64_t c = std::max<uint64_t>(rows, (uint64_t)(kMaxLoad * (double)h->cap) + 2);
-  GS_HIP(hipMalloc(&h->x_v, c * 8));
-  GS_HIP(hipMalloc(&h->x_l, c * 8));
-  GS_HIP(hipMalloc(&h->x_p, c));
+  GS_HIP(dmalloc(&h->x_v, c * 8));
+  GS_HIP(dmalloc(&h->x_l, c * 8));
+  GS_HIP(dmalloc(&h->x_p, c));
   h->x_cap = c;
   return GS_OK;
 }
@@ -141,11 +189,29 @@ void reset_capacity_tracking(gs_summary* h, uint64_t nv) {
   h->rep_pending_edges = 0;
 }
 
+}  // namespace
+
+// gs_create's table for a hint: kSlotsPerHintedVertex slots per expected vertex, a power of
+// two, >= 1024
+uint64_t create_capacity(uint64_t capacity_hint) {
+  const uint64_t cap = next_pow2(std::max<uint64_t>(kSlotsPerHintedVertex * std::max<uint64_t>(capacity_hint, 1), 1024));
+  return std::min(cap, kMaxCap);
+}
+
+// device bytes gs_create allocates for a table of cap slots (alloc_table + gs_create's own;
+// the host-fold staging comes with the first host fold, sized for its chunks)
+uint64_t create_bytes(uint64_t cap) {
+  return (cap + 1) * sizeof(gs::Slot) + (uint64_t)gs::kShards * (cap / gs::kShards + 1024) * 4 +
+         (uint64_t)gs::CTR_COUNT * gs::kCtrStride * 4 + 64;
+}
+
+namespace {
+
 int alloc_vlist(gs_summary* h) {
-  (void)hipFree(h->vlist);
+  (void)dfree(h->vlist);
   h->vlist = nullptr;
   h->vshard_cap = (uint32_t)(h->cap / gs::kShards + 1024);
-  GS_HIP(hipMalloc(&h->vlist, (size_t)gs::kShards * h->vshard_cap * 4));
+  GS_HIP(dmalloc(&h->vlist, (size_t)gs::kShards * h->vshard_cap * 4));
   return GS_OK;
 }
 
@@ -154,7 +220,7 @@ int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
   h->cap = cap;
   h->logcap = 0;
   while ((1ull << h->logcap) < cap) ++h->logcap;
-  GS_HIP(hipMalloc(&h->tab, (cap + 1) * sizeof(gs::Slot)));
+  GS_HIP(dmalloc(&h->tab, (cap + 1) * sizeof(gs::Slot)));
   if (int rc = alloc_vlist(h)) return rc;
   memset(h->h_flags, 0, 16);  // the device flags are cleared below (no kernel of the old table runs)
   if (keep_delta) {
@@ -184,11 +250,11 @@ int grow(gs_summary* h, uint64_t new_cap) {
   uint8_t* p = nullptr;
   const size_t m = nv + 1;
   auto release = [&] {
-    (void)hipFree(v);
-    (void)hipFree(l);
-    (void)hipFree(p);
+    (void)dfree(v);
+    (void)dfree(l);
+    (void)dfree(p);
   };
-  if (hipMalloc(&v, m * 8) != hipSuccess || hipMalloc(&l, m * 8) != hipSuccess || hipMalloc(&p, m) != hipSuccess) {
+  if (dmalloc(&v, m * 8) != hipSuccess || dmalloc(&l, m * 8) != hipSuccess || dmalloc(&p, m) != hipSuccess) {
     release();
     return fail(GS_ERR_HIP, "table rebuild: out of device memory");
   }
@@ -203,7 +269,7 @@ int grow(gs_summary* h, uint64_t new_cap) {
     release();
     return rc;
   }
-  (void)hipFree(h->tab);
+  (void)dfree(h->tab);
   h->tab = nullptr;
   const bool track = h->track;
   h->track = false;  // the rebuild is not a delta
@@ -273,11 +339,7 @@ int ensure_capacity(gs_summary* h, size_t n) {
   // GPU busy, instead of a drain before every fold (RMAT-20, config 2: 1.07 -> 0.72
   // ms/step).
   const uint64_t slack = 2ull * n * (uint64_t)(std::max({1, h->pipe_depth, h->group_lanes}) + 1);
-  static const bool slack_on = [] {  // experiment knob GS_SLACK_GROW=0: no slack sizing (tools/fold_stats.py)
-    const char* e = getenv("GS_SLACK_GROW");
-    return !(e && atoi(e) == 0);
-  }();
-  const bool slack_grow = slack_on && h->cap < kSlackGrowMaxCap && (double)(h->nv_exact + slack) > limit;
+  const bool slack_grow = h->cap < kSlackGrowMaxCap && (double)(h->nv_exact + slack) > limit;
   if (!slack_grow) {
     // wait for reports of the folds in flight (the GPU keeps working: no drain)
     h->cap_waits++;
@@ -362,16 +424,12 @@ int server_start(gs_summary* h) {
   // ~2 ms without a window: the launch leaves on its own (wall clock 100 MHz). It holds
   // its stream's hardware queue while resident, so another stream that shares the queue
   // waits at most that long behind an idle server (the config-5 windows arrive
-  // back to back; a restart costs one launch). GS_SERVER_IDLE_US overrides it (tests of
-  // the exit paths with late workgroups).
-  const char* idle_env = getenv("GS_SERVER_IDLE_US");  // read per start: a server start is rare
-  const long long idle_us = idle_env ? atoll(idle_env) : 0;
-  const unsigned long long idle_ticks = idle_us > 0 ? (unsigned long long)idle_us * 100ull : 200000ull;
-  const char* late_env = getenv("GS_SERVER_LATE_US");  // test hook: the last workgroup starts this late
-  const long long late_us = late_env ? atoll(late_env) : 0;
+  // back to back; a restart costs one launch). Tests of the exit paths shorten it
+  // (GS_TESTING_SERVER_IDLE_US, include/gs_testing.h).
+  const int64_t idle_us = testing_value(GS_TESTING_SERVER_IDLE_US, 2000);
+  const unsigned long long idle_ticks = (unsigned long long)std::max<int64_t>(idle_us, 1) * 100ull;
   gs::launch_window_server(h->kind == GS_KIND_SIGNED, h->table(), h->delta(), h->srv_box, h->srv_bc, h->done_dev,
-                           h->srv_seq, idle_ticks, late_us > 0 ? (unsigned long long)late_us * 100ull : 0ull,
-                           h->stream);
+                           h->srv_seq, idle_ticks, h->stream);
   GS_HIP(hipGetLastError());
   h->srv_running = true;
   h->srv_launches++;
@@ -498,13 +556,13 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
   // later batch; tools/fold_stats.py). The head inserts the stream's hubs; the rest reads
   // their keys. Config 2: 0.597 -> 0.552-0.558 ms/step; config 4 (uniform endpoints, no hubs)
   // pays the head's latency: 0.852-0.857 -> 0.858-0.865 (profiles/r05_young_ab.txt).
-  // GS_YOUNG_HEAD_LOG2 = k overrides the size (0: off).
-  static const int young_head_log2 = [] {
-    const char* e = getenv("GS_YOUNG_HEAD_LOG2");
-    return e ? atoi(e) : 14;
-  }();
+  // A build with -DGS_YOUNG_HEAD_LOG2=k sets the size (0: off). The head runs on the handle
+  // stream, so a fold the caller put on a lane or the side stream (and joins there) has none
+  // (ADVICE r5).
+  constexpr int young_head_log2 = GS_YOUNG_HEAD_LOG2;
   const bool young_head = young_head_log2 > 0 && check_cap && !track && fs.rows == 0 && !fs.take_out &&
-                          h->e_launched == 0 && h->nv_exact == 0 && n > ((size_t)2 << young_head_log2);
+                          fs.lane < 0 && !fs.on_side && h->e_launched == 0 && h->nv_exact == 0 &&
+                          n > ((size_t)2 << young_head_log2);
   if (check_cap && units) {
     if (int rc = ensure_capacity(h, units)) return rc;
   }
@@ -559,13 +617,13 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
         if (st == h->lane[li]) set = 1 + li;
       if (h->dd_edges[set] < c) {
         GS_HIP(hipStreamSynchronize(st));  // the set's previous user is done
-        (void)hipFree(h->dd_tab[set]);
-        (void)hipFree(h->dd_w[set]);
+        (void)dfree(h->dd_tab[set]);
+        (void)dfree(h->dd_w[set]);
         h->dd_tab[set] = nullptr;
         h->dd_w[set] = nullptr;
         const uint64_t e = next_pow2(c);
-        GS_HIP(hipMalloc(&h->dd_tab[set], 2 * e * 16));
-        GS_HIP(hipMalloc(&h->dd_w[set], e));
+        GS_HIP(dmalloc(&h->dd_tab[set], 2 * e * 16));
+        GS_HIP(dmalloc(&h->dd_w[set], e));
         h->dd_edges[set] = e;
       }
       const uint64_t slots = 2 * next_pow2(c);  // load factor <= 1/2
@@ -660,10 +718,10 @@ int ensure_delta_list(gs_summary* h, uint64_t edges) {
   if (per > 0xFFFFFFFFull) return fail(GS_ERR_INVALID, "delta list too large");
   if (h->drec) {
     GS_HIP(hipStreamSynchronize(h->stream));
-    (void)hipFree(h->drec);
+    (void)dfree(h->drec);
     h->drec = nullptr;
   }
-  GS_HIP(hipMalloc(&h->drec, (size_t)gs::kDeltaSets * gs::kShards * per * 24));
+  GS_HIP(dmalloc(&h->drec, (size_t)gs::kDeltaSets * gs::kShards * per * 24));
   h->delta_shard_cap = (uint32_t)per;
   h->delta_edges = edges;
   return GS_OK;
@@ -704,19 +762,16 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
   gs_summary* h = new gs_summary();
   h->device = device;
   h->kind = kind;
-  uint64_t cap = next_pow2(std::max<uint64_t>(kSlotsPerHintedVertex * std::max<uint64_t>(capacity_hint, 1), 1024));
-  if (cap > kMaxCap) cap = kMaxCap;
+  const uint64_t cap = create_capacity(capacity_hint);
   auto bail = [&](int code) {
     gs_destroy(h);
     return code;
   };
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipStreamCreate failed"));
-  if (hipMalloc(&h->ctr, gs::CTR_COUNT * gs::kCtrStride * 4) != hipSuccess)
+  if (dmalloc(&h->ctr, gs::CTR_COUNT * gs::kCtrStride * 4) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipMalloc(counters) failed"));
-  if (hipMalloc(&h->d_stage, sizeof(int64_t) * 4 * kStageChunk) != hipSuccess ||
-      hipMalloc(&h->d_wstage, 2 * kStageChunk) != hipSuccess || hipMalloc(&h->d_scratch, 64) != hipSuccess)
-    return bail(fail(GS_ERR_HIP, "hipMalloc(staging) failed"));
+  if (dmalloc(&h->d_scratch, 64) != hipSuccess) return bail(fail(GS_ERR_HIP, "hipMalloc(scratch) failed"));
   if (hipHostMalloc(&h->h_flags, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hflags_dev), h->h_flags, 0) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipHostMalloc(flags) failed"));
@@ -753,11 +808,11 @@ int gs_destroy(gs_handle h) {
   if (h->main_ev) (void)hipEventDestroy(h->main_ev);
   if (h->ext_ev) (void)hipEventDestroy(h->ext_ev);
   for (int i = 0; i < gs_summary::kDedupSets; ++i) {
-    (void)hipFree(h->dd_tab[i]);
-    (void)hipFree(h->dd_w[i]);
+    (void)dfree(h->dd_tab[i]);
+    (void)dfree(h->dd_w[i]);
   }
   if (h->srv_box) (void)hipHostFree(h->srv_box);
-  if (h->srv_bc) (void)hipFree(h->srv_bc);
+  if (h->srv_bc) (void)dfree(h->srv_bc);
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 2; ++i) {
     if (h->stage_ev[i]) (void)hipEventDestroy(h->stage_ev[i]);
@@ -776,7 +831,7 @@ int gs_destroy(gs_handle h) {
                   (void*)h->chg_ol, (void*)h->chg_op, (void*)h->d_stage,
                   (void*)h->d_wstage, (void*)h->d_scratch, (void*)h->x_v, (void*)h->x_l, (void*)h->x_p,
                   (void*)h->x_cnt})
-    (void)hipFree(p);
+    (void)dfree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return GS_OK;
@@ -863,18 +918,45 @@ static int ensure_host_stage(gs_summary* h) {
   return GS_OK;
 }
 
+// The device staging buffers (two, alternating) come with the first host fold, sized for
+// its chunks (a power of two, 4 K .. 2^20 edges), and grow with a larger one: a handle of
+// the JNI pool whose flushes are small does not hold 34 MB of staging (gs_hbm_bytes).
+static int ensure_dev_stage(gs_summary* h, size_t edges) {
+  if (edges <= h->d_stage_chunk) return GS_OK;
+  size_t c = 4096;
+  while (c < edges) c <<= 1;
+  c = std::min<size_t>(c, kStageChunk);
+  if (h->d_stage) {  // folds queued on the stream or the lanes may still read the old buffers
+    if (int rc = join_lanes(h)) return rc;
+    GS_HIP(hipStreamSynchronize(h->stream));
+    (void)dfree(h->d_stage);
+    (void)dfree(h->d_wstage);
+    h->d_stage = nullptr;
+    h->d_wstage = nullptr;
+    h->d_stage_chunk = 0;
+  }
+  GS_HIP(dmalloc(&h->d_stage, sizeof(int64_t) * 4 * c));
+  GS_HIP(dmalloc(&h->d_wstage, 2 * c));
+  h->d_stage_chunk = c;
+  return GS_OK;
+}
+
 static int fold_host_impl(gs_handle h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n) {
   bool direct_pending = false;
   const bool pinned = n > kDirectCopyEdges && host_pinned(src) && host_pinned(dst) && host_pinned(w);
+  if (n) {
+    if (int rc = ensure_dev_stage(h, std::min<size_t>(n, kStageChunk))) return rc;
+  }
+  const size_t sc = h->d_stage_chunk;
   for (size_t off = 0; off < n; off += kStageChunk) {
     const size_t c = std::min<size_t>(kStageChunk, n - off);
     const int b = h->stage_next;
     h->stage_next ^= 1;
-    int64_t* ds = h->d_stage + (size_t)b * 2 * kStageChunk;
-    uint8_t* dwp = w ? h->d_wstage + (size_t)b * kStageChunk : nullptr;
+    int64_t* ds = h->d_stage + (size_t)b * 2 * sc;
+    uint8_t* dwp = w ? h->d_wstage + (size_t)b * sc : nullptr;
     if (c <= kDirectCopyEdges || pinned) {
       GS_HIP(hipMemcpyAsync(ds, src + off, c * 8, hipMemcpyHostToDevice, h->stream));
-      GS_HIP(hipMemcpyAsync(ds + kStageChunk, dst + off, c * 8, hipMemcpyHostToDevice, h->stream));
+      GS_HIP(hipMemcpyAsync(ds + sc, dst + off, c * 8, hipMemcpyHostToDevice, h->stream));
       if (w) GS_HIP(hipMemcpyAsync(dwp, w + off, c, hipMemcpyHostToDevice, h->stream));
       direct_pending = true;
     } else {
@@ -884,7 +966,7 @@ static int fold_host_impl(gs_handle h, const int64_t* src, const int64_t* dst, c
       memcpy(hs, src + off, c * 8);
       memcpy(hs + kStageChunk, dst + off, c * 8);
       GS_HIP(hipMemcpyAsync(ds, hs, c * 8, hipMemcpyHostToDevice, h->stream));
-      GS_HIP(hipMemcpyAsync(ds + kStageChunk, hs + kStageChunk, c * 8, hipMemcpyHostToDevice, h->stream));
+      GS_HIP(hipMemcpyAsync(ds + sc, hs + kStageChunk, c * 8, hipMemcpyHostToDevice, h->stream));
       if (w) {
         uint8_t* hw = h->h_wstage + (size_t)b * kStageChunk;
         memcpy(hw, w + off, c);
@@ -893,7 +975,7 @@ static int fold_host_impl(gs_handle h, const int64_t* src, const int64_t* dst, c
       direct_pending = false;
     }
     GS_HIP(hipEventRecord(h->stage_ev[b], h->stream));  // this chunk's copies
-    int rc = fold_device_impl(h, ds, ds + kStageChunk, dwp, c, 1, 1, h->track);
+    int rc = fold_device_impl(h, ds, ds + sc, dwp, c, 1, 1, h->track);
     if (rc) return rc;
   }
   // a direct chunk reads the caller's buffer until its copies are done: the last chunk's
@@ -1364,7 +1446,7 @@ int gs_set_window_server(gs_handle h, int on) {
   if (int rc = join_lanes(h)) return rc;  // stops a running server
   if (on && !h->srv_box) {
     GS_HIP(hipHostMalloc(&h->srv_box, sizeof(gs::ServerBox), hipHostMallocMapped | hipHostMallocCoherent));
-    GS_HIP(hipMalloc(&h->srv_bc, sizeof(gs::ServerBcast)));
+    GS_HIP(dmalloc(&h->srv_bc, sizeof(gs::ServerBcast)));
     memset(h->srv_box, 0, sizeof(gs::ServerBox));
   }
   h->srv_on = on != 0;
@@ -1583,10 +1665,10 @@ int gs_fold_text(gs_handle h, const char* text, size_t len, int sep, uint64_t* n
     const size_t sb = gs::parse_scratch_bytes(kTextChunk, &cub);
     GS_HIP(hipHostMalloc(&h->h_text, 2 * kTextChunk, hipHostMallocDefault));
     GS_HIP(hipHostMalloc(&h->h_tres, 4 * sizeof(uint64_t), hipHostMallocDefault));
-    GS_HIP(hipMalloc(&h->d_text, 2 * kTextChunk));
-    GS_HIP(hipMalloc(&h->d_tsrc, max_lines * 8));
-    GS_HIP(hipMalloc(&h->d_tdst, max_lines * 8));
-    GS_HIP(hipMalloc(&h->d_tscratch, sb));
+    GS_HIP(dmalloc(&h->d_text, 2 * kTextChunk));
+    GS_HIP(dmalloc(&h->d_tsrc, max_lines * 8));
+    GS_HIP(dmalloc(&h->d_tdst, max_lines * 8));
+    GS_HIP(dmalloc(&h->d_tscratch, sb));
     for (int i = 0; i < 2; ++i) GS_HIP(hipEventCreateWithFlags(&h->text_ev[i], hipEventDisableTiming));
     gs::parse_scratch_init(h->tscratch, h->d_tscratch, kTextChunk);
   }
@@ -1648,3 +1730,29 @@ int gs_table_capacity(gs_handle h, uint64_t* slots) {
 }
 
 }  // extern "C"
+
+extern "C" int gs_testing_set(int knob, int64_t value) {
+  if (knob < 0 || knob >= GS_TESTING_KNOBS) return gsi::fail(GS_ERR_INVALID, "unknown test knob");
+  gsi::g_testing[knob].store(value < 0 ? -1 : value, std::memory_order_relaxed);
+  return GS_OK;
+}
+
+extern "C" int64_t gs_testing_get(int knob) {
+  if (knob < 0 || knob >= GS_TESTING_KNOBS) return -1;
+  static const int64_t product[GS_TESTING_KNOBS] = {2000, 1 << 16, 50000, 0, 2};
+  return gsi::testing_value(knob, product[knob]);
+}
+
+extern "C" int gs_hbm_bytes(int device, uint64_t* bytes) {
+  if (!bytes) return gsi::fail(GS_ERR_INVALID, "bytes is null");
+  if (device < 0 || device >= gsi::kMaxDevices) return gsi::fail(GS_ERR_INVALID, "bad device");
+  *bytes = gsi::g_hbm[device].load(std::memory_order_relaxed);
+  return GS_OK;
+}
+
+extern "C" int gs_create_bytes(int kind, uint64_t capacity_hint, uint64_t* bytes) {
+  if (!bytes) return gsi::fail(GS_ERR_INVALID, "bytes is null");
+  if (kind != GS_KIND_CC && kind != GS_KIND_SIGNED) return gsi::fail(GS_ERR_INVALID, "unknown kind");
+  *bytes = gsi::create_bytes(gsi::create_capacity(capacity_hint));
+  return GS_OK;
+}

@@ -24,9 +24,8 @@ namespace {
 
 constexpr uint32_t kWalkMax = 1u << 16;  // member-list walk limit per hooked root
 
-uint32_t walk_max() {
-  const char* e = getenv("GS_CHANGES_WALK_MAX");  // test knob: force the scan path
-  return e ? (uint32_t)std::max(1, atoi(e)) : kWalkMax;
+uint32_t walk_max() {  // test knob GS_TESTING_CHANGES_WALK_MAX forces the scan path
+  return (uint32_t)std::max<int64_t>(1, std::min<int64_t>(testing_value(GS_TESTING_CHANGES_WALK_MAX, kWalkMax), kWalkMax));
 }
 
 // scratch layout: [0] record count (u64), [1..8] vertex-list marks (64 x u32),
@@ -52,11 +51,11 @@ int ensure_scratch(gs_summary* h) {
   if (h->chg_scratch && h->chg_scratch_rows >= rows) return GS_OK;
   if (h->chg_scratch) {
     GS_HIP(hipStreamSynchronize(h->stream));
-    (void)hipFree(h->chg_scratch);
+    (void)dfree(h->chg_scratch);
     h->chg_scratch = nullptr;
   }
   const size_t words = 1 + gs::kShards / 2 + (rows + 1) / 2 + 3 * rows;
-  GS_HIP(hipMalloc(&h->chg_scratch, words * 8));
+  GS_HIP(dmalloc(&h->chg_scratch, words * 8));
   GS_HIP(hipMemsetAsync(h->chg_scratch, 0, (1 + gs::kShards / 2) * 8, h->stream));
   h->chg_scratch_rows = rows;
   return GS_OK;
@@ -66,10 +65,10 @@ int ensure_nxt(gs_summary* h) {
   if (h->nxt && h->nxt_slots == h->cap + 1) return GS_OK;
   if (h->nxt) {
     GS_HIP(hipStreamSynchronize(h->stream));
-    (void)hipFree(h->nxt);
+    (void)dfree(h->nxt);
     h->nxt = nullptr;
   }
-  GS_HIP(hipMalloc(&h->nxt, (h->cap + 1) * 4));
+  GS_HIP(dmalloc(&h->nxt, (h->cap + 1) * 4));
   h->nxt_slots = h->cap + 1;
   return GS_OK;
 }
@@ -191,16 +190,16 @@ int gs_take_changes(gs_handle h, int64_t* v, int64_t* label, uint8_t* parity, si
   *n = 0;
   if (cap < nv) return fail(GS_ERR_INVALID, "cap below the vertex count: " + std::to_string(nv));
   if (h->chg_ocap < nv + 1) {
-    (void)hipFree(h->chg_ov);
-    (void)hipFree(h->chg_ol);
-    (void)hipFree(h->chg_op);
+    (void)dfree(h->chg_ov);
+    (void)dfree(h->chg_ol);
+    (void)dfree(h->chg_op);
     h->chg_ov = h->chg_ol = nullptr;
     h->chg_op = nullptr;
     h->chg_ocap = 0;
     const uint64_t rows = std::max<uint64_t>(nv + 1, 1024) * 5 / 4;  // headroom: fewer reallocations
-    GS_HIP(hipMalloc(&h->chg_ov, rows * 8));
-    GS_HIP(hipMalloc(&h->chg_ol, rows * 8));
-    GS_HIP(hipMalloc(&h->chg_op, rows));
+    GS_HIP(dmalloc(&h->chg_ov, rows * 8));
+    GS_HIP(dmalloc(&h->chg_ol, rows * 8));
+    GS_HIP(dmalloc(&h->chg_op, rows));
     h->chg_ocap = rows;
   }
   uint64_t k = 0;

@@ -36,6 +36,7 @@
 
 #include "gs_group.h"
 #include "gs_internal.hpp"
+#include "gs_testing.h"
 
 using namespace gsi;
 
@@ -59,237 +60,118 @@ constexpr uint64_t kMicro = 1ull << 20;
 #define GS_GROUP_LANES_N 3
 #endif
 constexpr int kGroupLanes = GS_GROUP_LANES_N;  // own-fold lanes (chunk c runs on lane c mod kGroupLanes)
+#ifndef GS_GROUP_HOSTPROF
+#define GS_GROUP_HOSTPROF 0
+#endif
+#ifndef GS_GROUP_NO_LANES
+#define GS_GROUP_NO_LANES 0
+#endif
+#ifndef GS_GROUP_NO_SIDE
+#define GS_GROUP_NO_SIDE 0
+#endif
+#ifndef GS_GROUP_HIPRIO
+#define GS_GROUP_HIPRIO 0
+#endif
 
-struct RcclApi {
+// RCCL behind the gs_comm_api table (include/gs_group.h). ncclCommInitRank takes its
+// ncclUniqueId (128 B) by value: the adapter copies the caller's bytes into one.
+struct Id128 {
+  char b[kIdBytes];
+};
+struct RcclSyms {
   void* lib = nullptr;
   int (*getUniqueId)(void*) = nullptr;
-  int (*allGather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
+  int (*initRank)(void**, int, Id128, int) = nullptr;
   int (*commDestroy)(void*) = nullptr;
+  int (*commCount)(void*, int*) = nullptr;
+  int (*allGather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
+  int (*allToAllv)(const void*, const size_t*, const size_t*, void*, const size_t*, const size_t*, int, void*,
+                   hipStream_t) = nullptr;
   int (*send)(const void*, size_t, int, int, void*, hipStream_t) = nullptr;
   int (*recv)(void*, size_t, int, int, void*, hipStream_t) = nullptr;
   int (*groupStart)() = nullptr;
   int (*groupEnd)() = nullptr;
   const char* (*getErrorString)(int) = nullptr;
-  int (*commCount)(void*, int*) = nullptr;  // ncclCommCount: ranks of a communicator
-  void* initRankSym = nullptr;  // ncclCommInitRank takes ncclUniqueId (128 B) by value: see Id128
 };
+RcclSyms g_rs;
 
-struct Id128 {
-  char b[kIdBytes];
-};
+int rc_unique_id(void* id) { return g_rs.getUniqueId(id); }
+int rc_init(void** comm, int n, const void* id, int rank) {
+  Id128 u;
+  memcpy(u.b, id, kIdBytes);
+  return g_rs.initRank(comm, n, u, rank);
+}
+int rc_destroy(void* c) { return g_rs.commDestroy(c); }
+int rc_count(void* c, int* n) { return g_rs.commCount ? g_rs.commCount(c, n) : 1; }
+int rc_all_gather(const void* s, void* r, size_t n, int t, void* c, void* st) {
+  return g_rs.allGather(s, r, n, t, c, (hipStream_t)st);
+}
+int rc_all_to_allv(const void* s, const size_t* sc, const size_t* sd, void* r, const size_t* rc, const size_t* rd,
+                   int t, void* c, void* st) {
+  return g_rs.allToAllv ? g_rs.allToAllv(s, sc, sd, r, rc, rd, t, c, (hipStream_t)st) : 1;
+}
+int rc_send(const void* b, size_t n, int t, int p, void* c, void* st) {
+  return g_rs.send ? g_rs.send(b, n, t, p, c, (hipStream_t)st) : 1;
+}
+int rc_recv(void* b, size_t n, int t, int p, void* c, void* st) {
+  return g_rs.recv ? g_rs.recv(b, n, t, p, c, (hipStream_t)st) : 1;
+}
+int rc_group_start() { return g_rs.groupStart ? g_rs.groupStart() : 1; }
+int rc_group_end() { return g_rs.groupEnd ? g_rs.groupEnd() : 1; }
+const char* rc_error(int r) { return g_rs.getErrorString ? g_rs.getErrorString(r) : "rccl error"; }
 
-RcclApi g_rccl;
+gs_comm_api g_rccl_api = {rc_unique_id, rc_init,  rc_destroy,     rc_count,     rc_all_gather, rc_all_to_allv,
+                          rc_send,      rc_recv,  rc_group_start, rc_group_end, rc_error};
 
 int rccl_load() {
-  if (g_rccl.lib) return GS_OK;
+  if (g_rs.lib) return GS_OK;
   void* l = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
   if (!l) l = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
   if (!l) return fail(GS_ERR_HIP, std::string("cannot load RCCL: ") + dlerror());
-  g_rccl.getUniqueId = (int (*)(void*))dlsym(l, "ncclGetUniqueId");
-  g_rccl.initRankSym = dlsym(l, "ncclCommInitRank");
-  g_rccl.allGather = (int (*)(const void*, void*, size_t, int, void*, hipStream_t))dlsym(l, "ncclAllGather");
-  g_rccl.commDestroy = (int (*)(void*))dlsym(l, "ncclCommDestroy");
-  g_rccl.getErrorString = (const char* (*)(int))dlsym(l, "ncclGetErrorString");
-  g_rccl.send = (int (*)(const void*, size_t, int, int, void*, hipStream_t))dlsym(l, "ncclSend");
-  g_rccl.recv = (int (*)(void*, size_t, int, int, void*, hipStream_t))dlsym(l, "ncclRecv");
-  g_rccl.groupStart = (int (*)())dlsym(l, "ncclGroupStart");
-  g_rccl.groupEnd = (int (*)())dlsym(l, "ncclGroupEnd");
-  g_rccl.commCount = (int (*)(void*, int*))dlsym(l, "ncclCommCount");
-  if (!g_rccl.getUniqueId || !g_rccl.initRankSym || !g_rccl.allGather || !g_rccl.commDestroy)
+  RcclSyms s;
+  s.getUniqueId = (int (*)(void*))dlsym(l, "ncclGetUniqueId");
+  s.initRank = (int (*)(void**, int, Id128, int))dlsym(l, "ncclCommInitRank");
+  s.allGather = (int (*)(const void*, void*, size_t, int, void*, hipStream_t))dlsym(l, "ncclAllGather");
+  s.allToAllv = (int (*)(const void*, const size_t*, const size_t*, void*, const size_t*, const size_t*, int, void*,
+                         hipStream_t))dlsym(l, "ncclAllToAllv");
+  s.commDestroy = (int (*)(void*))dlsym(l, "ncclCommDestroy");
+  s.getErrorString = (const char* (*)(int))dlsym(l, "ncclGetErrorString");
+  s.send = (int (*)(const void*, size_t, int, int, void*, hipStream_t))dlsym(l, "ncclSend");
+  s.recv = (int (*)(void*, size_t, int, int, void*, hipStream_t))dlsym(l, "ncclRecv");
+  s.groupStart = (int (*)())dlsym(l, "ncclGroupStart");
+  s.groupEnd = (int (*)())dlsym(l, "ncclGroupEnd");
+  s.commCount = (int (*)(void*, int*))dlsym(l, "ncclCommCount");
+  if (!s.getUniqueId || !s.initRank || !s.allGather || !s.commDestroy)
     return fail(GS_ERR_HIP, "RCCL is missing ncclGetUniqueId/ncclCommInitRank/ncclAllGather/ncclCommDestroy");
-  g_rccl.lib = l;
+  s.lib = l;
+  g_rs = s;
   return GS_OK;
 }
 
-int rccl_fail(const RcclApi* api, const char* what, int r) {
-  return fail(GS_ERR_HIP, std::string(what) + ": " + (api && api->getErrorString ? api->getErrorString(r) : "rccl error"));
+int rccl_fail(const gs_comm_api* api, const char* what, int r) {
+  return fail(GS_ERR_HIP, std::string(what) + ": " + (api && api->error_string ? api->error_string(r) : "comm error"));
 }
 
 constexpr int kNcclInt64 = 4;  // ncclInt64 (rccl.h)
 constexpr int kNcclUint8 = 1;  // ncclUint8 (rccl.h)
 
-// ---------------------------------------------------------------------------
-// In-process emulation of the RCCL calls the group uses, selected with
-// GS_GROUP_FAKE_COMM=1: N threads of ONE process, each driving one rank's summary
-// on the same GPU, meet at host barriers; the data moves with device copies
-// ordered by events. Test infrastructure only (RCCL refuses two ranks on one GPU,
-// and the GPU box has one): it runs the group's N-rank code paths -- count and data
-// collectives, exchange-layout fold of real remote rows on the side stream, the
-// binomial tree -- exactly as with RCCL.
-struct FakeShared {
-  int n = 0, refs = 0;
-  std::mutex m;
-  std::condition_variable cv;
-  int arrived = 0;
-  uint64_t gen = 0;
-  std::vector<const void*> src;
-  std::vector<hipEvent_t> ev;
-  struct Msg {
-    const void* buf;
-    size_t bytes;
-    hipEvent_t ready, copied;
-    bool done = false;
-  };
-  std::map<std::pair<int, int>, std::deque<Msg*>> box;  // (from, to) -> messages
-};
-struct FakeComm {
-  FakeShared* s;
-  int rank;
-  hipEvent_t ready = nullptr, done = nullptr;
-  std::vector<hipEvent_t> spare;  // message events, destroyed with the comm
-};
-std::mutex g_fake_mu;
-std::map<std::string, FakeShared*> g_fake_reg;
+// gs_group_set_comm_api: a caller's table (copied), or RCCL
+std::mutex g_api_mu;
+bool g_user_api_on = false;
+gs_comm_api g_user_api;
 
-void fake_barrier(FakeShared* s) {
-  std::unique_lock<std::mutex> lk(s->m);
-  const uint64_t g0 = s->gen;
-  if (++s->arrived == s->n) {
-    s->arrived = 0;
-    s->gen++;
-    s->cv.notify_all();
-  } else {
-    s->cv.wait(lk, [&] { return s->gen != g0; });
-  }
-}
-size_t fake_elem(int dtype) { return dtype == kNcclUint8 ? 1 : 8; }
-int fake_unique_id(void* id) {
-  static std::atomic<uint64_t> ctr{1};
-  memset(id, 0, kIdBytes);
-  const uint64_t v[2] = {(uint64_t)getpid(), ctr++};
-  memcpy(id, v, sizeof v);
-  return 0;
-}
-int fake_init(void** comm, int n, Id128 id, int rank) {
-  std::lock_guard<std::mutex> lk(g_fake_mu);
-  FakeShared*& s = g_fake_reg[std::string(id.b, kIdBytes)];
-  if (!s) {
-    s = new FakeShared();
-    s->n = n;
-    s->src.resize(n);
-    s->ev.resize(n);
-  }
-  s->refs++;
-  FakeComm* c = new FakeComm{s, rank};
-  if (hipEventCreateWithFlags(&c->ready, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess)
-    return 1;
-  *comm = c;
-  return 0;
-}
-int fake_destroy(void* comm) {
-  FakeComm* c = (FakeComm*)comm;
-  (void)hipEventDestroy(c->ready);
-  (void)hipEventDestroy(c->done);
-  for (hipEvent_t e : c->spare) (void)hipEventDestroy(e);
-  std::lock_guard<std::mutex> lk(g_fake_mu);
-  if (--c->s->refs == 0) {
-    for (auto it = g_fake_reg.begin(); it != g_fake_reg.end(); ++it)
-      if (it->second == c->s) {
-        g_fake_reg.erase(it);
-        break;
-      }
-    delete c->s;
-  }
-  delete c;
-  return 0;
-}
-int fake_all_gather(const void* send, void* recv, size_t count, int dtype, void* comm, hipStream_t st) {
-  FakeComm* c = (FakeComm*)comm;
-  FakeShared* s = c->s;
-  const size_t bytes = count * fake_elem(dtype);
-  if (hipEventRecord(c->ready, st) != hipSuccess) return 1;
+// the communication API a new group (or id) uses; the returned table lives as long as
+// the process (a group keeps a copy)
+int comm_api(gs_comm_api* out) {
   {
-    std::lock_guard<std::mutex> lk(s->m);
-    s->src[c->rank] = send;
-    s->ev[c->rank] = c->ready;
-  }
-  fake_barrier(s);  // every rank's send buffer is staged (in its stream order)
-  for (int q = 0; q < s->n; ++q) {
-    if (hipStreamWaitEvent(st, s->ev[q], 0) != hipSuccess) return 1;
-    if (bytes && hipMemcpyAsync((char*)recv + (size_t)q * bytes, s->src[q], bytes, hipMemcpyDeviceToDevice, st) !=
-                     hipSuccess)
-      return 1;
-  }
-  if (hipEventRecord(c->done, st) != hipSuccess) return 1;
-  fake_barrier(s);  // (the ready events were captured by every stream's wait)
-  {
-    std::lock_guard<std::mutex> lk(s->m);
-    s->ev[c->rank] = c->done;
-  }
-  fake_barrier(s);
-  // the collective completes on this rank once every rank has read its send buffer
-  for (int q = 0; q < s->n; ++q)
-    if (q != c->rank && hipStreamWaitEvent(st, s->ev[q], 0) != hipSuccess) return 1;
-  fake_barrier(s);  // slots and events may be reused after this
-  return 0;
-}
-int fake_send(const void* buf, size_t count, int dtype, int peer, void* comm, hipStream_t st) {
-  FakeComm* c = (FakeComm*)comm;
-  FakeShared* s = c->s;
-  FakeShared::Msg msg{buf, count * fake_elem(dtype), nullptr, nullptr};
-  if (hipEventCreateWithFlags(&msg.ready, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&msg.copied, hipEventDisableTiming) != hipSuccess || hipEventRecord(msg.ready, st))
-    return 1;
-  c->spare.push_back(msg.ready);
-  c->spare.push_back(msg.copied);
-  std::unique_lock<std::mutex> lk(s->m);
-  s->box[{c->rank, peer}].push_back(&msg);
-  s->cv.notify_all();
-  s->cv.wait(lk, [&] { return msg.done; });  // the receiver has queued its copy
-  return hipStreamWaitEvent(st, msg.copied, 0) == hipSuccess ? 0 : 1;
-}
-int fake_recv(void* buf, size_t count, int dtype, int peer, void* comm, hipStream_t st) {
-  FakeComm* c = (FakeComm*)comm;
-  FakeShared* s = c->s;
-  std::unique_lock<std::mutex> lk(s->m);
-  auto& q = s->box[{peer, c->rank}];
-  s->cv.wait(lk, [&] { return !q.empty(); });
-  FakeShared::Msg* msg = q.front();
-  q.pop_front();
-  int r = 0;
-  if (msg->bytes != count * fake_elem(dtype)) r = 1;
-  if (!r && (hipStreamWaitEvent(st, msg->ready, 0) != hipSuccess ||
-             hipMemcpyAsync(buf, msg->buf, msg->bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-             hipEventRecord(msg->copied, st) != hipSuccess))
-    r = 1;
-  msg->done = true;
-  s->cv.notify_all();
-  return r;
-}
-int fake_count(void* comm, int* n) {
-  *n = ((FakeComm*)comm)->s->n;
-  return 0;
-}
-int fake_noop() { return 0; }
-const char* fake_error(int) { return "in-process comm emulation error"; }
-
-RcclApi make_fake_api() {
-  RcclApi a;
-  a.lib = (void*)&g_fake_reg;
-  a.getUniqueId = fake_unique_id;
-  a.allGather = fake_all_gather;
-  a.commDestroy = fake_destroy;
-  a.send = fake_send;
-  a.recv = fake_recv;
-  a.groupStart = fake_noop;
-  a.groupEnd = fake_noop;
-  a.getErrorString = fake_error;
-  a.commCount = fake_count;
-  a.initRankSym = (void*)&fake_init;
-  return a;
-}
-const RcclApi g_fake = make_fake_api();
-
-// the communication API a new group (or id) uses
-int comm_api(const RcclApi** api) {
-  const char* f = getenv("GS_GROUP_FAKE_COMM");
-  if (f && atoi(f) != 0) {
-    *api = &g_fake;
-    return GS_OK;
+    std::lock_guard<std::mutex> lk(g_api_mu);
+    if (g_user_api_on) {
+      *out = g_user_api;
+      return GS_OK;
+    }
   }
   if (int rc = rccl_load()) return rc;
-  *api = &g_rccl;
+  *out = g_rccl_api;
   return GS_OK;
 }
 
@@ -297,14 +179,14 @@ int comm_api(const RcclApi** api) {
 
 struct gs_group {
   gs_summary* h = nullptr;
-  const RcclApi* api = nullptr;  // RCCL, or the in-process emulation (GS_GROUP_FAKE_COMM=1, tests)
+  gs_comm_api api = {};          // RCCL, or the caller's backend (gs_group_set_comm_api)
   void* comm_c = nullptr;        // count collectives (stream xc)
   void* comm_d = nullptr;        // data collectives (stream xd) and the tree combine
   int nranks = 1, rank = 0;
   int width = 3;                 // int64 per exchange row: {a, b} for CC (16 B), {a, b, parity} signed
   bool exchange = false;         // false: tree-combine-only group
   bool prev_track = false;       // the summary's delta tracking before the group turned it on
-  bool self_apply = false;       // test knob (GS_GROUP_SELF_APPLY=1): also fold this rank's own rows back
+  bool self_apply = false;       // test knob (GS_TESTING_GROUP_SELF_APPLY): also fold this rank's own rows back
   uint64_t batch = 0, rows_cap = 0;
   // exchange b uses buffer set b % kLag (send, counts, headers, receive) and delta set b % kDeltaSets
   int64_t* send[kLag] = {};                             // [rows_cap * width]
@@ -321,13 +203,16 @@ struct gs_group {
   uint64_t own_edges = 0;  // own edges folded since create / finish (the ramp's position)
   uint64_t ramp_edges = 1ull << 22, ramp_batch = 1ull << 20;  // gs_group_set_ramp
   uint64_t done = 0;    // exchanges whose data half has been issued
-  int data_lag = 2;     // exchanges between an exchange's own fold and its data half (GS_GROUP_DATA_LAG: 1..kLag)
+  int data_lag = 2;     // exchanges between an exchange's own fold and its data half (GS_TESTING_GROUP_DATA_LAG: 1..kLag)
   uint64_t api_seen = 0;  // h->api_calls at the previous fold call (lane ordering)
   // statistics
   uint64_t exchanges = 0, rows_received = 0, live_received = 0;
-  bool hostprof = false;  // GS_GROUP_HOSTPROF=1: host seconds per phase, printed at destroy
-  bool no_lanes = false;  // GS_GROUP_LANES=0 (diagnostic): own folds on the handle stream
-  bool no_side = false;   // GS_GROUP_SIDE=0 (diagnostic): remote folds on the handle stream
+  // diagnostic builds (make variant VFLAGS=-DGS_GROUP_HOSTPROF=1 ...): host seconds per
+  // phase printed at destroy; own folds (GS_GROUP_NO_LANES) or remote folds
+  // (GS_GROUP_NO_SIDE) on the handle stream
+  bool hostprof = GS_GROUP_HOSTPROF != 0;
+  bool no_lanes = GS_GROUP_NO_LANES != 0;
+  bool no_side = GS_GROUP_NO_SIDE != 0;
   double hp[4] = {};      // own fold, stage + count collective, wait for counts, data collective + apply
   uint64_t hp_calls = 0;
   // per-phase timing (gs_group_set_phase_timing): HIP timing events around each phase's
@@ -429,8 +314,8 @@ int finish_data(gs_group* g, uint64_t e) {
   GS_HIP(hipStreamWaitEvent(g->xd, g->counted[k], 0));  // behind the stage (and the count collective)
   if (e >= (uint64_t)kLag) GS_HIP(hipStreamWaitEvent(g->xd, g->applied[k], 0));  // recv[k]: fold of e - kLag done
   hipEvent_t pa = ph_begin(g, g->xd);
-  const int r = g->api->allGather(g->send[k], g->recv[k], rows * g->width, kNcclInt64, g->comm_d, g->xd);
-  if (r != 0) return rccl_fail(g->api, "ncclAllGather(data)", r);
+  const int r = g->api.all_gather(g->send[k], g->recv[k], rows * g->width, kNcclInt64, g->comm_d, g->xd);
+  if (r != 0) return rccl_fail(&g->api, "ncclAllGather(data)", r);
   ph_end(g, 3, pa, g->xd);
   GS_HIP(hipEventRecord(g->gathered[k], g->xd));
   const bool use_side = side_ok(h) && !g->no_side;
@@ -465,10 +350,10 @@ int finish_data(gs_group* g, uint64_t e) {
 // so every replica missed those edges' vertices (tools/emu_check.py; DESIGN.md
 // section 5). Normal-priority streams, or the remote folds serialised on the handle
 // stream, were exact in every run.
-// GS_GROUP_HIPRIO=1 (diagnostic, tools/lostwork_probe.py) brings the highest priority back.
+// A diagnostic build with -DGS_GROUP_HIPRIO=1 (tools/lostwork_probe.py) brings the highest
+// priority back.
 hipError_t create_comm_stream(hipStream_t* st) {
-  const char* e = getenv("GS_GROUP_HIPRIO");
-  if (e && atoi(e) != 0) {
+  if (GS_GROUP_HIPRIO) {
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
       return hipStreamCreateWithPriority(st, hipStreamNonBlocking, hi);
@@ -480,13 +365,22 @@ hipError_t create_comm_stream(hipStream_t* st) {
 
 extern "C" {
 
+int gs_group_set_comm_api(const gs_comm_api* api) {
+  if (api && (!api->get_unique_id || !api->comm_init_rank || !api->comm_destroy || !api->all_gather))
+    return fail(GS_ERR_INVALID, "comm api needs get_unique_id, comm_init_rank, comm_destroy and all_gather");
+  std::lock_guard<std::mutex> lk(g_api_mu);
+  g_user_api_on = api != nullptr;
+  if (api) g_user_api = *api;
+  return GS_OK;
+}
+
 int gs_group_unique_id(void* id) {
   if (!id) return fail(GS_ERR_INVALID, "id is null");
-  const RcclApi* api = nullptr;
+  gs_comm_api api;
   if (int rc = comm_api(&api)) return rc;
   for (int i = 0; i < 2; ++i) {  // two communicators: counts and data
-    const int r = api->getUniqueId(static_cast<char*>(id) + i * kIdBytes);
-    if (r) return rccl_fail(api, "ncclGetUniqueId", r);
+    const int r = api.get_unique_id(static_cast<char*>(id) + i * kIdBytes);
+    if (r) return rccl_fail(&api, "ncclGetUniqueId", r);
   }
   return GS_OK;
 }
@@ -497,7 +391,7 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   if (!h) return fail(GS_ERR_INVALID, "null handle");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(GS_ERR_INVALID, "bad group shape");
   if (batch_edges > kMaxGroupBatch) return fail(GS_ERR_INVALID, "batch_edges above 2^26");
-  const RcclApi* api = nullptr;
+  gs_comm_api api;
   if (int rc = comm_api(&api)) return rc;
   DeviceGuard dg(h->device);
   gs_group* g = new gs_group();
@@ -508,11 +402,8 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
   g->width = h->kind == GS_KIND_SIGNED ? 3 : 2;
   g->exchange = batch_edges != 0;
   g->batch = batch_edges;
-  if (const char* m = getenv("GS_GROUP_SELF_APPLY")) g->self_apply = atoi(m) != 0;
-  if (const char* m = getenv("GS_GROUP_HOSTPROF")) g->hostprof = atoi(m) != 0;
-  if (const char* m = getenv("GS_GROUP_LANES")) g->no_lanes = atoi(m) == 0;
-  if (const char* m = getenv("GS_GROUP_SIDE")) g->no_side = atoi(m) == 0;
-  if (const char* m = getenv("GS_GROUP_DATA_LAG")) g->data_lag = std::min(kLag, std::max(1, atoi(m)));
+  g->self_apply = testing_value(GS_TESTING_GROUP_SELF_APPLY, 0) != 0;
+  g->data_lag = (int)std::min<int64_t>(kLag, std::max<int64_t>(1, testing_value(GS_TESTING_GROUP_DATA_LAG, 2)));
   auto bail = [&](int code) {
     gs_group_destroy(g);
     return code;
@@ -528,7 +419,7 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
     bool ok = hipHostMalloc(&g->hdr_host, kLag * (size_t)(nranks + 1) * 8,
                             hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
               hipHostGetDevicePointer(reinterpret_cast<void**>(&g->hdr_dev), g->hdr_host, 0) == hipSuccess &&
-              hipMalloc(&g->cnt, (kLag + kLag * (size_t)nranks) * 8) == hipSuccess &&
+              dmalloc(&g->cnt, (kLag + kLag * (size_t)nranks) * 8) == hipSuccess &&
               create_comm_stream(&g->xc) == hipSuccess && create_comm_stream(&g->xd) == hipSuccess &&
               hipStreamCreateWithFlags(&g->as, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&g->as_ev, hipEventDisableTiming) == hipSuccess;
@@ -538,8 +429,8 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
       ok = ok && hipEventCreateWithFlags(&g->staged[k], hipEventDisableTiming) == hipSuccess;
     }
     for (int k = 0; k < kLag && ok; ++k)
-      ok = hipMalloc(&g->send[k], g->rows_cap * g->width * 8) == hipSuccess &&
-           hipMalloc(&g->recv[k], (size_t)nranks * g->rows_cap * g->width * 8) == hipSuccess &&
+      ok = dmalloc(&g->send[k], g->rows_cap * g->width * 8) == hipSuccess &&
+           dmalloc(&g->recv[k], (size_t)nranks * g->rows_cap * g->width * 8) == hipSuccess &&
            hipEventCreateWithFlags(&g->counted[k], hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&g->gathered[k], hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&g->applied[k], hipEventDisableTiming) == hipSuccess;
@@ -550,16 +441,12 @@ int gs_group_create(gs_group_t* out, gs_handle h, const void* id, int nranks, in
     h->side_dirty = false;
     h->group_lanes = kGroupLanes;
   }
-  typedef int (*InitRank)(void**, int, Id128, int);
-  Id128 uid;
   if (g->exchange) {
-    memcpy(uid.b, id, kIdBytes);
-    const int r = ((InitRank)api->initRankSym)(&g->comm_c, nranks, uid, rank);
-    if (r != 0) return bail(rccl_fail(api, "ncclCommInitRank(counts)", r));
+    const int r = api.comm_init_rank(&g->comm_c, nranks, id, rank);
+    if (r != 0) return bail(rccl_fail(&api, "ncclCommInitRank(counts)", r));
   }
-  memcpy(uid.b, static_cast<const char*>(id) + kIdBytes, kIdBytes);
-  const int r = ((InitRank)api->initRankSym)(&g->comm_d, nranks, uid, rank);
-  if (r != 0) return bail(rccl_fail(api, "ncclCommInitRank(data)", r));
+  const int r = api.comm_init_rank(&g->comm_d, nranks, static_cast<const char*>(id) + kIdBytes, rank);
+  if (r != 0) return bail(rccl_fail(&api, "ncclCommInitRank(data)", r));
   *out = g;
   return GS_OK;
 }
@@ -650,8 +537,8 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
   if (int rc = stage_delta(h, g->send[k], g->rows_cap, g->width, g->cnt_send(k), h->kind == GS_KIND_SIGNED, g->xc, d))
     return rc;
   GS_HIP(hipEventRecord(g->staged[d], g->xc));
-  const int r = g->api->allGather(g->cnt_send(k), g->cnt_recv(k), 1, kNcclInt64, g->comm_c, g->xc);
-  if (r != 0) return rccl_fail(g->api, "ncclAllGather(counts)", r);
+  const int r = g->api.all_gather(g->cnt_send(k), g->cnt_recv(k), 1, kNcclInt64, g->comm_c, g->xc);
+  if (r != 0) return rccl_fail(&g->api, "ncclAllGather(counts)", r);
   gs::launch_headers(g->cnt_recv(k), g->nranks, g->hdr_dev + (size_t)k * (g->nranks + 1), (long long)b, g->xc);
   GS_HIP(hipGetLastError());
   ph_end(g, 2, pc, g->xc);
@@ -722,12 +609,12 @@ int tree_send(gs_group* g, int peer, int64_t* hdr) {
   int64_t *v = nullptr, *l = nullptr;
   uint8_t* p = nullptr;
   auto release = [&] {
-    (void)hipFree(v);
-    (void)hipFree(l);
-    (void)hipFree(p);
+    (void)dfree(v);
+    (void)dfree(l);
+    (void)dfree(p);
   };
-  if (hipMalloc(&v, (nv + 1) * 8) != hipSuccess || hipMalloc(&l, (nv + 1) * 8) != hipSuccess ||
-      hipMalloc(&p, nv + 1) != hipSuccess) {
+  if (dmalloc(&v, (nv + 1) * 8) != hipSuccess || dmalloc(&l, (nv + 1) * 8) != hipSuccess ||
+      dmalloc(&p, nv + 1) != hipSuccess) {
     release();
     return fail(GS_ERR_HIP, "tree combine: out of device memory");
   }
@@ -742,16 +629,16 @@ int tree_send(gs_group* g, int peer, int64_t* hdr) {
   if (!rc && hipMemcpyAsync(hdr, hv, 16, hipMemcpyHostToDevice, h->stream) != hipSuccess)
     rc = fail(GS_ERR_HIP, "tree combine: header copy failed");
   if (!rc) {
-    const int r = g->api->send(hdr, 2, kNcclInt64, peer, g->comm_d, h->stream);
-    if (r) rc = rccl_fail(g->api, "ncclSend", r);
+    const int r = g->api.send(hdr, 2, kNcclInt64, peer, g->comm_d, h->stream);
+    if (r) rc = rccl_fail(&g->api, "ncclSend", r);
   }
   if (!rc && got) {
-    g->api->groupStart();
-    int r = g->api->send(v, got, kNcclInt64, peer, g->comm_d, h->stream);
-    if (!r) r = g->api->send(l, got, kNcclInt64, peer, g->comm_d, h->stream);
-    if (!r) r = g->api->send(p, got, kNcclUint8, peer, g->comm_d, h->stream);
-    const int e = g->api->groupEnd();
-    if (r || e) rc = rccl_fail(g->api, "ncclSend", r ? r : e);
+    g->api.group_start();
+    int r = g->api.send(v, got, kNcclInt64, peer, g->comm_d, h->stream);
+    if (!r) r = g->api.send(l, got, kNcclInt64, peer, g->comm_d, h->stream);
+    if (!r) r = g->api.send(p, got, kNcclUint8, peer, g->comm_d, h->stream);
+    const int e = g->api.group_end();
+    if (r || e) rc = rccl_fail(&g->api, "ncclSend", r ? r : e);
   }
   if (hipStreamSynchronize(h->stream) != hipSuccess && !rc) rc = fail(GS_ERR_HIP, "tree combine: sync failed");
   release();  // the sends have completed
@@ -761,8 +648,8 @@ int tree_send(gs_group* g, int peer, int64_t* hdr) {
 // one tree edge, receiving side: fold the peer's exported summary into this one
 int tree_recv(gs_group* g, int peer, int64_t* hdr) {
   gs_summary* h = g->h;
-  int r = g->api->recv(hdr, 2, kNcclInt64, peer, g->comm_d, h->stream);
-  if (r) return rccl_fail(g->api, "ncclRecv", r);
+  int r = g->api.recv(hdr, 2, kNcclInt64, peer, g->comm_d, h->stream);
+  if (r) return rccl_fail(&g->api, "ncclRecv", r);
   int64_t hv[2] = {0, 0};
   GS_HIP(hipMemcpyAsync(hv, hdr, 16, hipMemcpyDeviceToHost, h->stream));
   GS_HIP(hipStreamSynchronize(h->stream));
@@ -770,21 +657,21 @@ int tree_recv(gs_group* g, int peer, int64_t* hdr) {
   int64_t *v = nullptr, *l = nullptr;
   uint8_t* p = nullptr;
   auto release = [&] {
-    (void)hipFree(v);
-    (void)hipFree(l);
-    (void)hipFree(p);
+    (void)dfree(v);
+    (void)dfree(l);
+    (void)dfree(p);
   };
   int rc = GS_OK;
-  if (got && (hipMalloc(&v, got * 8) != hipSuccess || hipMalloc(&l, got * 8) != hipSuccess ||
-              hipMalloc(&p, got) != hipSuccess))
+  if (got && (dmalloc(&v, got * 8) != hipSuccess || dmalloc(&l, got * 8) != hipSuccess ||
+              dmalloc(&p, got) != hipSuccess))
     rc = fail(GS_ERR_HIP, "tree combine: out of device memory");
   if (!rc && got) {
-    g->api->groupStart();
-    r = g->api->recv(v, got, kNcclInt64, peer, g->comm_d, h->stream);
-    if (!r) r = g->api->recv(l, got, kNcclInt64, peer, g->comm_d, h->stream);
-    if (!r) r = g->api->recv(p, got, kNcclUint8, peer, g->comm_d, h->stream);
-    const int e = g->api->groupEnd();
-    if (r || e) rc = rccl_fail(g->api, "ncclRecv", r ? r : e);
+    g->api.group_start();
+    r = g->api.recv(v, got, kNcclInt64, peer, g->comm_d, h->stream);
+    if (!r) r = g->api.recv(l, got, kNcclInt64, peer, g->comm_d, h->stream);
+    if (!r) r = g->api.recv(p, got, kNcclUint8, peer, g->comm_d, h->stream);
+    const int e = g->api.group_end();
+    if (r || e) rc = rccl_fail(&g->api, "ncclRecv", r ? r : e);
   }
   if (!rc) {
     const bool track = h->track;
@@ -803,13 +690,13 @@ extern "C" {
 
 int gs_group_tree_combine(gs_group_t g) {
   if (!g) return fail(GS_ERR_INVALID, "null group");
-  if (!g->api || !g->api->send || !g->api->recv || !g->api->groupStart || !g->api->groupEnd)
+  if (!g->api.send || !g->api.recv || !g->api.group_start || !g->api.group_end)
     return fail(GS_ERR_HIP, "RCCL is missing ncclSend/ncclRecv/ncclGroupStart/ncclGroupEnd");
   gs_summary* h = g->h;
   DeviceGuard dg(h->device);
   if (int rc = join_lanes(h)) return rc;
   int64_t* hdr = nullptr;  // device {count, failed}
-  GS_HIP(hipMalloc(&hdr, 16));
+  GS_HIP(dmalloc(&hdr, 16));
   int rc = GS_OK;
   // binomial tree (SummaryTreeReduce.enhance pairs partitions by f0/2, :107): at level l
   // rank r with r mod 2^(l+1) == 2^l sends to r - 2^l and leaves the tree
@@ -821,7 +708,7 @@ int gs_group_tree_combine(gs_group_t g) {
     }
     if (pos == 0 && g->rank + step < g->nranks) rc = tree_recv(g, g->rank + step, hdr);
   }
-  (void)hipFree(hdr);
+  (void)dfree(hdr);
   return rc;
 }
 
@@ -840,15 +727,15 @@ int gs_group_stats(gs_group_t g, uint64_t* exchanges, uint64_t* records_sent, ui
 
 int gs_group_comm_ranks(gs_group_t g, int* count_comm, int* data_comm) {
   if (!g) return fail(GS_ERR_INVALID, "null group");
-  if (!g->api->commCount) return fail(GS_ERR_HIP, "RCCL is missing ncclCommCount");
+  if (!g->api.comm_count) return fail(GS_ERR_HIP, "the comm backend has no comm_count");
   int c = 0, d = 0;
   if (g->comm_c) {
-    const int r = g->api->commCount(g->comm_c, &c);
-    if (r) return rccl_fail(g->api, "ncclCommCount(counts)", r);
+    const int r = g->api.comm_count(g->comm_c, &c);
+    if (r) return rccl_fail(&g->api, "ncclCommCount(counts)", r);
   }
   if (g->comm_d) {
-    const int r = g->api->commCount(g->comm_d, &d);
-    if (r) return rccl_fail(g->api, "ncclCommCount(data)", r);
+    const int r = g->api.comm_count(g->comm_d, &d);
+    if (r) return rccl_fail(&g->api, "ncclCommCount(data)", r);
   }
   if (count_comm) *count_comm = c;
   if (data_comm) *data_comm = d;
@@ -891,8 +778,8 @@ int gs_group_destroy(gs_group_t g) {
   (void)hipStreamSynchronize(g->h->stream);
   if (g->xc) (void)hipStreamSynchronize(g->xc);
   if (g->xd) (void)hipStreamSynchronize(g->xd);
-  if (g->comm_c && g->api && g->api->commDestroy) g->api->commDestroy(g->comm_c);
-  if (g->comm_d && g->api && g->api->commDestroy) g->api->commDestroy(g->comm_d);
+  if (g->comm_c && g->api.comm_destroy) g->api.comm_destroy(g->comm_c);
+  if (g->comm_d && g->api.comm_destroy) g->api.comm_destroy(g->comm_d);
   if (g->as) {
     (void)hipStreamSynchronize(g->as);
     if (g->h->side == g->as) {
@@ -914,12 +801,12 @@ int gs_group_destroy(gs_group_t g) {
   for (int k = 0; k < kLag; ++k) {
     for (hipEvent_t e : {g->counted[k], g->gathered[k], g->applied[k]})
       if (e) (void)hipEventDestroy(e);
-    (void)hipFree(g->send[k]);
-    (void)hipFree(g->recv[k]);
+    (void)dfree(g->send[k]);
+    (void)dfree(g->recv[k]);
   }
   ph_drain(g);
   for (hipEvent_t e : g->ph_pool) (void)hipEventDestroy(e);
-  (void)hipFree(g->cnt);
+  (void)dfree(g->cnt);
   if (g->xc) (void)hipStreamDestroy(g->xc);
   if (g->xd) (void)hipStreamDestroy(g->xd);
   if (g->hdr_host) (void)hipHostFree(g->hdr_host);

@@ -787,7 +787,10 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
   if (tiles > s.tiles_cap) return -1;
   const bool aligned = ((uintptr_t)text & 15u) == 0;
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
-  const bool st_zero = s.st_zero;
+  // Block 0 of k_parse_finish publishes the result before the other blocks have cleared
+  // every status word; on the same stream the next parse starts after that whole kernel,
+  // on another one it could overlap the late clears: fill again there.
+  const bool st_zero = s.st_zero && s.zero_stream == st;
   s.st_zero = false;  // until this call has queued a k_parse_finish
   if (fused) {  // aggregate words (s.tile_cnt) and prefix words (s.tile_pre) zero, then one pass
     // the previous one-pass parse's k_parse_finish left them zero; else one fill (the
@@ -799,10 +802,9 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
     unsigned long long* agg = reinterpret_cast<unsigned long long*>(s.tile_cnt);
     unsigned long long* pre = reinterpret_cast<unsigned long long*>(s.tile_pre);
     if (kev0 && hipEventRecord(kev0, st) != hipSuccess) return -1;
-    // GS_PARSE_LB_TIMEOUT_US (test hook, read per call): how long a look-back waits before it
-    // counts the '\n' before its tile itself (default ~50 ms; 0: at once)
-    const char* lbe = getenv("GS_PARSE_LB_TIMEOUT_US");
-    const unsigned long long lb_timeout = lbe ? 100ull * strtoull(lbe, nullptr, 10) : 5000000ull;
+    // how long a look-back waits before it counts the '\n' before its tile itself (~50 ms;
+    // tests shorten it with GS_TESTING_PARSE_LB_TIMEOUT_US, 0: at once)
+    const unsigned long long lb_timeout = 100ull * (unsigned long long)gsi::testing_value(GS_TESTING_PARSE_LB_TIMEOUT_US, 50000);
     hipLaunchKernelGGL(k_parse_fused, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, src, dst,
                        (uint64_t)cap, s.bad, aligned, agg, pre, lb_timeout);
     if (kev1 && hipEventRecord(kev1, st) != hipSuccess) return -1;
@@ -837,6 +839,7 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
                        agg, pre, tiles, s.tiles_cap, t, (uint64_t)len, s.bad, s.res, host_res, seq);
     if (hipGetLastError() != hipSuccess) return -1;
     s.st_zero = true;
+    s.zero_stream = st;
     return 0;
   }
   hipLaunchKernelGGL(k_count_lines, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, s.tile_cnt, aligned,
@@ -914,14 +917,15 @@ struct ParseCache {
 thread_local ParseCache t_parse;
 
 // Free the cache's device scratch, mapped result record and timing events (on the device
-// they belong to). Safe between parses: gs_parse_edges_device returns only after the parse's
-// last kernel has written the mapped result, so nothing in flight still reads the scratch.
+// they belong to). gs_parse_edges_device returns once the parse's result is published,
+// but the other blocks of k_parse_finish may still be clearing status words:
+// the device is synchronised before the scratch goes.
 int parse_cache_free(ParseCache& c) {
   if (c.device < 0) return 0;
   int cur = -1;
   if (hipGetDevice(&cur) != hipSuccess) return -1;
   if (cur != c.device && hipSetDevice(c.device) != hipSuccess) return -1;
-  int rc = 0;
+  int rc = hipDeviceSynchronize() == hipSuccess ? 0 : -1;
   if (c.mem && hipFree(c.mem) != hipSuccess) rc = -1;
   if (c.host && hipHostFree(c.host) != hipSuccess) rc = -1;
   for (hipEvent_t e : c.kev)
@@ -947,7 +951,8 @@ int parse_cache_ready(hipStream_t st, size_t len) {
   }
   if (c.len_cap < len || !c.mem) {
     if (c.mem) {
-      if (hipStreamSynchronize(st) != hipSuccess) return -1;  // the old scratch's last user
+      // the old scratch's last user (k_parse_finish of the previous parse, on any stream)
+      if (hipDeviceSynchronize() != hipSuccess) return -1;
       (void)hipFree(c.mem);
       c.mem = nullptr;
     }
@@ -972,10 +977,7 @@ extern "C" int gs_parse_edges_device(void* stream, const char* text, size_t len,
   if (parse_cache_ready(st, len)) return GS_ERR_HIP;
   ParseCache& c = t_parse;
   const unsigned long long seq = ++c.seq;
-  static const bool one_pass = [] {  // experiment knob: GS_PARSE_MODE=0 = count pass + scan + parse pass
-    const char* e = getenv("GS_PARSE_MODE");
-    return !(e && atoi(e) == 0);
-  }();
+  constexpr bool one_pass = true;  // (the count pass + scan + parse pass serves gs_fold_text's chunks)
   const bool prof = c.prof && one_pass;
   const int rc = gs::parse_text_enqueue(st, text, len, sep, src, dst, cap, c.s, c.host_dev, seq, one_pass,
                                         prof ? c.kev[0] : nullptr, prof ? c.kev[1] : nullptr);

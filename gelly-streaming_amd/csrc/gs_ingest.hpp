@@ -4,6 +4,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "gs_testing.h"
+
+namespace gsi {
+int64_t testing_value(int knob, int64_t product);  // include/gs_testing.h (gs_capi.cpp)
+}
+
 namespace gs {
 
 struct ParseScratch {
@@ -16,6 +22,7 @@ struct ParseScratch {
   uint64_t tiles_cap = 0;
   bool bad_ready = false;  // `bad` holds ~0 (k_parse_result resets it after every parse)
   bool st_zero = false;    // the one-pass status words are zero (the last one-pass parse's k_parse_finish cleared them)
+  hipStream_t zero_stream = nullptr;  // the stream that k_parse_finish ran on (st_zero holds only there)
 };
 
 // Device bytes needed to parse up to max_len bytes of text.

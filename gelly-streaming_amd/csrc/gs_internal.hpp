@@ -10,10 +10,25 @@
 #include "gs_ingest.hpp"
 #include "gs_kernels.hpp"
 #include "gs_summary.h"
+#include "gs_testing.h"
 
 namespace gsi {
 
 int fail(int code, const std::string& msg);
+// gs_testing.h: a test knob's value, or `product` while the knob is unset
+int64_t testing_value(int knob, int64_t product);
+
+// Device memory of summaries and groups: hipMalloc / hipFree plus the per-device byte
+// count gs_hbm_bytes reports (tables that grow inside a fold or combine included).
+hipError_t dmalloc(void** p, size_t bytes);
+template <typename T>
+inline hipError_t dmalloc(T** p, size_t bytes) {
+  return dmalloc(reinterpret_cast<void**>(p), bytes);
+}
+hipError_t dfree(void* p);
+constexpr int kMaxDevices = 64;
+uint64_t create_capacity(uint64_t capacity_hint);
+uint64_t create_bytes(uint64_t cap);
 
 #define GS_HIP(call)                                                                                  \
   do {                                                                                                \
@@ -119,8 +134,9 @@ struct gs_summary {
   uint64_t chg_ocap = 0;
   bool chg_scan_all = false;  // the next emission emits every vertex (after a rebuild)
   // staging for host folds
-  int64_t* d_stage = nullptr;  // [2][2][kStageChunk]
-  uint8_t* d_wstage = nullptr; // [2][kStageChunk]
+  int64_t* d_stage = nullptr;  // [2][2][d_stage_chunk] (allocated by the first host fold)
+  uint8_t* d_wstage = nullptr; // [2][d_stage_chunk]
+  uint64_t d_stage_chunk = 0;  // edges per staging buffer
   int64_t* h_stage = nullptr;  // pinned, same shape: large host folds (allocated on first use)
   uint8_t* h_wstage = nullptr;
   hipEvent_t stage_ev[2] = {nullptr, nullptr};  // after each buffer's copies

@@ -568,17 +568,20 @@ __device__ __forceinline__ void fold_block(const Table& t, const Delta& D, const
 template <bool SIGNED>
 __global__ __launch_bounds__(kFoldBS) void k_window_server(Table t, Delta D, ServerBox* box, ServerBcast* bc,
                                                            unsigned long long* done, unsigned long long seq0,
-                                                           unsigned long long idle_ticks,
-                                                           unsigned long long late_ticks) {
+                                                           unsigned long long idle_ticks) {
   __shared__ int64_t lrec[kFoldBS * 3];
   __shared__ uint32_t lcnt, lnv;
   __shared__ unsigned long long w[8];
-  // test hook (GS_SERVER_LATE_US): the last workgroup starts late, as one the dispatcher
-  // held back behind another stream's kernels would (the exit paths' late-block test)
-  if (late_ticks && blockIdx.x == gridDim.x - 1) {
+#ifdef GS_TEST_LATE_WORKGROUP
+  // test build only (make testhooks -> lib_testhooks/): the last workgroup starts
+  // GS_TEST_LATE_WORKGROUP us late, as one the dispatcher held back behind another
+  // stream's kernels would (the exit paths' late-block test). The product kernel has no
+  // such branch.
+  if (blockIdx.x == gridDim.x - 1) {
     const unsigned long long t0 = wall_clock64();
-    while (wall_clock64() - t0 < late_ticks) __builtin_amdgcn_s_sleep(8);
+    while (wall_clock64() - t0 < 100ull * GS_TEST_LATE_WORKGROUP) __builtin_amdgcn_s_sleep(8);
   }
+#endif
   D.lrec = lrec;
   D.lcnt = &lcnt;
   D.lnv = &lnv;
@@ -1178,13 +1181,13 @@ void launch_fold(bool sign, bool track, const Table& t, const Delta& D, const Fo
 
 void launch_window_server(bool sign, const Table& t, const Delta& D, ServerBox* box, ServerBcast* bc,
                           unsigned long long* done, unsigned long long seq0, unsigned long long idle_ticks,
-                          unsigned long long late_ticks, hipStream_t st) {
+                          hipStream_t st) {
   if (sign)
     hipLaunchKernelGGL(k_window_server<true>, dim3(kServerBlocks), dim3(kFoldBS), 0, st, t, D, box, bc, done, seq0,
-                       idle_ticks, late_ticks);
+                       idle_ticks);
   else
     hipLaunchKernelGGL(k_window_server<false>, dim3(kServerBlocks), dim3(kFoldBS), 0, st, t, D, box, bc, done, seq0,
-                       idle_ticks, late_ticks);
+                       idle_ticks);
 }
 
 int window_server_resident_blocks(bool sign, int device) {

@@ -65,7 +65,7 @@ struct alignas(64) ServerBcast {    // device memory: block 0 -> the other block
 };
 void launch_window_server(bool sign, const Table& t, const Delta& D, ServerBox* box, ServerBcast* bc,
                           unsigned long long* done, unsigned long long seq0, unsigned long long idle_ticks,
-                          unsigned long long late_ticks, hipStream_t st);
+                          hipStream_t st);
 // Workgroups of k_window_server that can be resident on the device at once (occupancy x
 // CUs): a window completes only when all kServerBlocks of them run together.
 int window_server_resident_blocks(bool sign, int device);

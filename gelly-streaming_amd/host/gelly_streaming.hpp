@@ -29,6 +29,7 @@
 #include <functional>
 #include <limits>
 #include <map>
+#include <set>
 #include <memory>
 #include <optional>
 #include <stdexcept>
@@ -92,16 +93,20 @@ struct MapFunction {
 // after the all-window reduce; creating a GPU summary each time would cost a table
 // allocation and initialisation per window. Released handles are reset (O(touched
 // vertices) on the device, asynchronous) and handed to the next summary of the same
-// kind and device whose table size class fits (up to kClassSlack classes larger).
+// kind and device: one whose table size class fits (up to kClassSlack classes larger),
+// else any larger pooled one -- reusing HBM that is already held costs nothing against
+// the budget, a create does (the per-window copy of the EMPTY initial value
+// asks for the smallest class, and grown pooled tables must still serve it).
 //
-// HBM budget (the Java HandlePool's model): the pool accounts the HBM of
-// every handle it holds or has handed out (table slots x 16 B + the vertex list's 4 B per
-// slot). Summaries a Flink job drops without release() -- per-emission copies with object
-// reuse off, window partials cleared after a fire -- return their handles only when the JVM
-// finalizes them; set_budget's `collect` hook stands for System.gc() +
-// System.runFinalization(), which acquire() runs before a create would pass the budget;
-// if that is not enough, pooled handles of other sizes are destroyed first. The total then
-// stays within the budget unless live summaries need more (one table over at a time).
+// HBM budget (the Java HandlePool's model). The budget is
+// checked against the library's own count of the device memory every live summary holds
+// (gs_hbm_bytes: tables, vertex lists, staging, scratch), so a table that grew inside a
+// fold or combine while handed out -- the Merger's running summary -- counts at once, not
+// at its release. A create of gs_create_bytes(hint) that would pass the budget first runs
+// set_budget's `collect` hook (System.gc() + System.runFinalization(): summaries a Flink
+// job dropped without release() come back through their finalizers), then destroys pooled
+// handles until it fits. The total then stays within the budget plus the table being
+// created, unless live summaries alone need more.
 // --------------------------------------------------------------------------
 class HandlePool {
  public:
@@ -118,107 +123,102 @@ class HandlePool {
     while (s < want) s <<= 1;
     return s;
   }
-  static uint64_t bytes_of_slots(uint64_t slots) { return slots * 20; }
   static int size_class(uint64_t slots) {
     int c = 0;
     while ((2ull << c) <= slots) ++c;
     return c;
   }
-  // budget of the handed-out handles' HBM (0: none) and the finalization hook it runs
+  // the library's count of device memory held by live summaries on `device`
+  static uint64_t device_bytes(int device) {
+    uint64_t b = 0;
+    gs_check(gs_hbm_bytes(device, &b));
+    return b;
+  }
+  // budget of the device's summary HBM (0: none) and the finalization hook it runs
   void set_budget(uint64_t bytes, std::function<void()> collect) {
     budget_ = bytes;
     collect_ = std::move(collect);
   }
   gs_handle acquire(int kind, int device, uint64_t capacity_hint) {
-    const uint64_t slots = slots_for(capacity_hint), need = bytes_of_slots(slots);
-    if (gs_handle h = take(kind, device, size_class(slots))) return h;
-    if (budget_ && total_ + need > budget_) {
+    const uint64_t slots = slots_for(capacity_hint);
+    if (gs_handle h = take(kind, device, size_class(slots), false)) return h;
+    uint64_t need = 0;
+    gs_check(gs_create_bytes(kind, capacity_hint, &need));
+    if (budget_ && device_bytes(device) + need > budget_) {
       if (collect_) {
         ++collections_;
         collect_();  // the dropped summaries' destructors release into this pool
-        if (gs_handle h = take(kind, device, size_class(slots))) return h;
+        if (gs_handle h = take(kind, device, size_class(slots), true)) return h;
       }
-      // still over: pooled handles of other sizes make room before a table is created
-      for (auto it = free_.begin(); it != free_.end() && total_ + need > budget_; ++it)
-        while (!it->second.empty() && total_ + need > budget_) {
+      // still over: pooled handles (largest first) make room before a table is created
+      for (auto it = free_.rbegin(); it != free_.rend() && device_bytes(device) + need > budget_; ++it)
+        while (!it->second.empty() && device_bytes(device) + need > budget_) {
           gs_handle f = it->second.back();
           it->second.pop_back();
           --nfree_;
-          total_ -= bytes_[f];
-          bytes_.erase(f);
+          live_.erase(f);
           gs_destroy(f);
         }
     }
     gs_handle h = nullptr;
     gs_check(gs_create(&h, device, kind, capacity_hint));
     ++created_;
-    bytes_[h] = need;
-    total_ += need;
-    peak_total_ = std::max(peak_total_, total_);
-    add_outstanding(need);
+    live_.insert(h);
+    note(device);
     return h;
   }
   void release(gs_handle h, int kind, int device) {
-    auto it = bytes_.find(h);
-    if (it != bytes_.end()) {
-      outstanding_ -= it->second;
-      total_ -= it->second;
-    }
     uint64_t slots = 0;
     // the value AND the configuration (tracking, pipelining, profiling) of a fresh handle;
-    // a table keeps a grown capacity across resets: account and pool it by its real size
+    // a table keeps a grown capacity across resets: pool it by its real size
     if (gs_reset_config(h) != GS_OK || gs_table_capacity(h, &slots) != GS_OK) {  // a broken handle is not pooled
-      bytes_.erase(h);
+      live_.erase(h);
       gs_destroy(h);
       return;
     }
+    note(device);
     if (nfree_ < kMaxFree) {
-      bytes_[h] = bytes_of_slots(slots);
-      total_ += bytes_[h];
-      peak_total_ = std::max(peak_total_, total_);
       free_[{kind, device, size_class(slots)}].push_back(h);
       ++nfree_;
     } else {
-      bytes_.erase(h);
+      live_.erase(h);
       gs_destroy(h);
     }
   }
   size_t created() const { return created_; }
   size_t reused() const { return reused_; }
+  size_t reused_larger() const { return reused_larger_; }
   size_t collections() const { return collections_; }
-  uint64_t outstanding_bytes() const { return outstanding_; }
-  uint64_t peak_outstanding_bytes() const { return peak_; }
-  uint64_t total_bytes() const { return total_; }  // every handle the pool accounts: handed out + pooled
-  uint64_t peak_total_bytes() const { return peak_total_; }
-  size_t live_handles() const { return bytes_.size(); }  // handed out + pooled
+  uint64_t peak_total_bytes() const { return peak_total_; }  // gs_hbm_bytes seen at acquires / releases
+  size_t live_handles() const { return live_.size(); }       // handed out + pooled
   ~HandlePool() {
     for (auto& kv : free_)
       for (gs_handle h : kv.second) gs_destroy(h);
   }
 
  private:
-  gs_handle take(int kind, int device, int cls) {
+  // a pooled handle of class cls .. cls + kClassSlack, or (any_larger) of any larger class
+  gs_handle take(int kind, int device, int cls, bool any_larger) {
     for (auto it = free_.lower_bound({kind, device, cls}); it != free_.end(); ++it) {
       const auto& k = it->first;
-      if (std::get<0>(k) != kind || std::get<1>(k) != device || std::get<2>(k) > cls + kClassSlack) break;
+      if (std::get<0>(k) != kind || std::get<1>(k) != device) break;
+      const bool near = std::get<2>(k) <= cls + kClassSlack;
+      if (!near && !any_larger) break;
       if (it->second.empty()) continue;
       gs_handle h = it->second.back();
       it->second.pop_back();
       --nfree_;
       ++reused_;
-      add_outstanding(bytes_[h]);
+      if (!near) ++reused_larger_;
       return h;
     }
     return nullptr;
   }
-  void add_outstanding(uint64_t b) {
-    outstanding_ += b;
-    peak_ = std::max(peak_, outstanding_);
-  }
+  void note(int device) { peak_total_ = std::max(peak_total_, device_bytes(device)); }
   std::map<std::tuple<int, int, int>, std::vector<gs_handle>> free_;
-  std::map<gs_handle, uint64_t> bytes_;
-  size_t nfree_ = 0, created_ = 0, reused_ = 0, collections_ = 0;
-  uint64_t budget_ = 0, outstanding_ = 0, peak_ = 0, total_ = 0, peak_total_ = 0;
+  std::set<gs_handle> live_;
+  size_t nfree_ = 0, created_ = 0, reused_ = 0, reused_larger_ = 0, collections_ = 0;
+  uint64_t budget_ = 0, peak_total_ = 0;
   std::function<void()> collect_;
 };
 

@@ -22,6 +22,16 @@
 
 #include "gs_summary.h"
 
+/* Collective order (round 6). Every collective the group issues -- count all-gathers on
+ * communicator C, data all-gathers and the tree's send/recv on communicator D -- is
+ * issued by the calling thread in a program order that depends only on the sequence of
+ * gs_group_* calls (exchange numbers and the fixed data lag), never on timing (when a
+ * count lands, which stream is idle). So every rank issues the same interleaving of
+ * C and D operations, the condition RCCL places on several communicators of one
+ * device. The test emulation (tests/cpp/gs_fake_comm.cpp) asserts it: each collective
+ * carries the rank's running hash of the (communicator, call number) sequence so far,
+ * and a collective whose ranks disagree fails instead of hanging. */
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -29,6 +39,33 @@ extern "C" {
 typedef struct gs_group* gs_group_t;
 
 #define GS_GROUP_ID_BYTES 256 /* two RCCL unique ids: count and data communicators */
+
+/* Collectives backend. By default a group loads RCCL (librccl.so.1) on first use and
+ * calls it through this table. A caller may install its own implementation of the
+ * same calls before gs_group_unique_id / gs_group_create -- e.g. one over MPI, or the
+ * in-process emulation the tests use (N ranks as N threads on one GPU,
+ * tests/cpp/gs_fake_comm.cpp, which also checks that every rank issues its collectives
+ * in one order). dtype values are rccl.h's (ncclUint8 = 1, ncclInt64 = 4); `stream`
+ * is a hipStream_t; `id` is one 128-byte unique id; 0 = success. */
+typedef struct gs_comm_api {
+  int (*get_unique_id)(void* id);
+  int (*comm_init_rank)(void** comm, int nranks, const void* id, int rank);
+  int (*comm_destroy)(void* comm);
+  int (*comm_count)(void* comm, int* nranks);
+  int (*all_gather)(const void* send, void* recv, size_t count, int dtype, void* comm, void* stream);
+  /* ncclAllToAllv: counts and displacements in elements, host arrays of nranks */
+  int (*all_to_allv)(const void* send, const size_t* send_counts, const size_t* send_displs, void* recv,
+                     const size_t* recv_counts, const size_t* recv_displs, int dtype, void* comm, void* stream);
+  int (*send)(const void* buf, size_t count, int dtype, int peer, void* comm, void* stream);
+  int (*recv)(void* buf, size_t count, int dtype, int peer, void* comm, void* stream);
+  int (*group_start)(void);
+  int (*group_end)(void);
+  const char* (*error_string)(int code);
+} gs_comm_api;
+
+/* Process-wide: ids and groups created afterwards use `api` (the table is copied);
+ * NULL restores RCCL. Groups already created keep the backend they were created with. */
+int gs_group_set_comm_api(const gs_comm_api* api);
 
 /* Create the communicator id on one rank and hand its GS_GROUP_ID_BYTES bytes to
  * every rank (any host channel: MPI, TCP, torch.distributed, a file). */

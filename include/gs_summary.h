@@ -331,6 +331,16 @@ int gs_kernel_stats(gs_handle h, int id, uint64_t* launches, double* total_ms);
 int gs_table_capacity(gs_handle h, uint64_t* slots);
 int gs_capacity_stats(gs_handle h, uint64_t* waits, uint64_t* syncs, double* wait_ms);
 
+/* HBM accounting for a handle pool's budget (the Java HandlePool,
+ * S/SummaryAggregation.java:107-119 and S/SummaryBulkAggregation.java:79-83 drop partials
+ * and copies without a release). gs_hbm_bytes: bytes of device memory held right now by
+ * every live summary and group of this process on `device` -- tables, vertex lists, delta
+ * lists, staging and scratch -- counted by the library's allocator, so a table that grew
+ * inside a fold or combine while handed out is included at once. gs_create_bytes: the bytes
+ * gs_create(kind, capacity_hint) allocates. Neither synchronises. */
+int gs_hbm_bytes(int device, uint64_t* bytes);
+int gs_create_bytes(int kind, uint64_t capacity_hint, uint64_t* bytes);
+
 /* Device counters (synchronises): out[0] vertices, [1] bipartiteness failed,
  * [2] table-overflow error, [3] list overflow (bit 0 delta list, bit 1 vertex
  * list), [4] records staged,

@@ -193,8 +193,8 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 		return handle;
 	}
 
-	/** Back to the pool (the combine dropped this summary, GpuBipartitenessCheck); it reads
-	 *  as a fresh initial value afterwards. */
+	/** Size the handle taken at the first use for about `vertices` vertices (a copy: its
+	 *  source's count); no effect once a handle is held. */
 	@Override
 	public void sizeFor(long vertices) {
 		if (handle == 0) {
@@ -202,6 +202,8 @@ public class GpuCandidates extends Candidates implements GpuSummary {
 		}
 	}
 
+	/** Back to the pool (the combine dropped this summary, GpuBipartitenessCheck); it reads
+	 *  as a fresh initial value afterwards. */
 	@Override
 	public void release() {
 		n = 0;

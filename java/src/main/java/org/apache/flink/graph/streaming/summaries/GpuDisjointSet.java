@@ -145,8 +145,8 @@ public class GpuDisjointSet extends DisjointSet<Long> implements GpuSummary {
 		return handle;
 	}
 
-	/** Back to the pool: the combine dropped this summary (GpuConnectedComponents), or it
-	 *  is no longer needed. It reads as a fresh, empty initial value afterwards. */
+	/** Size the handle taken at the first use for about `vertices` vertices (a copy: its
+	 *  source's count); no effect once a handle is held. */
 	@Override
 	public void sizeFor(long vertices) {
 		if (handle == 0) {
@@ -154,6 +154,8 @@ public class GpuDisjointSet extends DisjointSet<Long> implements GpuSummary {
 		}
 	}
 
+	/** Back to the pool: the combine dropped this summary (GpuConnectedComponents), or it
+	 *  is no longer needed. It reads as a fresh, empty initial value afterwards. */
 	@Override
 	public void release() {
 		n = 0;

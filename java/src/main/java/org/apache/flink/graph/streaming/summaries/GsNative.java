@@ -37,7 +37,9 @@ final class GsNative {
 	// ---- queries (gs_find, gs_num_vertices, gs_export_labels, gs_bip_status, gs_export_colouring)
 	static native Long find(long h, long v);
 	static native long numVertices(long h);
-	static native long tableCapacity(long h);  // gs_table_capacity: slots (the pool's HBM accounting)
+	static native long tableCapacity(long h);  // gs_table_capacity: slots (the pool's size classes)
+	static native long hbmBytes(int device);  // gs_hbm_bytes: device memory of every live summary (the pool's budget)
+	static native long createBytes(int kind, long capacityHint);  // gs_create_bytes: what a create allocates
 	static native int exportLabels(long h, long[] v, long[] label);
 	static native boolean bipStatus(long h);
 	static native int exportColouring(long h, long[] comp, long[] v, byte[] sign);

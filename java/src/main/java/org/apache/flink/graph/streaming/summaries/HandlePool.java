@@ -6,26 +6,31 @@
  * and initialise a table per window; a released handle is instead restored with
  * gs_reset_config (O(touched vertices) on the device, asynchronous; tracking,
  * pipelining and profiling back to a fresh handle's settings) and handed to the next
- * summary of the same kind.
+ * summary of the same kind: one of the size class it asks for (up to CLASS_SLACK classes
+ * larger), else any larger pooled one -- reusing HBM already held costs nothing against
+ * the budget, a create does (ADVICE r5: copies of the EMPTY initial value ask for the
+ * smallest class, and grown pooled tables must still serve them).
  *
- * HBM lifetime (VERDICT r4 item 3). A summary's Java object is a few bytes while its table
- * is megabytes of HBM. Summaries the operators drop without release() -- Flink's per-emission
- * TypeSerializer.copy of the Merger's output when object reuse is off, and the window
- * partials Flink clears after a fire (S/SummaryAggregation.java:107-119,
- * S/SummaryBulkAggregation.java:79-83) -- return their handles only through finalize(),
- * and the JVM heap never feels the pressure that would run it. So the pool accounts the HBM
- * of every handle it holds or has handed out (gs_table_capacity x the slot and vertex-list
- * bytes) and, before a create would take that past gs.hbmBudgetBytes, runs System.gc() and
- * System.runFinalization() (outside its lock: the finalizers release into it), looks in
- * the free lists again, and destroys pooled handles of other sizes to make room. Free
- * handles are kept by table size class, and a summary asks for the size it needs (a copy:
- * its source's vertex count), so a copy of a small partial does not pin a 2^20-vertex table. The C++ host mirror models this pool and a 1,000-window
- * run with Flink's copies and dropped partials (tests/cpp/test_handle_budget.cpp).
+ * HBM budget (VERDICT r4 item 3, r5 item 2). A summary's Java object is a few bytes while
+ * its table is megabytes of HBM. Summaries the operators drop without release() -- Flink's
+ * per-emission TypeSerializer.copy of the Merger's output when object reuse is off, and the
+ * window partials Flink clears after a fire (S/SummaryAggregation.java:107-119,
+ * S/SummaryBulkAggregation.java:79-83) -- return their handles only through finalize(), and
+ * the JVM heap never feels the pressure that would run it. The budget is checked against
+ * the library's own count of the device memory every live summary holds
+ * (gs_hbm_bytes: tables, vertex lists, staging), so a table that grew inside a fold or
+ * combine while handed out -- the Merger's running summary -- counts at once. A create of
+ * gs_create_bytes(hint) is reserved under the pool's lock (concurrent task slots cannot
+ * all pass the check); if it would pass gs.hbmBudgetBytes, System.gc() and
+ * System.runFinalization() run outside the lock (the finalizers release into the pool; a
+ * pass that returned nothing blocks the next for gs.gcBackoffMs), then pooled handles are
+ * destroyed, largest first, to make room. Device work (gs_reset_config, gs_destroy) never
+ * runs under the lock. The C++ host mirror models this pool and a 1,000-window run with
+ * Flink's copies and dropped partials (tests/cpp/test_handle_budget.cpp).
  */
 package org.apache.flink.graph.streaming.summaries;
 
 import java.util.ArrayDeque;
-import java.util.HashMap;
 import java.util.Map;
 import java.util.TreeMap;
 
@@ -35,11 +40,13 @@ final class HandlePool {
 	/** Expected vertices of a summary whose size is not known (the operator's initial value);
 	 *  the table grows past it on its own. */
 	static final long CAPACITY_HINT = Long.getLong("gs.capacityHint", 1L << 20);
-	/** HBM the pool's handles (handed out + pooled) may hold before a create makes the JVM
-	 *  finalize dropped summaries. */
+	/** Device memory the process's summaries may hold (gs_hbm_bytes) before a create makes the
+	 *  JVM finalize dropped summaries and the pool give up pooled handles. */
 	static final long BUDGET_BYTES = Long.getLong("gs.hbmBudgetBytes", 32L << 30);
+	/** After a forced collection that returned no handle, the next one waits this long. */
+	static final long GC_BACKOFF_MS = Long.getLong("gs.gcBackoffMs", 100L);
 	static final int MAX_FREE = 64;
-	/** Size classes a request may take from above its own (a bigger pooled table serves it). */
+	/** Size classes a request takes from above its own before it considers any larger one. */
 	static final int CLASS_SLACK = 2;
 
 	static final HandlePool CC = new HandlePool(GsNative.KIND_CC);
@@ -47,11 +54,11 @@ final class HandlePool {
 
 	private final int kind;
 	private final TreeMap<Integer, ArrayDeque<Long>> free = new TreeMap<>();  // size class -> handles
-	private final Map<Long, Long> bytesOf = new HashMap<>();  // every live handle -> its HBM
 	private int nfree;
-	private long outstandingBytes;  // HBM of the handles handed out
-	private long totalBytes;        // HBM of every live handle: handed out + pooled (what the budget bounds)
-	private long created, reused, collections;
+	private long reserved;  // bytes of creates between their budget check and gs_create's allocation
+	private long created, reused, reusedLarger, collections;
+	private long lastCollectNanos;
+	private boolean lastCollectReturned = true;
 
 	private HandlePool(int kind) {
 		this.kind = kind;
@@ -63,11 +70,6 @@ final class HandlePool {
 		return Long.highestOneBit(want - 1) << 1;
 	}
 
-	/** HBM of a table of `slots` 16-byte slots plus its vertex list (4 B per slot). */
-	static long bytesOfSlots(long slots) {
-		return slots * 20L;
-	}
-
 	static int sizeClass(long slots) {
 		return 63 - Long.numberOfLeadingZeros(Math.max(slots, 1L));
 	}
@@ -76,101 +78,143 @@ final class HandlePool {
 		return acquire(CAPACITY_HINT);
 	}
 
-	/** A handle for a summary of about `hint` vertices: a pooled one of that size class (or up to
-	 *  CLASS_SLACK classes larger), else a new one -- after a finalization pass (and pooled
-	 *  handles of other sizes destroyed) if it would take the pool past the HBM budget. */
+	/** A handle for a summary of about `hint` vertices: a pooled one (its size class, else any
+	 *  larger), else a new one -- after a finalization pass and pooled handles destroyed if the
+	 *  create would take the device's summary HBM past the budget. */
 	long acquire(long hint) {
-		final long slots = slotsFor(hint);
-		Long h = take(sizeClass(slots));
+		final int cls = sizeClass(slotsFor(hint));
+		Long h = take(cls, false);
 		if (h != null) {
 			return h;
 		}
-		final long need = bytesOfSlots(slots);
-		if (total() + need > BUDGET_BYTES) {
-			System.gc();
-			System.runFinalization();
-			synchronized (this) {
-				collections++;
-			}
-			h = take(sizeClass(slots));
+		final long need = GsNative.createBytes(kind, hint);
+		if (!reserve(need, false)) {
+			collect();
+			h = take(cls, true);
 			if (h != null) {
 				return h;
 			}
-			evictFor(need);  // pooled handles of other sizes make room
+			evictFor(need);
+			reserve(need, true);  // live summaries alone may need more than the budget: create anyway
 		}
-		long nh = GsNative.create(DEVICE, kind, hint);
-		synchronized (this) {
-			created++;
-			bytesOf.put(nh, need);
-			outstandingBytes += need;
-			totalBytes += need;
-		}
-		return nh;
-	}
-
-	/** Destroy pooled handles until a table of `need` bytes fits the budget (or none is left). */
-	private synchronized void evictFor(long need) {
-		for (ArrayDeque<Long> q : free.values()) {
-			while (!q.isEmpty() && totalBytes + need > BUDGET_BYTES) {
-				long f = q.poll();
-				nfree--;
-				totalBytes -= bytesOf.remove(f);
-				GsNative.destroy(f);
+		try {
+			long nh = GsNative.create(DEVICE, kind, hint);
+			synchronized (this) {
+				created++;
+			}
+			return nh;
+		} finally {
+			synchronized (this) {
+				reserved -= need;
 			}
 		}
 	}
 
-	private synchronized Long take(int cls) {
+	/** Reserve `need` bytes if the device's summary HBM plus the reservations leaves room (or
+	 *  unconditionally with `force`). gs_hbm_bytes is an atomic read, no device work. */
+	private synchronized boolean reserve(long need, boolean force) {
+		if (!force && GsNative.hbmBytes(DEVICE) + reserved + need > BUDGET_BYTES) {
+			return false;
+		}
+		reserved += need;
+		return true;
+	}
+
+	/** System.gc() + System.runFinalization(), outside the lock (the finalizers release into this
+	 *  pool); skipped while the previous pass returned nothing and gs.gcBackoffMs has not passed. */
+	private void collect() {
+		final long now = System.nanoTime();
+		final int before;
+		synchronized (this) {
+			if (!lastCollectReturned && now - lastCollectNanos < GC_BACKOFF_MS * 1_000_000L) {
+				return;
+			}
+			lastCollectNanos = now;
+			collections++;
+			before = nfree;
+		}
+		System.gc();
+		System.runFinalization();
+		synchronized (this) {
+			lastCollectReturned = nfree > before;
+		}
+	}
+
+	/** Destroy pooled handles, largest first, until a create of `need` bytes fits the budget (or
+	 *  none is left). Each handle leaves the free list under the lock and is destroyed outside it. */
+	private void evictFor(long need) {
+		while (true) {
+			Long f;
+			synchronized (this) {
+				if (GsNative.hbmBytes(DEVICE) + reserved + need <= BUDGET_BYTES) {
+					return;
+				}
+				f = null;
+				for (ArrayDeque<Long> q : free.descendingMap().values()) {
+					f = q.poll();
+					if (f != null) {
+						nfree--;
+						break;
+					}
+				}
+			}
+			if (f == null) {
+				return;
+			}
+			GsNative.destroy(f);
+		}
+	}
+
+	/** A pooled handle of class cls .. cls + CLASS_SLACK, or (anyLarger) of any larger class. */
+	private synchronized Long take(int cls, boolean anyLarger) {
 		for (Map.Entry<Integer, ArrayDeque<Long>> e : free.tailMap(cls, true).entrySet()) {
-			if (e.getKey() > cls + CLASS_SLACK) {
+			final boolean near = e.getKey() <= cls + CLASS_SLACK;
+			if (!near && !anyLarger) {
 				break;
 			}
 			Long h = e.getValue().poll();
 			if (h != null) {
 				nfree--;
 				reused++;
-				outstandingBytes += bytesOf.get(h);
+				if (!near) {
+					reusedLarger++;
+				}
 				return h;
 			}
 		}
 		return null;
 	}
 
-	synchronized void release(long h) {
+	/** Back to the pool: reset to a fresh handle's value and configuration (device work, outside
+	 *  the lock), then pooled by its real table size (tables keep a grown capacity across resets). */
+	void release(long h) {
 		if (h == 0) {
 			return;
 		}
-		Long b = bytesOf.get(h);
-		if (b != null) {
-			outstandingBytes -= b;
-			totalBytes -= b;
-		}
 		long slots;
 		try {
-			GsNative.resetConfig(h);  // value and configuration of a fresh handle
-			slots = GsNative.tableCapacity(h);  // tables keep a grown capacity across resets
+			GsNative.resetConfig(h);
+			slots = GsNative.tableCapacity(h);
 		} catch (RuntimeException broken) {
-			bytesOf.remove(h);
 			GsNative.destroy(h);  // a broken handle is not pooled
 			return;
 		}
-		if (nfree < MAX_FREE) {
-			bytesOf.put(h, bytesOfSlots(slots));
-			totalBytes += bytesOfSlots(slots);
-			free.computeIfAbsent(sizeClass(slots), k -> new ArrayDeque<>()).push(h);
-			nfree++;
-		} else {
-			bytesOf.remove(h);
+		boolean pooled;
+		synchronized (this) {
+			pooled = nfree < MAX_FREE;
+			if (pooled) {
+				free.computeIfAbsent(sizeClass(slots), k -> new ArrayDeque<>()).push(h);
+				nfree++;
+			}
+		}
+		if (!pooled) {
 			GsNative.destroy(h);
 		}
 	}
 
-	synchronized long outstanding() {
-		return outstandingBytes;
-	}
-
-	synchronized long total() {
-		return totalBytes;
+	/** The device memory of every live summary of this process (gs_hbm_bytes). */
+	static long deviceBytes() {
+		return GsNative.hbmBytes(DEVICE);
 	}
 
 	synchronized long created() {
@@ -179,6 +223,11 @@ final class HandlePool {
 
 	synchronized long reused() {
 		return reused;
+	}
+
+	/** Reuses served by a pooled table more than CLASS_SLACK classes above the request. */
+	synchronized long reusedLarger() {
+		return reusedLarger;
 	}
 
 	/** Finalization passes the budget forced. */

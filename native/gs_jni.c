@@ -168,6 +168,26 @@ JNIEXPORT jlong JNICALL FN(numVertices)(JNIEnv* env, jclass c, jlong h) {
   return (jlong)n;
 }
 
+JNIEXPORT jlong JNICALL FN(hbmBytes)(JNIEnv* env, jclass c, jint device) {
+  (void)c;
+  uint64_t b = 0;
+  if (gs_hbm_bytes(device, &b) != GS_OK) {
+    throw_gs(env);
+    return 0;
+  }
+  return (jlong)b;
+}
+
+JNIEXPORT jlong JNICALL FN(createBytes)(JNIEnv* env, jclass c, jint kind, jlong hint) {
+  (void)c;
+  uint64_t b = 0;
+  if (gs_create_bytes(kind, (uint64_t)hint, &b) != GS_OK) {
+    throw_gs(env);
+    return 0;
+  }
+  return (jlong)b;
+}
+
 JNIEXPORT jlong JNICALL FN(tableCapacity)(JNIEnv* env, jclass c, jlong h) {
   (void)c;
   uint64_t slots = 0;

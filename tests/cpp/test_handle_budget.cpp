@@ -12,7 +12,12 @@
 // Java pool's System.gc() + System.runFinalization()). The run must keep the HBM the pool
 // accounts (handles handed out + pooled) within the budget (plus one table) and end with the
 // oracle's summary.
-// Usage: test_handle_budget <edges.bin: int64 src,dst pairs> <window edges> <budget bytes> <out.bin>
+// Round 6: the budget is checked against the library's count of device
+// memory (gs_hbm_bytes), so the Merger's running summary, which grows while handed out,
+// counts at once. With a small default hint (the "grow" case) that summary grows 16x and
+// more during the run. The window partial is a copy of the (empty) initial value
+// (ADVICE r5): the pool must keep reusing grown pooled tables for it instead of creating.
+// Usage: test_handle_budget <edges.bin: int64 src,dst pairs> <window edges> <budget bytes> <out.bin> [default hint]
 // out.bin: int64 n, then n rows of int64 {v, label}. Prints one JSON line of pool statistics.
 #include <cstdio>
 #include <cstdlib>
@@ -37,8 +42,14 @@ static DisjointSetRef copy_of(DisjointSet& src, uint64_t default_hint) {
   return c;
 }
 
+static uint64_t slots_of(DisjointSet& s) {
+  uint64_t n = 0;
+  gs_check(gs_table_capacity(s.handle(), &n));
+  return n;
+}
+
 int main(int argc, char** argv) {
-  if (argc != 5) die("usage: test_handle_budget <edges.bin> <window> <budget bytes> <out.bin>");
+  if (argc != 5 && argc != 6) die("usage: test_handle_budget <edges.bin> <window> <budget bytes> <out.bin> [hint]");
   FILE* f = std::fopen(argv[1], "rb");
   if (!f) die("cannot open edges");
   std::vector<int64_t> e;
@@ -48,7 +59,7 @@ int main(int argc, char** argv) {
   std::fclose(f);
   const size_t n = e.size() / 2, window = std::strtoull(argv[2], nullptr, 0);
   const uint64_t budget = std::strtoull(argv[3], nullptr, 0);
-  const uint64_t default_hint = 1 << 16;  // the operator's initial value (the pool's default hint)
+  const uint64_t default_hint = argc == 6 ? std::strtoull(argv[5], nullptr, 0) : 1 << 16;  // the pool's default hint
   std::vector<std::shared_ptr<GpuSummary>> finalizer_queue;  // dropped, not yet finalized
   size_t finalized = 0, max_queue = 0;
   HandlePool& pool = HandlePool::instance();
@@ -56,15 +67,19 @@ int main(int argc, char** argv) {
     finalized += finalizer_queue.size();
     finalizer_queue.clear();
   });
-  uint64_t worst = 0;  // handed-out bytes seen after any acquire that had to create
+  uint64_t worst = 0;     // gs_hbm_bytes after each window's emission
+  uint64_t worst_over = 0;  // max over windows of (gs_hbm_bytes - budget - the largest table created in it)
+  uint64_t summary_slots0 = 0, summary_slots1 = 0;
   try {
     ConnectedComponents<NullValue>::CombineCC combine;
     const auto initialVal = std::make_shared<DisjointSet>(0, default_hint);  // never used itself
     DisjointSetRef summary = std::make_shared<DisjointSet>(0, default_hint);  // Merger.summary
+    summary_slots0 = slots_of(*summary);
     size_t windows = 0;
     for (size_t i = 0; i < n; i += window, ++windows) {
-      // the window's fold state: a copy of the initial value (empty: the default hint)
-      auto partial = std::make_shared<DisjointSet>(0, default_hint);
+      const size_t created0 = pool.created();
+      // the window's fold state: Flink's copy of the initial value (empty: sized 2 x 0)
+      DisjointSetRef partial = copy_of(*initialVal, default_hint);
       const size_t j = std::min(n, i + window);
       for (size_t k = i; k < j; ++k) partial->union_(e[2 * k], e[2 * k + 1]);  // UpdateCC.foldEdges
       // Merger.flatMap: summary = reduce(partial, summary); the input the combine dropped is
@@ -78,9 +93,20 @@ int main(int argc, char** argv) {
       if (out->size() != summary->size()) die("the emitted copy differs from the summary");
       finalizer_queue.push_back(out);
       max_queue = std::max(max_queue, finalizer_queue.size());
-      worst = std::max(worst, pool.outstanding_bytes());
+      const uint64_t now = HandlePool::device_bytes(0);
+      worst = std::max(worst, now);
+      // one table over the budget at most: the largest create of this window (the copies are
+      // sized from the summary; a created partial from the initial value)
+      uint64_t table = 0;
+      if (pool.created() != created0) {
+        uint64_t a = 0, b = 0;
+        gs_check(gs_create_bytes(GS_KIND_CC, 2 * summary->size(), &a));
+        gs_check(gs_create_bytes(GS_KIND_CC, default_hint, &b));
+        table = std::max(a, b);
+      }
+      if (now > budget + table) worst_over = std::max(worst_over, now - budget - table);
     }
-    (void)initialVal;
+    summary_slots1 = slots_of(*summary);
     const auto rows = summary->rows();
     std::vector<int64_t> o = {(int64_t)rows.size()};
     for (const auto& r : rows) {
@@ -91,13 +117,14 @@ int main(int argc, char** argv) {
     if (!g || std::fwrite(o.data(), 8, o.size(), g) != o.size()) die("cannot write output");
     std::fclose(g);
     std::printf(
-        "{\"windows\": %zu, \"budget\": %llu, \"peak_outstanding\": %llu, \"peak_total\": %llu, "
-        "\"worst_after_window\": %llu, "
-        "\"created\": %zu, \"reused\": %zu, \"collections\": %zu, \"finalized\": %zu, \"max_queue\": %zu, "
-        "\"live_handles\": %zu}\n",
-        windows, (unsigned long long)budget, (unsigned long long)pool.peak_outstanding_bytes(),
-        (unsigned long long)pool.peak_total_bytes(), (unsigned long long)worst, pool.created(), pool.reused(),
-        pool.collections(), finalized, max_queue, pool.live_handles());
+        "{\"windows\": %zu, \"budget\": %llu, \"peak_total\": %llu, \"worst_after_window\": %llu, "
+        "\"worst_over_budget_plus_table\": %llu, \"summary_slots_start\": %llu, \"summary_slots_end\": %llu, "
+        "\"created\": %zu, \"reused\": %zu, \"reused_larger\": %zu, \"collections\": %zu, \"finalized\": %zu, "
+        "\"max_queue\": %zu, \"live_handles\": %zu}\n",
+        windows, (unsigned long long)budget, (unsigned long long)pool.peak_total_bytes(), (unsigned long long)worst,
+        (unsigned long long)worst_over, (unsigned long long)summary_slots0, (unsigned long long)summary_slots1,
+        pool.created(), pool.reused(), pool.reused_larger(), pool.collections(), finalized, max_queue,
+        pool.live_handles());
     finalizer_queue.clear();
     summary.reset();
   } catch (const std::exception& x) {

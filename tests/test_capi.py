@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared_symbols():
     names = set()
-    for h in ("gs_summary.h", "gs_gen.h", "gs_group.h", "gs_ingest.h"):
+    for h in ("gs_summary.h", "gs_gen.h", "gs_group.h", "gs_ingest.h", "gs_testing.h"):
         with open(os.path.join(ROOT, "include", h)) as f:
             text = f.read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
@@ -53,3 +53,27 @@ def test_library_is_gfx950_code_object(gs):
     with open(gs.LIB_PATH, "rb") as f:
         blob = f.read()
     assert b"gfx950" in blob
+
+
+def test_product_library_reads_no_environment_knob(gs):
+    """experiment and test switches are gs_testing.h knobs or build
+    variants, not environment variables of the shipped library."""
+    with open(gs.LIB_PATH, "rb") as f:
+        blob = f.read()
+    found = sorted(set(re.findall(rb"GS_[A-Z0-9_]{4,}", blob)))
+    assert not found, found
+
+
+def test_testing_knobs_roundtrip(gs):
+    assert gs.testing_get("server_idle_us") == 2000 and gs.testing_get("group_data_lag") == 2
+    with gs.testing(server_idle_us=100, group_data_lag=1):
+        assert gs.testing_get("server_idle_us") == 100 and gs.testing_get("group_data_lag") == 1
+    assert gs.testing_get("server_idle_us") == 2000 and gs.testing_get("group_data_lag") == 2
+    assert gs.lib().gs_testing_set(99, 1) == gs.GS_ERR_INVALID
+
+
+def test_comm_emulation_library_loads(gs):
+    F = gs.fake_comm()
+    assert F.gs_fake_comm_api()
+    assert gs.lib().gs_group_set_comm_api(F.gs_fake_comm_api()) == gs.GS_OK
+    assert gs.lib().gs_group_set_comm_api(None) == gs.GS_OK

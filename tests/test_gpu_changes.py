@@ -71,11 +71,11 @@ def test_changes_rmat16_windows(gs, oracle_mod, window):
     _run_windows(gs, oracle_mod, s, d, bounds, 1 << 16)  # no table rebuild: exact emissions
 
 
-def test_changes_scan_path_for_large_relabels(gs, oracle_mod, monkeypatch):
+def test_changes_scan_path_for_large_relabels(gs, oracle_mod, knobs):
     # walk limit 8: every hooked component with more members is emitted by the scan
     # (a superset with unchanged members of the absorbing component); the sink state
     # must still equal the oracle after every window
-    monkeypatch.setenv("GS_CHANGES_WALK_MAX", "8")
+    knobs(changes_walk_max=8)
     s, d = oracle_mod.rmat_edges(0x5EED0017, 12, 0, 1 << 14, True)
     bounds = list(range(0, len(s), 1 << 11)) + [len(s)]
     _run_windows(gs, oracle_mod, s, d, bounds, 1 << 12, exact=False)

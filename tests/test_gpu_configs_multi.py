@@ -2,7 +2,7 @@
 timed entry point over the whole stream.
 
 RCCL refuses two ranks on one GPU, so the 8 ranks are threads of this process driving
-8 replicas through the library's in-process communicator (GS_GROUP_FAKE_COMM=1: host
+8 replicas through the library's in-process communicator (gs_group_set_comm_api + tests/cpp/gs_fake_comm.cpp: host
 barriers + device copies ordered by events); everything else -- tracked own folds on
 the lanes, staging, 16-/24-byte rows, count and data collectives, the exchange-layout
 fold of the other ranks' rows on the side stream -- is the code bench.py runs at N = 8.
@@ -72,9 +72,8 @@ def _labels_of(summ, keys, chunk=1 << 26):
     return out, found
 
 
-def test_config3_eight_ranks_full_stream(gs, monkeypatch):
+def test_config3_eight_ranks_full_stream(gs, fake_comm):
     import torch
-    monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
     scale, E, world = 26, 1 << 30, 8
     per, B, ramp, ramp_b = E // world, 1 << 22, 1 << 22, 1 << 20
     src = torch.empty(E, dtype=torch.int64, device="cuda")
@@ -141,9 +140,8 @@ def _mid_shard_injection(oracle_mod, gs, rank, per, logside, seed):
 
 
 @pytest.mark.parametrize("variant", ["bench_injections", "mid_shard", "clean"])
-def test_config4_eight_ranks_full_stream(gs, oracle_mod, monkeypatch, variant):
+def test_config4_eight_ranks_full_stream(gs, oracle_mod, fake_comm, variant):
     import torch
-    monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
     logside, E, world, B, seed = 19, 1 << 24, 8, 1 << 20, 0x5EED0B1B
     per = E // world
     if variant == "bench_injections":

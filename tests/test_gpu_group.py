@@ -9,13 +9,13 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("self_apply,batch", [(0, 1 << 13), (1, 1 << 13), (1, 1 << 12)])
-def test_group_single_rank_matches_oracle(gs, oracle_mod, monkeypatch, self_apply, batch):
+def test_group_single_rank_matches_oracle(gs, oracle_mod, knobs, self_apply, batch):
     """self_apply: the rank also folds its own gathered rows (16-B CC rows, exchange
     layout from the gathered count words, applied one exchange late on the side
     stream) -- the remote-fold path, exercised at one rank; folding a delta twice is
     idempotent, so any mis-parsed row would show in the labels."""
     import torch
-    monkeypatch.setenv("GS_GROUP_SELF_APPLY", str(self_apply))
+    knobs(group_self_apply=self_apply)
     n, B = 1 << 17, batch
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -37,10 +37,10 @@ def test_group_single_rank_matches_oracle(gs, oracle_mod, monkeypatch, self_appl
     assert np.array_equal(v, ov) and np.array_equal(lab, olab)
 
 
-def test_group_fold_batches_native_loop(gs, oracle_mod, monkeypatch):
+def test_group_fold_batches_native_loop(gs, oracle_mod, knobs):
     """gs_group_fold_batches_device == the per-batch calls (ragged last batch)."""
     import torch
-    monkeypatch.setenv("GS_GROUP_SELF_APPLY", "1")
+    knobs(group_self_apply=1)
     n, B = (1 << 16) + 777, 1 << 12
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -58,12 +58,12 @@ def test_group_fold_batches_native_loop(gs, oracle_mod, monkeypatch):
 
 
 @pytest.mark.parametrize("inject", [(), (1 << 15,)])
-def test_group_signed_rows_self_apply(gs, oracle_mod, monkeypatch, inject):
+def test_group_signed_rows_self_apply(gs, oracle_mod, knobs, inject):
     """Signed summary in a group: 24-B rows {a, b, parity}; the rank folds its own
     gathered rows back (GS_GROUP_SELF_APPLY) -- verdict and colouring must equal
     the truth."""
     import torch
-    monkeypatch.setenv("GS_GROUP_SELF_APPLY", "1")
+    knobs(group_self_apply=1)
     n, B = 1 << 16, 1 << 12
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -136,13 +136,13 @@ def test_tree_only_group_single_rank(gs, oracle_mod):
     assert np.array_equal(v, ov) and np.array_equal(lab, olab)
 
 
-def test_group_ramp_exchange_cadence(gs, oracle_mod, monkeypatch):
+def test_group_ramp_exchange_cadence(gs, oracle_mod, knobs):
     """gs_group_set_ramp: the first `ramp` edges after create / finish are exchanged
     every `ramp_batch` edges, the rest every `batch` (a self-applying rank folds its
     own rows back, so every exchange's rows are parsed); the ramp restarts after
     finish, bad arguments are refused."""
     import torch
-    monkeypatch.setenv("GS_GROUP_SELF_APPLY", "1")
+    knobs(group_self_apply=1)
     n, B = 1 << 17, 1 << 14
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")

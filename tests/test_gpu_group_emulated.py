@@ -1,6 +1,6 @@
 """GPU: the native group (include/gs_group.h) at 2-4 ranks on the box's one GPU.
 RCCL refuses two ranks on one device, so the group's communicator is replaced by
-the library's in-process emulation (GS_GROUP_FAKE_COMM=1: host barriers + device
+the library's in-process emulation (gs_group_set_comm_api + tests/cpp/gs_fake_comm.cpp: host barriers + device
 copies ordered by events) and every rank is a thread of this process driving its
 own summary. Everything else -- staging, 16-/24-byte rows, count and data
 collectives, the exchange-layout fold of real remote rows on the side stream, the
@@ -34,9 +34,8 @@ def _run_ranks(world, body):
 
 
 @pytest.mark.parametrize("world,batch", [(2, 1 << 12), (3, 1 << 11), (4, 1 << 12)])
-def test_delta_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, world, batch):
+def test_delta_exchange_emulated_ranks(gs, oracle_mod, fake_comm, world, batch):
     import torch
-    monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
     scale, n, B = 14, 1 << 18, batch
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -78,12 +77,11 @@ _BENCH_SHAPE = {}
 
 
 @pytest.mark.parametrize("world,log_batch", [(2, 20), (4, 20), (2, 22)])
-def test_bench_exchange_shape_emulated_ranks(gs, oracle_mod, monkeypatch, world, log_batch):
+def test_bench_exchange_shape_emulated_ranks(gs, oracle_mod, fake_comm, world, log_batch):
     """bench.py's N-GPU shape at reduced scale: RMAT-20 (2^24 edges), 2^20-edge
     per-rank micro-batches and 2^22, a capacity hint of twice
     the vertex scale. Every replica equals the oracle."""
     import torch
-    monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
     scale, n, B = 20, 1 << 24, 1 << log_batch
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -112,15 +110,14 @@ def test_bench_exchange_shape_emulated_ranks(gs, oracle_mod, monkeypatch, world,
 
 @pytest.mark.parametrize("lag", [1, 2, 3])
 @pytest.mark.parametrize("kind", ["cc", "signed"])
-def test_data_lag_emulated_ranks(gs, oracle_mod, monkeypatch, lag, kind):
-    """GS_GROUP_DATA_LAG: the data half of exchange b - L is issued
+def test_data_lag_emulated_ranks(gs, oracle_mod, fake_comm, knobs, lag, kind):
+    """The data lag (GS_TESTING_GROUP_DATA_LAG): the data half of exchange b - L is issued
     after own fold b is queued (L = 1, 2; the default is 2) or, at L = 3, before it.
     Every schedule leaves every replica equal to the oracle (CC labels; signed colouring
     and verdict, with a mid-shard odd cycle in the signed case), with small batches so
     that many exchanges are in flight."""
     import torch
-    monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
-    monkeypatch.setenv("GS_GROUP_DATA_LAG", str(lag))
+    knobs(group_data_lag=lag)
     world, B = 4, 1 << 11
     n = 1 << 17
     src = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -155,14 +152,13 @@ def test_data_lag_emulated_ranks(gs, oracle_mod, monkeypatch, lag, kind):
 
 
 @pytest.mark.parametrize("inject", [(), (1 << 15,), (5 << 12,), (2 << 15) + 777])
-def test_signed_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, inject):
+def test_signed_exchange_emulated_ranks(gs, oracle_mod, fake_comm, inject):
     """inject (1 << 15) is the first edge of rank 1's shard (its endpoints are new
     there, so it travels as a hook record); (5 << 12) and (2 << 15) + 777 sit in the
     MIDDLE of a shard, where the injected same-side edge joins vertices that rank
     already connected: the odd cycle is found without any record, and only the count
     word's failure bit tells the other replicas."""
     import torch
-    monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
     world, n, B = 3, 3 << 15, 1 << 12
     if not isinstance(inject, tuple):
         inject = (inject,)
@@ -192,9 +188,8 @@ def test_signed_exchange_emulated_ranks(gs, oracle_mod, monkeypatch, inject):
 
 
 @pytest.mark.parametrize("kind,world", [("cc", 3), ("cc", 4), ("signed", 3)])
-def test_tree_combine_emulated_ranks(gs, oracle_mod, monkeypatch, kind, world):
+def test_tree_combine_emulated_ranks(gs, oracle_mod, fake_comm, kind, world):
     import torch
-    monkeypatch.setenv("GS_GROUP_FAKE_COMM", "1")
     n = 1 << 16
     src = torch.empty(n, dtype=torch.int64, device="cuda")
     dst = torch.empty(n, dtype=torch.int64, device="cuda")

@@ -255,14 +255,14 @@ def test_parse_release_frees_the_cache_and_parses_again(gs, oracle_mod):
 
 
 @pytest.mark.parametrize("offset", [0, 1, 7])
-def test_parse_lookback_fallback_counts_directly(gs, oracle_mod, offset, monkeypatch):
+def test_parse_lookback_fallback_counts_directly(gs, oracle_mod, offset, knobs):
     """a tile whose predecessors have not published within the look-back's timeout
     counts the '\\n' before it itself (16-byte loads across the wave, an unaligned head and
     tail byte by byte). GS_PARSE_LB_TIMEOUT_US=0 makes every tile that finds an unpublished
     predecessor take that path; the result is still the oracle's, for aligned and unaligned
     texts of many tiles."""
     rng = np.random.default_rng(17 + offset)
-    monkeypatch.setenv("GS_PARSE_LB_TIMEOUT_US", "0")
+    knobs(parse_lb_timeout_us=0)
     for nlines in (3000, 120000):
         text = _random_text(rng, nlines, 0)
         es, ed, en, eb = oracle_mod.parse_edges(text, 0)

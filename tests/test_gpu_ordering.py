@@ -72,13 +72,13 @@ def test_fold_device_after_event(gs, oracle_mod):
     assert np.array_equal(v, ov) and np.array_equal(lab, olab)
 
 
-def test_group_lanes_follow_handle_stream_every_call(gs, oracle_mod, monkeypatch):
+def test_group_lanes_follow_handle_stream_every_call(gs, oracle_mod, knobs):
     """a group's own-fold lanes wait for the handle stream at EVERY call, so
     a caller that writes each batch on the summary's stream (gs_get_stream) needs no
     device synchronisation. Batches are generated on the summary stream behind a GPU
     sleep into one reused buffer."""
     import torch
-    monkeypatch.setenv("GS_GROUP_SELF_APPLY", "1")
+    knobs(group_self_apply=1)
     n, B, scale = 1 << 16, 1 << 12, 14
     with gs.Summary("cc", capacity_hint=1 << scale) as s:
         g = gs.Group(s, gs.group_unique_id(), 1, 0, B)
@@ -99,13 +99,13 @@ def test_group_lanes_follow_handle_stream_every_call(gs, oracle_mod, monkeypatch
     assert np.array_equal(v, ov) and np.array_equal(lab, olab)
 
 
-def test_group_lanes_follow_marked_handle_stream(gs, oracle_mod, monkeypatch):
+def test_group_lanes_follow_marked_handle_stream(gs, oracle_mod, knobs):
     """gs_group.h ordering contract: a caller that queues its own kernels on the
     handle's stream (a cached gs_get_stream) between group calls, with no other call on
     the handle, marks them with gs_wait_stream(h, that stream); the own folds then run
     behind them. Every batch is generated into its own buffers behind a GPU sleep."""
     import torch
-    monkeypatch.setenv("GS_GROUP_SELF_APPLY", "1")
+    knobs(group_self_apply=1)
     n, B, scale = 1 << 16, 1 << 12, 14
     with gs.Summary("cc", capacity_hint=1 << scale) as s:
         g = gs.Group(s, gs.group_unique_id(), 1, 0, B)

@@ -364,53 +364,22 @@ def test_window_server_mixed_window_sizes(gs, oracle_mod, kind):
 
 
 @pytest.mark.parametrize("kind", ["cc", "signed"])
-def test_window_server_late_workgroup(gs, oracle_mod, kind, monkeypatch):
+def test_window_server_late_workgroup(kind):
     """a workgroup that becomes resident late keeps block 0 waiting (up to 8 x the
     idle limit) for the window it handed out; when that window completes the host posts the
     next one at once and block 0 takes it. Every other block must still be polling then (their
-    own limit is 10 x the idle limit), or the next window never completes. The hook
-    GS_SERVER_LATE_US starts the last workgroup of every server launch late (400 us) against
-    a 100-us idle limit (GS_SERVER_IDLE_US): with the old 2 x limit the other blocks left after
+    own limit is 10 x the idle limit), or the next window never completes. The test build of
+    the library (lib_testhooks: -DGS_TEST_LATE_WORKGROUP=400; the product kernel has no such
+    branch) starts the last workgroup of every server launch 400 us late against a 100-us
+    idle limit (GS_TESTING_SERVER_IDLE_US): with the old 2 x limit the other blocks left after
     200 us and the second window of every session failed. Idle gaps between some windows
     restart the server (a new late workgroup each time). Every window's rows replay to the
-    summary, and both equal the oracle."""
-    import time
-    import torch
-    monkeypatch.setenv("GS_SERVER_IDLE_US", "100")
-    monkeypatch.setenv("GS_SERVER_LATE_US", "400")
-    B, nw = 1 << 16, 12
-    E = B * nw
-    src = torch.empty(E, dtype=torch.int64, device="cuda")
-    dst = torch.empty(E, dtype=torch.int64, device="cuda")
-    if kind == "cc":
-        gs.gen_er(src, dst, 0, E, 17, 0x5EED00E9, True)
-    else:
-        gs.gen_bip(src, dst, 0, E, 16, 0x5EED0B1F, [])
-    torch.cuda.synchronize()
-    hs, hd = src.cpu().numpy(), dst.cpu().numpy()
-    rec = torch.empty((B + 16, 3), dtype=torch.int64, device="cuda")
-    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-    with gs.Summary(kind, capacity_hint=1 << 18) as srv, gs.Summary(kind, capacity_hint=1 << 18) as rep:
-        srv.set_delta_tracking(True)
-        srv.set_window_server(True)
-        for w in range(nw):
-            srv.fold_take(src[w * B:], dst[w * B:], B, rec, B + 16, cnt)
-            rep.fold_records(rec, srv.last_take_word)
-            rep.sync()
-            if w % 4 == 3:
-                time.sleep(0.01)  # past every limit: the server leaves; the next window starts a new launch
-        st = srv.window_server_stats()
-        assert st["launches"] >= 3 and st["windows"] >= nw - 1, st
-        if kind == "cc":
-            ov, olab = oracle_mod.cc_labels(hs, hd)
-            for s in (srv, rep):
-                v, lab = s.labels()
-                assert np.array_equal(v, ov) and np.array_equal(lab, olab)
-        else:
-            tok = oracle_mod.bip_truth(hs, hd)[0]
-            assert srv.ok() == rep.ok() == tok
-            a, b = srv.colouring(), rep.colouring()
-            assert a[0] == b[0] and all(np.array_equal(x, y) for x, y in zip(a[1:], b[1:]))
-            if tok:  # and the truth's colouring
-                assert oracle_mod.canonical_candidates_string(*a) == oracle_mod.canonical_candidates_string(
-                    *oracle_mod.bip_truth(hs, hd))
+    summary, and both equal the oracle. A child process loads the test build."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GS_LIB_VARIANT="testhooks")
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "late_workgroup_check.py"), kind], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "late workgroup ok" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

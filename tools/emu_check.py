@@ -1,7 +1,7 @@
 """Correctness check of the emulated N-rank exchange, pass by pass (diagnostic).
 
 Runs tools/emulated_scaling.py's shape -- N rank threads on one GPU, in-process
-communicator (GS_GROUP_FAKE_COMM=1), summaries reset between passes -- at a scale
+communicator (gs_group_set_comm_api: tests/cpp/gs_fake_comm.cpp), summaries reset between passes -- at a scale
 the oracle labels in seconds, and compares EVERY replica with the oracle after
 EVERY pass. Prints one line per pass and exits 1 on the first difference.
 
@@ -12,13 +12,14 @@ import os
 import sys
 import threading
 
-os.environ["GS_GROUP_FAKE_COMM"] = "1"
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import gsamd as gs  # noqa: E402
+
+gs.use_comm_emulation(True)  # in-process collectives (tests/cpp/gs_fake_comm.cpp)
 import oracle  # noqa: E402
 
 

@@ -2,7 +2,7 @@
 
 N rank threads each drive their own replica through the native group
 (include/gs_group.h) with the in-process communicator emulation
-(GS_GROUP_FAKE_COMM=1): every rank folds its contiguous 1/N shard of the RMAT
+(gs_group_set_comm_api: tests/cpp/gs_fake_comm.cpp): every rank folds its contiguous 1/N shard of the RMAT
 stream in per-rank micro-batches, stages its structural delta, "all-gathers" it
 (device copies) and folds the other ranks' rows -- exactly bench.py's N-GPU step,
 with all N ranks' work sharing one GPU. With perfect scaling the N ranks' total
@@ -21,11 +21,12 @@ import sys
 import threading
 import time
 
-os.environ["GS_GROUP_FAKE_COMM"] = "1"
 import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import gsamd as gs  # noqa: E402
+
+gs.use_comm_emulation(True)  # in-process collectives (tests/cpp/gs_fake_comm.cpp)
 
 
 def main():

@@ -16,13 +16,14 @@ import os
 import sys
 import threading
 
-os.environ["GS_GROUP_FAKE_COMM"] = "1"
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import gsamd as gs  # noqa: E402
+
+gs.use_comm_emulation(True)  # in-process collectives (tests/cpp/gs_fake_comm.cpp)
 import oracle  # noqa: E402
 
 LOG_DT = np.dtype([("t0", "<u8"), ("t1", "<u8"), ("src", "<u8"), ("tab", "<u8"), ("blk", "<u4"), ("nblk", "<u4"),

@@ -88,7 +88,7 @@ def main():
 
     # the same shard as a group's tracked own folds (1 rank, in-process communicator: 3 fold
     # lanes, per-exchange stage + count/data collectives, no remote rows) vs the plain fold
-    os.environ["GS_GROUP_FAKE_COMM"] = "1"
+    gs.use_comm_emulation(True)
     g = gs.Group(s, gs.group_unique_id(), 1, 0, B)
 
     def run_tracked():
