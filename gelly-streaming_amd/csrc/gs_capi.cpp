@@ -46,7 +46,7 @@ std::unordered_map<void*, std::pair<int, size_t>> g_allocs;
 hipError_t dmalloc(void** p, size_t bytes) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  const hipError_t e = dmalloc(p, bytes);
+  const hipError_t e = hipMalloc(p, bytes);
   if (e == hipSuccess && *p) {
     std::lock_guard<std::mutex> lk(g_alloc_mu);
     g_allocs[*p] = {dev, bytes};
@@ -65,7 +65,7 @@ hipError_t dfree(void* p) {
       g_allocs.erase(it);
     }
   }
-  return dfree(p);
+  return hipFree(p);
 }
 
 // include/gs_testing.h: process-wide test knobs, -1 = unset (the product value)
