@@ -59,6 +59,9 @@ EXPORTED_SYMBOLS = (
     "gs_fold_parity", "gs_set_window_server", "gs_window_server_stats", "gs_set_batch_dedup",
     "gs_digest", "gs_group_comm_ranks", "gs_group_set_phase_timing", "gs_group_phase_stats",
     "gs_group_set_comm_api", "gs_testing_set", "gs_testing_get", "gs_hbm_bytes", "gs_create_bytes",
+    "gs_group_create_partitioned", "gs_group_part_fold_device", "gs_group_part_combine",
+    "gs_group_part_labels_device", "gs_group_part_status", "gs_group_part_reset", "gs_group_part_stats",
+    "gs_group_part_phase_stats",
 )
 
 FAIL_BIT = 1 << 62  # count words: a failed signed verdict (GS_FAIL_BIT)
@@ -167,6 +170,14 @@ def lib():
     L.gs_group_set_phase_timing.argtypes = [_vp, ctypes.c_int]
     L.gs_group_phase_stats.argtypes = [_vp, ctypes.POINTER(ctypes.c_double)]
     L.gs_group_set_comm_api.argtypes = [_vp]
+    L.gs_group_create_partitioned.argtypes = [ctypes.POINTER(_vp), _vp, _vp, ctypes.c_int, ctypes.c_int, _u64, _sz]
+    L.gs_group_part_fold_device.argtypes = [_vp, _vp, _vp, _sz]
+    L.gs_group_part_combine.argtypes = [_vp]
+    L.gs_group_part_labels_device.argtypes = [_vp, _vp, _vp, _vp, _sz, ctypes.POINTER(_sz)]
+    L.gs_group_part_status.argtypes = [_vp, ctypes.POINTER(ctypes.c_int)]
+    L.gs_group_part_reset.argtypes = [_vp]
+    L.gs_group_part_stats.argtypes = [_vp, ctypes.POINTER(_u64)]
+    L.gs_group_part_phase_stats.argtypes = [_vp, ctypes.POINTER(ctypes.c_double)]
     L.gs_hbm_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(_u64)]
     L.gs_create_bytes.argtypes = [ctypes.c_int, _u64, ctypes.POINTER(_u64)]
     L.gs_testing_set.argtypes = [ctypes.c_int, _i64]
@@ -685,6 +696,84 @@ class Group:
         _check(lib().gs_group_phase_stats(self._g, out))
         return {"own_fold_lane_ms": out[0], "remote_fold_ms": out[1], "stage_count_collective_ms": out[2],
                 "data_collective_ms": out[3], "host_wait_counts_ms": out[4], "exchanges": int(out[5])}
+
+    def close(self):
+        if getattr(self, "_g", None):
+            lib().gs_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PartGroup:
+    """Owner-partitioned multi-GPU combine (include/gs_group.h gs_group_create_partitioned;
+    DESIGN.md section 5b): each rank folds its own edges into a LOCAL forest (`summary`),
+    and every combine sends the new local labels to the vertices' owners, which keep one
+    anchor per vertex and feed the label pairs to every rank's label forest. labels()
+    returns this rank's owned slice. Collective calls: create, combine."""
+
+    def __init__(self, summary, uid, nranks, rank, vertices_hint, window_edges=0):
+        g = _vp()
+        buf = ctypes.create_string_buffer(bytes(uid), GROUP_ID_BYTES)
+        _check(lib().gs_group_create_partitioned(ctypes.byref(g), summary.handle, buf, int(nranks), int(rank),
+                                                 int(vertices_hint), int(window_edges)))
+        self._g = g
+        self.summary = summary
+
+    def fold_device(self, src, dst, n):
+        _check(lib().gs_group_part_fold_device(self._g, _ptr(src), _ptr(dst), int(n)))
+
+    def combine(self):
+        _check(lib().gs_group_part_combine(self._g))
+
+    def labels_device(self, v, label, parity=None):
+        got = _sz()
+        cap = v.numel() if hasattr(v, "numel") else len(v)
+        _check(lib().gs_group_part_labels_device(self._g, _ptr(v), _ptr(label), _ptr(parity), int(cap),
+                                                 ctypes.byref(got)))
+        return got.value
+
+    def labels(self, cap, with_parity=False):
+        """This rank's owned (v, label[, parity]) as numpy arrays sorted by v."""
+        import torch
+        dev = torch.device("cuda", self.summary.device)
+        v = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        lab = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        par = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev) if with_parity else None
+        k = self.labels_device(v, lab, par)
+        hv, hl = v[:k].cpu().numpy(), lab[:k].cpu().numpy()
+        o = np.argsort(hv, kind="stable")
+        if with_parity:
+            return hv[o], hl[o], par[:k].cpu().numpy()[o]
+        return hv[o], hl[o]
+
+    def ok(self):
+        o = ctypes.c_int()
+        _check(lib().gs_group_part_status(self._g, ctypes.byref(o)))
+        return bool(o.value)
+
+    def reset(self):
+        _check(lib().gs_group_part_reset(self._g))
+
+    def stats(self):
+        a = (_u64 * 8)()
+        _check(lib().gs_group_part_stats(self._g, a))
+        keys = ("combines", "rows_exported", "rows_owned", "pairs_sent", "pairs_folded", "label_forest_vertices",
+                "owner_slots")
+        return dict(zip(keys, list(a)))
+
+    def set_phase_timing(self, on=True):
+        _check(lib().gs_group_set_phase_timing(self._g, 1 if on else 0))
+
+    def phase_stats(self):
+        out = (ctypes.c_double * 8)()
+        _check(lib().gs_group_part_phase_stats(self._g, out))
+        keys = ("own_fold_ms", "export_ms", "bucket_ms", "alltoall_ms", "owner_ms", "pairs_ms", "combines")
+        return dict(zip(keys, list(out)))
 
     def close(self):
         if getattr(self, "_g", None):

@@ -36,6 +36,7 @@
 
 #include "gs_group.h"
 #include "gs_internal.hpp"
+#include "gs_part.hpp"
 #include "gs_testing.h"
 
 using namespace gsi;
@@ -226,9 +227,29 @@ struct gs_group {
   };
   std::vector<PhaseEv> ph_pending;
   std::vector<hipEvent_t> ph_pool;
-  double ph_ms[4] = {};
+  double ph_ms[8] = {};
   uint64_t ph_exchanges = 0;
   double wait_s = 0;
+
+  // ---- owner-partitioned mode (gs_group_create_partitioned)
+  bool part = false;
+  gs_summary* G = nullptr;       // the label forest: a replica of the labels that need a cross-rank union
+  uint64_t window = 0;           // own edges between combines (0: one combine per pass, untracked folds)
+  uint64_t win_edges = 0;        // own edges since the last combine
+  gs::OwnerTable ot{};
+  uint32_t* mark = nullptr;      // device [64]: vertex-list fill at the previous combine
+  uint32_t* snap = nullptr;      // device [64]: the fill now
+  uint32_t* pflags = nullptr;    // device: [0] owner-table overflow, [1] odd cycle found by an owner
+  unsigned long long* pdev = nullptr;  // device: [0..2] snap out, [3] pairs, [4] count word, [5] label rows,
+                                       // [8, 8 + N) send counts, then N x N all send counts, then N count words
+  unsigned long long* phost = nullptr;  // pinned host mirror of pdev's words
+  int64_t *stage = nullptr, *sendbuf = nullptr, *recvbuf = nullptr, *pairs = nullptr, *pairs_all = nullptr;
+  uint64_t stage_cap = 0, send_cap = 0, recv_cap = 0, pairs_cap = 0, pairs_all_cap = 0;
+  uint32_t* bcnt = nullptr;
+  uint64_t bcnt_cap = 0;
+  uint64_t cap_seen = 0;         // the local table's capacity at the previous combine (a rebuild re-exports all)
+  hipEvent_t pev = nullptr;      // the combine's pair gather -> the label forest's fold
+  uint64_t combines = 0, rows_exported = 0, rows_owned = 0, pairs_sent = 0, pairs_folded = 0;
 
   unsigned long long* cnt_send(int k) const { return cnt + k; }
   unsigned long long* cnt_recv(int k) const { return cnt + kLag + (size_t)k * nranks; }
@@ -804,6 +825,15 @@ int gs_group_destroy(gs_group_t g) {
     (void)dfree(g->send[k]);
     (void)dfree(g->recv[k]);
   }
+  if (g->part) {
+    if (g->G) (void)gs_destroy(g->G);
+    for (void* q : {(void*)g->ot.tab, (void*)g->mark, (void*)g->snap, (void*)g->pflags, (void*)g->pdev, (void*)g->stage,
+                    (void*)g->sendbuf, (void*)g->recvbuf, (void*)g->pairs, (void*)g->pairs_all, (void*)g->bcnt})
+      (void)dfree(q);
+    if (g->phost) (void)hipHostFree(g->phost);
+    if (g->pev) (void)hipEventDestroy(g->pev);
+    if (g->window && !g->prev_track) (void)gs_set_delta_tracking(g->h, 0);
+  }
   ph_drain(g);
   for (hipEvent_t e : g->ph_pool) (void)hipEventDestroy(e);
   (void)dfree(g->cnt);
@@ -811,6 +841,324 @@ int gs_group_destroy(gs_group_t g) {
   if (g->xd) (void)hipStreamDestroy(g->xd);
   if (g->hdr_host) (void)hipHostFree(g->hdr_host);
   delete g;
+  return GS_OK;
+}
+
+
+// ---------------------------------------------------------------------------
+// Owner-partitioned mode (include/gs_group.h; kernels gs_part_k.hip)
+
+}  // extern "C"
+
+namespace {
+
+int part_of(gs_group* g) {
+  if (!g) return fail(GS_ERR_INVALID, "null group");
+  if (!g->part) return fail(GS_ERR_INVALID, "not a partitioned group (gs_group_create_partitioned)");
+  return GS_OK;
+}
+
+// grow-only device buffer of `need` elements of T; `keep` elements are carried over (stream st)
+template <typename T>
+int ensure_buf(T*& buf, uint64_t& cap, uint64_t need, hipStream_t st, uint64_t keep = 0) {
+  if (need <= cap && buf) return GS_OK;
+  const uint64_t c = std::max<uint64_t>(need + need / 4, 1024);
+  T* nb = nullptr;
+  GS_HIP(dmalloc(&nb, c * sizeof(T)));
+  if (buf) {
+    if (keep) GS_HIP(hipMemcpyAsync(nb, buf, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
+    GS_HIP(hipStreamSynchronize(st));
+    (void)dfree(buf);
+  }
+  buf = nb;
+  cap = c;
+  return GS_OK;
+}
+
+// device words of pdev -> host (phost), one stream synchronisation
+int part_read(gs_group* g, size_t first, size_t n) {
+  hipStream_t st = g->h->stream;
+  GS_HIP(hipMemcpyAsync(g->phost + first, g->pdev + first, n * 8, hipMemcpyDeviceToHost, st));
+  GS_HIP(hipStreamSynchronize(st));
+  return GS_OK;
+}
+
+int part_init_tables(gs_group* g) {
+  hipStream_t st = g->h->stream;
+  gs::launch_part_init(g->ot.tab, (uint64_t)g->ot.cap + 1, st);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemsetAsync(g->mark, 0, gs::kShards * 4, st));
+  GS_HIP(hipMemsetAsync(g->pflags, 0, 16, st));
+  g->win_edges = 0;
+  g->cap_seen = g->h->cap;
+  return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_group_create_partitioned(gs_group_t* out, gs_handle h, const void* id, int nranks, int rank,
+                                uint64_t vertices_hint, size_t window_edges) {
+  if (!out || !id) return fail(GS_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (!h) return fail(GS_ERR_INVALID, "null handle");
+  if (nranks < 1 || nranks > gs::kPartMaxRanks || rank < 0 || rank >= nranks)
+    return fail(GS_ERR_INVALID, "bad group shape (1..64 ranks)");
+  if (window_edges > kMaxGroupBatch) return fail(GS_ERR_INVALID, "window_edges above 2^26");
+  if (h->side) return fail(GS_ERR_INVALID, "the summary already belongs to an exchange group");
+  gs_comm_api api;
+  if (int rc = comm_api(&api)) return rc;
+  DeviceGuard dg(h->device);
+  gs_group* g = new gs_group();
+  g->h = h;
+  g->api = api;
+  g->nranks = nranks;
+  g->rank = rank;
+  g->width = h->kind == GS_KIND_SIGNED ? 3 : 2;
+  g->part = true;
+  g->window = window_edges;
+  auto bail = [&](int code) {
+    gs_group_destroy(g);
+    return code;
+  };
+  if (int rc = join_lanes(h)) return bail(rc);
+  g->prev_track = h->track;
+  if (window_edges) {  // records of the window: roots hooked away since the previous combine
+    if (int rc = ensure_delta_list(h, window_edges)) return bail(rc);
+    if (int rc = gs_set_delta_tracking(h, 1)) return bail(rc);
+  }
+  // the label forest: grows on its own (capacity checks of its folds)
+  if (int rc = gs_create(&g->G, h->device, h->kind, std::max<uint64_t>(vertices_hint / 64, 1u << 12)))
+    return bail(rc);
+  uint64_t ocap = 1024;
+  while (ocap < 4 * (vertices_hint / (uint64_t)nranks + 256)) ocap <<= 1;
+  if (ocap > (1ull << 31)) return bail(fail(GS_ERR_INVALID, "vertices_hint too large for the owner table"));
+  g->ot.cap = (uint32_t)ocap;
+  g->ot.mask = (uint32_t)(ocap - 1);
+  int lg = 0;
+  while ((1ull << lg) < ocap) ++lg;
+  g->ot.shift = 64 - lg;
+  g->ot.r0 = (uint32_t)ocap;
+  const size_t pwords = 8 + (size_t)nranks + (size_t)nranks * nranks + nranks;
+  bool ok = dmalloc(&g->ot.tab, (ocap + 1) * sizeof(gs::OwnerSlot)) == hipSuccess &&
+            dmalloc(&g->mark, gs::kShards * 4) == hipSuccess && dmalloc(&g->snap, gs::kShards * 4) == hipSuccess &&
+            dmalloc(&g->pflags, 16) == hipSuccess && dmalloc(&g->pdev, pwords * 8) == hipSuccess &&
+            hipHostMalloc(&g->phost, pwords * 8, hipHostMallocDefault) == hipSuccess &&
+            hipEventCreateWithFlags(&g->pev, hipEventDisableTiming) == hipSuccess;
+  if (!ok) return bail(fail(GS_ERR_HIP, "partitioned group allocation failed"));
+  g->ot.err = g->pflags;
+  if (int rc = part_init_tables(g)) return bail(rc);
+  GS_HIP(hipStreamSynchronize(h->stream));
+  int r = api.comm_init_rank(&g->comm_c, nranks, id, rank);
+  if (r != 0) return bail(rccl_fail(&api, "ncclCommInitRank(counts)", r));
+  r = api.comm_init_rank(&g->comm_d, nranks, static_cast<const char*>(id) + kIdBytes, rank);
+  if (r != 0) return bail(rccl_fail(&api, "ncclCommInitRank(data)", r));
+  *out = g;
+  return GS_OK;
+}
+
+int gs_group_part_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n) {
+  if (int rc = part_of(g)) return rc;
+  if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "null edge arrays");
+  if (g->window && g->win_edges + n > g->window)
+    return fail(GS_ERR_INVALID, "more than window_edges own edges since the last combine");
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  FoldSource fs;
+  fs.allow_pipe = g->window == 0;  // untracked folds may pipeline (gs_set_pipelining)
+  hipEvent_t pa = ph_begin(g, h->stream);
+  if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, /*track=*/g->window != 0, true, fs)) return rc;
+  ph_end(g, 0, pa, h->stream);
+  g->win_edges += n;
+  return GS_OK;
+}
+
+int gs_group_part_combine(gs_group_t g) {
+  if (int rc = part_of(g)) return rc;
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  if (int rc = join_lanes(h)) return rc;
+  hipStream_t st = h->stream;
+  const int N = g->nranks, W = g->width;
+  const bool sign = h->kind == GS_KIND_SIGNED;
+  const bool full = h->cap != g->cap_seen;  // the table was rebuilt: every vertex again
+  const gs::Delta D = h->delta(0);
+  unsigned long long* sendcnt = g->pdev + 8;
+  unsigned long long* allcnt = sendcnt + N;
+  unsigned long long* words = allcnt + (size_t)N * N;
+  // 1. what is new since the previous combine
+  hipEvent_t p0 = ph_begin(g, st);
+  gs::launch_part_snap(h->table(), g->mark, g->snap, full ? 1 : 0, D.dctr, h->drec ? D.shard_cap : 0u, g->pdev, st);
+  GS_HIP(hipGetLastError());
+  if (int rc = part_read(g, 0, 3)) return rc;
+  if (g->phost[2]) return fail(GS_ERR_CAPACITY, "vertex list overflow: the partitioned combine needs the list");
+  const uint64_t total = g->phost[0], nrec = (g->window && h->track) ? g->phost[1] : 0;
+  const uint32_t nblocks = (uint32_t)((total + gs::kPartRowsPB - 1) / gs::kPartRowsPB);
+  if (int rc = ensure_buf(g->stage, g->stage_cap, std::max<uint64_t>(total, 1) * W, st)) return rc;
+  if (int rc = ensure_buf(g->bcnt, g->bcnt_cap, (uint64_t)std::max<uint32_t>(nblocks, 1) * N, st)) return rc;
+  if (int rc = ensure_buf(g->pairs, g->pairs_cap, (nrec + 1) * W, st)) return rc;
+  GS_HIP(hipMemsetAsync(g->pdev + 3, 0, 8, st));
+  // 2. export the new vertices (marks their roots), then the marked roots hooked away
+  gs::launch_part_export(sign, h->table(), g->mark, g->snap, full ? 1 : 0, total, g->stage, W, g->bcnt, N, st);
+  GS_HIP(hipGetLastError());
+  if (nrec) {
+    gs::launch_part_records(sign, h->table(), D, g->pairs, W, g->pdev + 3, g->pairs_cap / W, st);
+    GS_HIP(hipGetLastError());
+  }
+  if (h->track) {  // the window's records are consumed
+    GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_DELTA), 0, (size_t)gs::kShards * gs::kCtrStride * 4, st));
+    h->delta_fill_ub[0] = 0;
+  }
+  ph_end(g, 1, p0, st);
+  // 3. bucket by owner
+  hipEvent_t p1 = ph_begin(g, st);
+  if (total) {
+    gs::launch_part_scan(g->bcnt, nblocks, N, sendcnt, st);
+  } else {
+    GS_HIP(hipMemsetAsync(sendcnt, 0, (size_t)N * 8, st));
+  }
+  if (int rc = ensure_buf(g->sendbuf, g->send_cap, std::max<uint64_t>(total, 1) * W, st)) return rc;
+  gs::launch_part_scatter(g->stage, total, W, g->bcnt, nblocks, sendcnt, N, g->sendbuf, st);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(g->mark, g->snap, gs::kShards * 4, hipMemcpyDeviceToDevice, st));
+  g->cap_seen = h->cap;
+  ph_end(g, 2, p1, st);
+  // 4. counts, then the rows to their owners
+  hipEvent_t p2 = ph_begin(g, st);
+  int r = g->api.all_gather(sendcnt, allcnt, (size_t)N, kNcclInt64, g->comm_c, st);
+  if (r) return rccl_fail(&g->api, "ncclAllGather(part counts)", r);
+  if (int rc = part_read(g, 8 + N, (size_t)N * N)) return rc;
+  std::vector<size_t> sc(N), sd(N), rcv(N), rd(N);
+  uint64_t total_recv = 0, so = 0;
+  for (int q = 0; q < N; ++q) {
+    sc[q] = (size_t)g->phost[8 + N + (size_t)g->rank * N + q] * W;
+    sd[q] = so;
+    so += sc[q];
+    rcv[q] = (size_t)g->phost[8 + N + (size_t)q * N + g->rank] * W;
+    rd[q] = (size_t)total_recv * W;
+    total_recv += rcv[q] / W;
+  }
+  if (int rc = ensure_buf(g->recvbuf, g->recv_cap, std::max<uint64_t>(total_recv, 1) * W, st)) return rc;
+  if (!g->api.all_to_allv) return fail(GS_ERR_HIP, "the comm backend has no all_to_allv");
+  r = g->api.all_to_allv(g->sendbuf, sc.data(), sd.data(), g->recvbuf, rcv.data(), rd.data(), kNcclInt64, g->comm_d,
+                         st);
+  if (r) return rccl_fail(&g->api, "ncclAllToAllv(part rows)", r);
+  ph_end(g, 3, p2, st);
+  // 5. the owner step: anchors and label pairs
+  hipEvent_t p3 = ph_begin(g, st);
+  if (int rc = ensure_buf(g->pairs, g->pairs_cap, (nrec + total_recv + 1) * W, st, nrec * W)) return rc;
+  gs::launch_part_owner(sign, g->ot, g->recvbuf, total_recv, W, g->pairs, g->pdev + 3, g->pairs_cap / W,
+                        g->pflags + 1, st);
+  GS_HIP(hipGetLastError());
+  gs::launch_part_count_word(g->pdev + 3, sign ? h->ctr + gs::ctr_index(gs::CTR_FAIL) : nullptr,
+                             sign ? g->pflags + 1 : nullptr, g->pdev + 4, st);
+  GS_HIP(hipGetLastError());
+  ph_end(g, 4, p3, st);
+  // 6. every rank's pairs into every rank's label forest
+  hipEvent_t p4 = ph_begin(g, st);
+  r = g->api.all_gather(g->pdev + 4, words, 1, kNcclInt64, g->comm_c, st);
+  if (r) return rccl_fail(&g->api, "ncclAllGather(pair counts)", r);
+  GS_HIP(hipMemcpyAsync(g->phost, g->pflags, 4, hipMemcpyDeviceToHost, st));  // owner-table overflow
+  if (int rc = part_read(g, 8 + N + (size_t)N * N, (size_t)N)) return rc;
+  if ((uint32_t)g->phost[0]) return fail(GS_ERR_CAPACITY, "owner table overflow: raise vertices_hint");
+  uint64_t maxp = 0, live = 0, own = 0;
+  for (int q = 0; q < N; ++q) {
+    const uint64_t c = g->phost[8 + N + (size_t)N * N + q] & (gs::kFailBit - 1);
+    maxp = std::max(maxp, c);
+    live += c;
+    if (q == g->rank) own = c;
+  }
+  if (own > g->pairs_cap / W) return fail(GS_ERR_CAPACITY, "label pair buffer overflow");
+  const uint64_t rows = std::max<uint64_t>(maxp, 1);
+  if (int rc = ensure_buf(g->pairs, g->pairs_cap, rows * W, st, own * W)) return rc;
+  if (int rc = ensure_buf(g->pairs_all, g->pairs_all_cap, (uint64_t)N * rows * W, st)) return rc;
+  r = g->api.all_gather(g->pairs, g->pairs_all, rows * W, kNcclInt64, g->comm_d, st);
+  if (r) return rccl_fail(&g->api, "ncclAllGather(label pairs)", r);
+  GS_HIP(hipEventRecord(g->pev, st));
+  gs_summary* G = g->G;
+  GS_HIP(hipStreamWaitEvent(G->stream, g->pev, 0));
+  FoldSource fs;
+  fs.rows = (uint32_t)rows;
+  fs.skip_rank = -1;
+  fs.counts = words;
+  fs.units = live;
+  const uint8_t* w = W == 3 ? reinterpret_cast<const uint8_t*>(g->pairs_all + 2) : nullptr;
+  if (int rc = fold_device_impl(G, g->pairs_all, g->pairs_all + 1, w, (size_t)N * rows, W, 8 * W, false, true, fs))
+    return rc;
+  // the next combine reuses pairs_all and the words only after this fold
+  GS_HIP(hipEventRecord(g->pev, G->stream));
+  GS_HIP(hipStreamWaitEvent(st, g->pev, 0));
+  ph_end(g, 5, p4, st);
+  g->combines++;
+  g->rows_exported += total;
+  g->rows_owned += total_recv;
+  g->pairs_sent += own;
+  g->pairs_folded += live;
+  g->win_edges = 0;
+  if (g->phases) g->ph_exchanges++;
+  return GS_OK;
+}
+
+int gs_group_part_labels_device(gs_group_t g, int64_t* v, int64_t* label, uint8_t* parity, size_t cap, size_t* n) {
+  if (int rc = part_of(g)) return rc;
+  if (!n || (cap && (!v || !label))) return fail(GS_ERR_INVALID, "null output");
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  hipStream_t st = h->stream;
+  if (int rc = join_lanes(g->G)) return rc;
+  GS_HIP(hipEventRecord(g->pev, g->G->stream));
+  GS_HIP(hipStreamWaitEvent(st, g->pev, 0));
+  GS_HIP(hipMemsetAsync(g->pdev + 5, 0, 8, st));
+  gs::launch_part_labels(g->ot, g->G->table(), v, label, parity, cap, g->pdev + 5, st);
+  GS_HIP(hipGetLastError());
+  if (int rc = part_read(g, 5, 1)) return rc;
+  *n = (size_t)g->phost[5];
+  if (*n > cap) return fail(GS_ERR_TRUNCATED, "output too small for the owned vertices");
+  return GS_OK;
+}
+
+int gs_group_part_status(gs_group_t g, int* ok) {
+  if (int rc = part_of(g)) return rc;
+  if (!ok) return fail(GS_ERR_INVALID, "ok is null");
+  return gs_bip_status(g->G, ok);  // every rank's verdict travels in its pair count word
+}
+
+int gs_group_part_reset(gs_group_t g) {
+  if (int rc = part_of(g)) return rc;
+  gs_summary* h = g->h;
+  DeviceGuard dg(h->device);
+  if (int rc = gs_reset(h)) return rc;
+  if (int rc = gs_reset(g->G)) return rc;
+  if (int rc = part_init_tables(g)) return rc;
+  g->cap_seen = h->cap;
+  return GS_OK;
+}
+
+int gs_group_part_stats(gs_group_t g, uint64_t* out8) {
+  if (int rc = part_of(g)) return rc;
+  if (!out8) return fail(GS_ERR_INVALID, "out is null");
+  uint64_t gv = 0;
+  if (int rc = gs_num_vertices(g->G, &gv)) return rc;
+  out8[0] = g->combines;
+  out8[1] = g->rows_exported;
+  out8[2] = g->rows_owned;
+  out8[3] = g->pairs_sent;
+  out8[4] = g->pairs_folded;
+  out8[5] = gv;
+  out8[6] = (uint64_t)g->ot.cap;
+  out8[7] = 0;
+  return GS_OK;
+}
+
+int gs_group_part_phase_stats(gs_group_t g, double* out8) {
+  if (int rc = part_of(g)) return rc;
+  if (!out8) return fail(GS_ERR_INVALID, "out is null");
+  DeviceGuard dg(g->h->device);
+  ph_drain(g);
+  for (int i = 0; i < 6; ++i) out8[i] = g->ph_ms[i];
+  out8[6] = (double)g->ph_exchanges;
+  out8[7] = 0;
   return GS_OK;
 }
 

@@ -136,6 +136,50 @@ int gs_group_comm_ranks(gs_group_t g, int* count_comm, int* data_comm);
 int gs_group_set_phase_timing(gs_group_t g, int on);
 int gs_group_phase_stats(gs_group_t g, double* out6);
 
+/* ---- Owner-partitioned mode (round 6) -----------------------------
+ * The replica mode above makes every rank insert every vertex of the graph. Here each rank
+ * keeps a LOCAL forest of its own edges only (the summary h: its min-key roots are local
+ * labels), and the vertices are partitioned by owner (a hash of the id mod nranks). At
+ * every combine (the window end of SummaryBulkAggregation.java:76-83; with window_edges 0,
+ * once per pass: the bulk combine of SummaryTreeReduce.java:68-123):
+ *   1. each rank exports (v, local root[, parity]) for the vertices new to it since the
+ *      previous combine, bucketed by owner (and marks those roots), plus a label pair
+ *      (a, root of a now) for every marked root a hooked away since then;
+ *   2. the rows go to their owners (ncclAllToAllv on the data communicator, counts first
+ *      on the count communicator);
+ *   3. the owner of v keeps one anchor label per vertex (the first row's) and turns every
+ *      other row (v, l) into the label pair (anchor, l) (deduplicated per block);
+ *   4. every rank's pairs are all-gathered and folded into every rank's LABEL FOREST, a
+ *      replica of only the labels that need a cross-rank union (a few % of V on RMAT).
+ * The canonical label of an owned vertex v is the label forest's label of anchor(v);
+ * gs_group_part_labels_device emits this rank's owned slice, and the slices of all ranks
+ * are the Merger's output (bit-exact with a single summary: labels = min id, signed
+ * colourings composed along anchor -> label). Collectives are issued on the handle's stream
+ * in program order. vertices_hint sizes the owner table (4 slots per expected owned
+ * vertex; overflow fails with GS_ERR_CAPACITY). window_edges > 0: at most that many own
+ * edges between combines (delta tracking on, records of hooked roots); 0: untracked
+ * (pipelinable) folds and one combine per pass -- gs_group_part_reset starts the next. */
+int gs_group_create_partitioned(gs_group_t* g, gs_handle h, const void* id, int nranks, int rank,
+                                uint64_t vertices_hint, size_t window_edges);
+/* Fold n device edges of this rank into its local forest (as gs_fold_device, stride 1). */
+int gs_group_part_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, size_t n);
+/* The window end: steps 1-4 above. Collective; synchronises this rank's streams. */
+int gs_group_part_combine(gs_group_t g);
+/* This rank's owned vertices after the last combine: (v, canonical label[, parity]) into
+ * DEVICE arrays of `cap` rows (parity may be NULL); *n = rows (GS_ERR_TRUNCATED if > cap). */
+int gs_group_part_labels_device(gs_group_t g, int64_t* v, int64_t* label, uint8_t* parity, size_t cap, size_t* n);
+/* The global bipartiteness verdict after the last combine (every rank's, AND-ed). */
+int gs_group_part_status(gs_group_t g, int* ok);
+/* Empty local forest, owner table and label forest (the next pass). Not collective. */
+int gs_group_part_reset(gs_group_t g);
+/* out8: combines, rows exported, rows owned (received), label pairs sent, label pairs folded
+ * (all ranks), label-forest vertices, owner-table slots, 0. */
+int gs_group_part_stats(gs_group_t g, uint64_t* out8);
+/* With gs_group_set_phase_timing on, device ms per phase since: out8[0] own folds (handle
+ * stream only), [1] export + records, [2] bucketing, [3] count + row all-to-all, [4] owner
+ * step, [5] pair all-gather + label-forest fold, [6] combines, [7] 0. */
+int gs_group_part_phase_stats(gs_group_t g, double* out8);
+
 int gs_group_destroy(gs_group_t g);
 
 #ifdef __cplusplus

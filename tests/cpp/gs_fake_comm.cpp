@@ -69,6 +69,30 @@ std::map<std::string, Shared*> g_reg;
 thread_local uint64_t t_order = 0x9E3779B97F4A7C15ull;  // this rank thread's order hash
 std::atomic<int> g_last_err{0};
 
+// Serialized replay (gs_fake_comm_set_serialize): a rank thread holds the GPU token
+// whenever it is outside a collective, so the ranks' work between two collectives runs
+// one rank at a time and each rank's HIP events time its own work alone (tools/part_replay.py:
+// the per-rank cost of an N-GPU pass, measured on one GPU).
+std::atomic<bool> g_serialize{false};
+std::mutex g_token;
+thread_local bool t_token = false;
+void token_release() {
+  if (g_serialize && t_token) {
+    t_token = false;
+    g_token.unlock();
+  }
+}
+void token_acquire() {
+  if (g_serialize && !t_token) {
+    g_token.lock();
+    t_token = true;
+  }
+}
+struct TokenGap {  // inside a collective: the token is free for the other ranks
+  TokenGap() { token_release(); }
+  ~TokenGap() { token_acquire(); }
+};
+
 uint64_t mix(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
@@ -172,6 +196,7 @@ int finish_collective(Comm* c, hipStream_t st) {
   return barrier(s);
 }
 int f_all_gather(const void* send, void* recv, size_t count, int dtype, void* comm, void* stream) {
+  TokenGap gap;
   Comm* c = (Comm*)comm;
   Shared* s = c->s;
   hipStream_t st = (hipStream_t)stream;
@@ -195,6 +220,7 @@ int f_all_gather(const void* send, void* recv, size_t count, int dtype, void* co
 }
 int f_all_to_allv(const void* send, const size_t* sc, const size_t* sd, void* recv, const size_t* rc,
                   const size_t* rd, int dtype, void* comm, void* stream) {
+  TokenGap gap;
   Comm* c = (Comm*)comm;
   Shared* s = c->s;
   hipStream_t st = (hipStream_t)stream;
@@ -223,6 +249,7 @@ int f_all_to_allv(const void* send, const size_t* sc, const size_t* sd, void* re
 // point-to-point: not part of the order hash (a tree's ranks legitimately issue
 // different send/recv sequences)
 int f_send(const void* buf, size_t count, int dtype, int peer, void* comm, void* stream) {
+  TokenGap gap;
   Comm* c = (Comm*)comm;
   Shared* s = c->s;
   hipStream_t st = (hipStream_t)stream;
@@ -239,6 +266,7 @@ int f_send(const void* buf, size_t count, int dtype, int peer, void* comm, void*
   return hipStreamWaitEvent(st, msg.copied, 0) == hipSuccess ? 0 : kErrHip;
 }
 int f_recv(void* buf, size_t count, int dtype, int peer, void* comm, void* stream) {
+  TokenGap gap;
   Comm* c = (Comm*)comm;
   Shared* s = c->s;
   hipStream_t st = (hipStream_t)stream;
@@ -288,4 +316,11 @@ int gs_fake_comm_last_error(void) { return g_last_err.exchange(0); }
 // the calling thread's order hash (tests compare ranks' hashes after a run)
 uint64_t gs_fake_comm_order_hash(void) { return t_order; }
 void gs_fake_comm_reset_order(void) { t_order = 0x9E3779B97F4A7C15ull; }
+// serialized replay: on -> every rank thread must call gs_fake_comm_token(1) before its first
+// GPU work and gs_fake_comm_token(0) when it is done
+void gs_fake_comm_set_serialize(int on) { g_serialize = on != 0; }
+void gs_fake_comm_token(int take) {
+  if (take) token_acquire();
+  else token_release();
+}
 }
