@@ -139,8 +139,12 @@ def parse():
     p.add_argument("--bip-prefix-log2", type=int, default=15,
                    help="bip: edges of the prefix the quirk-exact Candidates oracle folds (O(E x components))")
     p.add_argument("--cpu-sample-log2", type=int, default=24)
-    p.add_argument("--cpu-threads", type=int, default=1,
-                   help="also time the partitioned P-thread CPU baseline (CombineCC of the partials)")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="threads of SURVEY 8(d)'s CPU leg (b): P threads fold a partition each, then CombineCC of "
+                        "the partials + Merger (0: this process's CPU share, OMP_NUM_THREADS or the affinity set, "
+                        "at most 16; 1: skip leg b)")
+    p.add_argument("--cpu-threads-sample-log2", type=int, default=22,
+                   help="edges of the threaded CPU leg's sample (the same stream's first 2^k)")
     p.add_argument("--no-profile-pass", action="store_true")
     p.add_argument("--pipeline", type=int, default=3,
                    help="pipelined windows at N=1 (gs_set_pipelining depth; 1 = strictly in order)")
@@ -1037,21 +1041,37 @@ def main():
         hs = src[:m].cpu().numpy()
         hd = dst[:m].cpu().numpy()
         secs1 = oracle.cpu_baseline_cc(hs, hd, B, threads=1)
-        # BASELINE.md plan (b), opt-in (--cpu-threads P): P threads, each folding a 1/P
-        # partition of every window, then CombineCC of the partials and the Merger. It
-        # measured slower than one thread (0.66 vs 0.91 M edges/s, r02: the combines
-        # dominate) and cost 25 s of the run, so the default line times one thread.
-        p = max(1, args.cpu_threads)
-        secsp = oracle.cpu_baseline_cc(hs, hd, B, threads=p) if p > 1 else secs1
-        best_p, best = (p, secsp) if secsp < secs1 else (1, secs1)
-        cpu = {"value": round(m / best, 1), "unit": "edges/s", "cores": best_p, "kind": "port",
-               "value_1thread": round(m / secs1, 1),
+        # SURVEY.md 8(d) leg (b): P threads, each folding a 1/P partition of every window
+        # (PartitionMapper + keyed fold, S/SummaryBulkAggregation.java:77-83), then CombineCC of
+        # the partials and the Merger on one thread. P = this process's CPU share (the GPU box
+        # exports OMP_NUM_THREADS=16; nproc there shows the whole machine). Timed on the first
+        # 2^22 edges: the combines make it slower than one thread per edge (r02: 0.66 vs 0.91 M
+        # edges/s), and 2^24 edges would cost ~25 s.
+        p = args.cpu_threads
+        if p <= 0:
+            try:
+                aff = len(os.sched_getaffinity(0))
+            except AttributeError:
+                aff = os.cpu_count() or 1
+            p = min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff)
+        cpu = {"value": round(m / secs1, 1), "unit": "edges/s", "cores": 1, "kind": "port",
                "sample": "first 2^%d edges of the same RMAT-%d stream, %d-edge windows, C++ restatement of "
                          "DisjointSet.union + CombineCC/Merger per window (oracle/gs_oracle.cpp); 1 thread %.1f s"
-                         % (args.cpu_sample_log2, args.scale, B, secs1)}
+                         % (args.cpu_sample_log2, args.scale, B, secs1),
+               "legs": {"a_1thread": {"value": round(m / secs1, 1), "cores": 1, "edges": m,
+                                      "seconds": round(secs1, 2)}}}
         if p > 1:
-            cpu["value_%dthreads" % p] = round(m / secsp, 1)
-            cpu["sample"] += "; %d threads (partitioned fold + CombineCC) %.1f s; value = the faster" % (p, secsp)
+            mp = min(m, 1 << args.cpu_threads_sample_log2)
+            secsp = oracle.cpu_baseline_cc(hs[:mp], hd[:mp], B, threads=p)
+            cpu["legs"]["b_partitioned"] = {"value": round(mp / secsp, 1), "cores": p, "edges": mp,
+                                            "seconds": round(secsp, 2),
+                                            "what": "%d threads fold a partition of every window each, then "
+                                                    "CombineCC of the partials + Merger" % p}
+            cpu["value_%dthreads" % p] = round(mp / secsp, 1)
+            cpu["sample"] += "; leg b: %d threads (partitioned fold + CombineCC) on the first 2^%d edges, %.1f s" % (
+                p, args.cpu_threads_sample_log2, secsp)
+            if mp / secsp > m / secs1:  # value = the faster leg, cores = its threads
+                cpu["value"], cpu["cores"] = round(mp / secsp, 1), p
 
     if rank == 0:
         line = {
