@@ -177,3 +177,110 @@ def tree_combine(summary, group=None):
             summary.sync()
         step <<= 1
     return rank == 0
+
+
+def part_owner(v, world):
+    """Owner rank of vertex ids (numpy int64): csrc/gs_part.hpp part_owner, bit for bit."""
+    import numpy as np
+    z = np.asarray(v, np.int64).view(np.uint64) ^ np.uint64(0x5851F42D4C957F2D)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z ^= z >> np.uint64(31)
+    return ((z >> np.uint64(32)) % np.uint64(world)).astype(np.int64)
+
+
+class PartitionedLabelCombine:
+    """The owner-partitioned combine of include/gs_group.h (gs_group_create_partitioned,
+    DESIGN.md section 5b) over torch.distributed: no rank replicates the graph. Each rank
+    keeps a LOCAL forest of its own edges; a combine (the window end of
+    SummaryBulkAggregation.java:76-83)
+      1. exports (v, local root, parity) of the vertices new since the previous combine,
+         bucketed by owner (part_owner), and the label pairs (a, root of a now, parity) of
+         the exported roots hooked away since then;
+      2. moves the rows to their owners (counts all_to_all_single, then rows
+         all_to_all_single with splits);
+      3. at the owner, keeps one anchor (label, parity) per vertex -- the first row's -- and
+         turns every other row (v, l, p) into the pair (anchor, l, p ^ parity(anchor)); a row
+         with the anchor's label and the other parity is an odd cycle;
+      4. all-gathers the pairs (count words carry a failed verdict, FAIL_BIT) and folds
+         every rank's pairs into every rank's LABEL forest.
+    labels() = this rank's owned slice: (v, label of anchor(v), parity composed).
+
+    `local` provides export_new() -> (v, l, p) numpy int64 arrays (marks the roots l) and
+    hooked_exported() -> (a, l, p) for the marked roots hooked away since the previous call
+    (and marks their roots), and failed(); `forest` provides fold(a, b, w), find(x) ->
+    (root, parity) or None, and failed(). The native group runs the same steps in HIP
+    kernels (csrc/gs_part_k.hip); the CPU tests plug models (tests/test_distributed_cpu.py).
+    """
+
+    WIDTH = 3
+
+    def __init__(self, local, forest, group=None):
+        self.local = local
+        self.forest = forest
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.anchor = {}  # owned vertex -> (anchor label, parity of v relative to it)
+        self.odd = False  # an owner saw one vertex on both sides of one label
+        self.combines = 0
+        self.rows_owned = 0
+        self.pairs_folded = 0
+
+    def combine(self):
+        import numpy as np
+        W, world = self.WIDTH, self.world
+        v, l, p = self.local.export_new()
+        ha, hl, hp = self.local.hooked_exported()
+        own = part_owner(v, world) if len(v) else np.zeros(0, np.int64)
+        order = np.argsort(own, kind="stable")
+        send = torch.from_numpy(np.stack([v, l, p], 1)[order].astype(np.int64).reshape(-1, W).copy())
+        scounts = torch.from_numpy(np.bincount(own, minlength=world).astype(np.int64))
+        rcounts = torch.empty(world, dtype=torch.int64)
+        dist.all_to_all_single(rcounts, scounts, group=self.group)
+        recv = torch.empty((int(rcounts.sum()), W), dtype=torch.int64)
+        dist.all_to_all_single(recv, send, output_split_sizes=rcounts.tolist(),
+                               input_split_sizes=scounts.tolist(), group=self.group)
+        pairs = set(zip(ha.tolist(), hl.tolist(), hp.tolist()))
+        for x, lab, par in recv.tolist():
+            a = self.anchor.get(x)
+            if a is None:
+                self.anchor[x] = (lab, par)
+            elif lab != a[0]:
+                pairs.add((a[0], lab, par ^ a[1]))
+            elif par != a[1]:
+                self.odd = True
+        self.rows_owned += len(recv)
+        mine = torch.tensor(sorted(pairs), dtype=torch.int64).reshape(-1, W)
+        word = len(mine) | (FAIL_BIT if (self.odd or self.local.failed()) else 0)
+        words = [torch.empty(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(words, torch.tensor([word], dtype=torch.int64), group=self.group)
+        live = [int(w) & (FAIL_BIT - 1) for w in words]
+        rows = max(1, max(live))
+        pad = torch.zeros((rows, W), dtype=torch.int64)
+        pad[:len(mine)] = mine
+        parts = [torch.empty((rows, W), dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(parts, pad, group=self.group)
+        for r in range(world):
+            if int(words[r]) & FAIL_BIT:
+                self.forest.fail()
+            for a, b, w in parts[r][:live[r]].tolist():
+                self.forest.fold(a, b, w)
+        self.pairs_folded += sum(live)
+        self.combines += 1
+
+    def ok(self):
+        return not self.forest.failed()
+
+    def labels(self):
+        """This rank's owned (v, label, parity), sorted by v."""
+        import numpy as np
+        vs = sorted(self.anchor)
+        lab, par = [], []
+        for x in vs:
+            a, pa = self.anchor[x]
+            f = self.forest.find(a)
+            root, pr = f if f is not None else (a, 0)
+            lab.append(root)
+            par.append(pa ^ pr)
+        return np.array(vs, np.int64), np.array(lab, np.int64), np.array(par, np.int64)
