@@ -772,7 +772,8 @@ class PartGroup:
     def phase_stats(self):
         out = (ctypes.c_double * 8)()
         _check(lib().gs_group_part_phase_stats(self._g, out))
-        keys = ("own_fold_ms", "export_ms", "bucket_ms", "alltoall_ms", "owner_ms", "pairs_ms", "combines")
+        keys = ("own_fold_ms", "export_ms", "bucket_ms", "alltoall_ms", "owner_ms", "pair_gather_ms", "forest_fold_ms",
+                "combines")
         return dict(zip(keys, list(out)))
 
     def close(self):

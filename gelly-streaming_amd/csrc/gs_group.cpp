@@ -1054,8 +1054,8 @@ int gs_group_part_combine(gs_group_t g) {
   gs::launch_part_count_word(g->pdev + 3, sign ? h->ctr + gs::ctr_index(gs::CTR_FAIL) : nullptr,
                              sign ? g->pflags + 1 : nullptr, g->pdev + 4, st);
   GS_HIP(hipGetLastError());
-  ph_end(g, 4, p3, st);
   // 6. every rank's pairs into every rank's label forest
+  ph_end(g, 4, p3, st);
   hipEvent_t p4 = ph_begin(g, st);
   r = g->api.all_gather(g->pdev + 4, words, 1, kNcclInt64, g->comm_c, st);
   if (r) return rccl_fail(&g->api, "ncclAllGather(pair counts)", r);
@@ -1076,8 +1076,10 @@ int gs_group_part_combine(gs_group_t g) {
   r = g->api.all_gather(g->pairs, g->pairs_all, rows * W, kNcclInt64, g->comm_d, st);
   if (r) return rccl_fail(&g->api, "ncclAllGather(label pairs)", r);
   GS_HIP(hipEventRecord(g->pev, st));
+  ph_end(g, 5, p4, st);
   gs_summary* G = g->G;
   GS_HIP(hipStreamWaitEvent(G->stream, g->pev, 0));
+  hipEvent_t p5 = ph_begin(g, G->stream);
   FoldSource fs;
   fs.rows = (uint32_t)rows;
   fs.skip_rank = -1;
@@ -1086,10 +1088,10 @@ int gs_group_part_combine(gs_group_t g) {
   const uint8_t* w = W == 3 ? reinterpret_cast<const uint8_t*>(g->pairs_all + 2) : nullptr;
   if (int rc = fold_device_impl(G, g->pairs_all, g->pairs_all + 1, w, (size_t)N * rows, W, 8 * W, false, true, fs))
     return rc;
+  ph_end(g, 6, p5, G->stream);
   // the next combine reuses pairs_all and the words only after this fold
   GS_HIP(hipEventRecord(g->pev, G->stream));
   GS_HIP(hipStreamWaitEvent(st, g->pev, 0));
-  ph_end(g, 5, p4, st);
   g->combines++;
   g->rows_exported += total;
   g->rows_owned += total_recv;
@@ -1132,6 +1134,7 @@ int gs_group_part_reset(gs_group_t g) {
   if (int rc = gs_reset(g->G)) return rc;
   if (int rc = part_init_tables(g)) return rc;
   g->cap_seen = h->cap;
+  g->combines = g->rows_exported = g->rows_owned = g->pairs_sent = g->pairs_folded = 0;  // per pass
   return GS_OK;
 }
 
@@ -1156,9 +1159,8 @@ int gs_group_part_phase_stats(gs_group_t g, double* out8) {
   if (!out8) return fail(GS_ERR_INVALID, "out is null");
   DeviceGuard dg(g->h->device);
   ph_drain(g);
-  for (int i = 0; i < 6; ++i) out8[i] = g->ph_ms[i];
-  out8[6] = (double)g->ph_exchanges;
-  out8[7] = 0;
+  for (int i = 0; i < 7; ++i) out8[i] = g->ph_ms[i];
+  out8[7] = (double)g->ph_exchanges;
   return GS_OK;
 }
 

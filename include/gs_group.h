@@ -170,14 +170,16 @@ int gs_group_part_combine(gs_group_t g);
 int gs_group_part_labels_device(gs_group_t g, int64_t* v, int64_t* label, uint8_t* parity, size_t cap, size_t* n);
 /* The global bipartiteness verdict after the last combine (every rank's, AND-ed). */
 int gs_group_part_status(gs_group_t g, int* ok);
-/* Empty local forest, owner table and label forest (the next pass). Not collective. */
+/* Empty local forest, owner table and label forest, statistics zeroed (the next pass).
+ * Not collective. */
 int gs_group_part_reset(gs_group_t g);
-/* out8: combines, rows exported, rows owned (received), label pairs sent, label pairs folded
- * (all ranks), label-forest vertices, owner-table slots, 0. */
+/* out8 (since create or the last reset): combines, rows exported, rows owned (received), label
+ * pairs sent, label pairs folded (all ranks), label-forest vertices, owner-table slots, 0. */
 int gs_group_part_stats(gs_group_t g, uint64_t* out8);
 /* With gs_group_set_phase_timing on, device ms per phase since: out8[0] own folds (handle
  * stream only), [1] export + records, [2] bucketing, [3] count + row all-to-all, [4] owner
- * step, [5] pair all-gather + label-forest fold, [6] combines, [7] 0. */
+ * step, [5] pair-count + pair all-gathers, [6] label-forest fold, [7] combines. The
+ * collective phases [3], [5] include the wait for the other ranks. */
 int gs_group_part_phase_stats(gs_group_t g, double* out8);
 
 int gs_group_destroy(gs_group_t g);

@@ -78,6 +78,9 @@ std::mutex g_token;
 thread_local bool t_token = false;
 void token_release() {
   if (g_serialize && t_token) {
+    // this rank's queued device work (every stream) finishes before another rank runs: the
+    // other ranks are idle (they synchronised when they released the token)
+    (void)hipDeviceSynchronize();
     t_token = false;
     g_token.unlock();
   }

@@ -110,6 +110,7 @@ def main():
                     fold_ms += (time.perf_counter() - t0) * 1e3
                     g.combine()
                 ph = g.phase_stats()
+                torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 cap = 4 * (V // N) + (1 << 20)
                 ov = torch.empty(cap, dtype=torch.int64, device=dev)
@@ -141,13 +142,19 @@ def main():
     digest = sum(x["digest"] for x in res) & ((1 << 64) - 1)
     width_b = 16
     rows = []
+    max_pairs = max(x["pairs_sent"] for x in res)
     for x in res:
-        # all-to-all priced at the link rate: this rank's rows to the other N-1 owners, one link each
+        # the collectives priced at the link rate (the emulation's phases [3], [5] wait for the
+        # other ranks): this rank's rows to the N-1 other owners, one link each, and the pair
+        # all-gather (every rank sends its max-count-padded pairs to every other rank)
         sent_b = x["rows_exported"] * width_b
         a2a_model = (sent_b / max(N, 1)) / (a.link_gbs * 1e9) * 1e3 if N > 1 else 0.0
-        comp = x["export_ms"] + x["bucket_ms"] + x["owner_ms"] + x["pairs_ms"]
+        gather_model = (max_pairs * width_b) / (a.link_gbs * 1e9) * 1e3 if N > 1 else 0.0
+        comp = x["export_ms"] + x["bucket_ms"] + x["owner_ms"] + x["forest_fold_ms"]
         x["a2a_model_ms"] = a2a_model
-        x["rank_ms"] = x["own_fold_ms"] + comp + a2a_model + x["labels_ms"]
+        x["pair_gather_model_ms"] = gather_model
+        x["combine_compute_ms"] = comp
+        x["rank_ms"] = x["own_fold_ms"] + comp + a2a_model + gather_model + x["labels_ms"]
         rows.append(x)
     tmax = max(x["rank_ms"] for x in rows)
     summary = {
