@@ -932,7 +932,7 @@ int gs_group_create_partitioned(gs_group_t* out, gs_handle h, const void* id, in
   if (int rc = gs_create(&g->G, h->device, h->kind, std::max<uint64_t>(vertices_hint / 64, 1u << 12)))
     return bail(rc);
   uint64_t ocap = 1024;
-  while (ocap < 4 * (vertices_hint / (uint64_t)nranks + 256)) ocap <<= 1;
+  while (ocap < 4 * (vertices_hint / (uint64_t)nranks)) ocap <<= 1;  // load <= 1/4 at the hinted count
   if (ocap > (1ull << 31)) return bail(fail(GS_ERR_INVALID, "vertices_hint too large for the owner table"));
   g->ot.cap = (uint32_t)ocap;
   g->ot.mask = (uint32_t)(ocap - 1);

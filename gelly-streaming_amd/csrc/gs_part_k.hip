@@ -19,7 +19,6 @@ namespace {
 constexpr uint32_t kPartBS = 256;
 constexpr int kPartPer = (int)(kPartRowsPB / kPartBS);  // rows per thread (8)
 constexpr uint32_t kRootCache = 256;                    // LDS: roots this block has confirmed
-constexpr uint32_t kDedup = 2048;                       // LDS: label pairs this block has emitted
 
 __device__ __forceinline__ uint64_t part_prefix(const Table& t, const uint32_t* mark, const uint32_t* snap, int full,
                                                 uint32_t* lm, uint64_t* pre) {
@@ -343,20 +342,26 @@ __device__ __forceinline__ uint32_t owner_insert(const OwnerTable& ot, int64_t v
 
 // The owner step: every received row (v, l[, p]) claims or reads v's anchor; a row whose
 // label differs from the anchor (or, signed, whose parity does) becomes the label pair
-// (anchor, l, p ^ parity(anchor)). Pairs are deduplicated per block in LDS (a claimed
-// entry's pair is written by its claimer before it is marked ready, so a pair is only ever
-// dropped as the copy of one that was emitted). A row whose label equals the anchor with
-// the other parity is an odd cycle: `fail`.
+// (anchor, l, p ^ parity(anchor)). A row whose label equals the anchor with the other
+// parity is an odd cycle: `fail`. The block collects its pairs in an LDS table keyed by a
+// hash of the pair: per round of 256 rows the claimers of empty entries write theirs, a
+// block barrier, then a pair that finds its own entry is a repeat (dropped) and one that
+// finds another pair there goes out at once; the table's pairs go out at the block's end
+// with ONE reservation (the giant component's (anchor, label) pairs repeat thousands of
+// times per block: one append atomic per pair would queue on a single address).
+constexpr uint32_t kOwnerTab = 1024;
 template <bool SIGNED>
 __global__ __launch_bounds__(kPartBS) void k_part_owner(OwnerTable ot, const int64_t* __restrict__ rows, uint64_t nrows,
                                                         int width, int64_t* pairs, unsigned long long* npairs,
                                                         uint64_t pair_cap, uint32_t* fail) {
-  __shared__ uint32_t dflag[kDedup];
-  __shared__ int64_t da[kDedup], db[kDedup];
-  for (uint32_t i = threadIdx.x; i < kDedup; i += kPartBS) dflag[i] = 0;
+  __shared__ uint32_t dflag[kOwnerTab];  // 0 empty, 1 claimed, 2 | w << 2 ready
+  __shared__ int64_t da[kOwnerTab], db[kOwnerTab];
+  __shared__ uint32_t lwave[kPartBS / 64];
+  __shared__ unsigned long long lbase;
+  for (uint32_t i = threadIdx.x; i < kOwnerTab; i += kPartBS) dflag[i] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kPartRowsPB;
-  for (int j = 0; j < kPartPer; ++j) {  // wave-uniform
+  for (int j = 0; j < kPartPer; ++j) {  // block-uniform
     const uint64_t i = base + (uint64_t)j * kPartBS + threadIdx.x;
     const bool valid = i < nrows;
     int64_t v = 0, l = 0;
@@ -411,23 +416,58 @@ __global__ __launch_bounds__(kPartBS) void k_part_owner(OwnerTable ot, const int
         has = true;
       }
     }
-    // block dedup: drop an exact repeat of a pair this block has emitted
+    uint32_t e = 0;
+    bool mine = false;
     if (has) {
       const unsigned long long hsh =
           ((unsigned long long)A * 0x9E3779B97F4A7C15ull) ^ ((unsigned long long)l * 0xC2B2AE3D27D4EB4Full) ^ w;
-      const uint32_t e = (uint32_t)(hsh >> 40) & (kDedup - 1);
-      const uint32_t f = atomicCAS(&dflag[e], 0u, 1u);
-      if (f == 0u) {
+      e = (uint32_t)(hsh >> 40) & (kOwnerTab - 1);
+      if (atomicCAS(&dflag[e], 0u, 1u) == 0u) {
         da[e] = A;
         db[e] = l;
-        __threadfence_block();
-        atomicExch(&dflag[e], 2u | (w << 2));
-      } else {
-        const uint32_t g = __hip_atomic_load(&dflag[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if ((g & 3u) == 2u && (g >> 2) == w && da[e] == A && db[e] == l) has = false;
+        dflag[e] = 2u | (w << 2);
+        mine = true;
       }
     }
-    append_pair(has, A, l, w, pairs, width, npairs, pair_cap);
+    __syncthreads();  // every claimed entry of this round is ready
+    bool direct = false;
+    if (has && !mine) {
+      const uint32_t g = dflag[e];
+      direct = !((g >> 2) == w && da[e] == A && db[e] == l);  // another pair holds the entry
+    }
+    append_pair(direct, A, l, w, pairs, width, npairs, pair_cap);
+  }
+  __syncthreads();
+  // the table's pairs: one reservation per block
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t cnt = 0;
+  for (uint32_t q = threadIdx.x; q < kOwnerTab; q += kPartBS) cnt += (dflag[q] & 3u) == 2u;
+  uint32_t x = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) lwave[wid] = x;
+  __syncthreads();
+  uint32_t wb = 0, tot = 0;
+  for (int q = 0; q < (int)(kPartBS / 64); ++q) {
+    if (q < wid) wb += lwave[q];
+    tot += lwave[q];
+  }
+  if (threadIdx.x == 0) lbase = tot ? atomicAdd(npairs, (unsigned long long)tot) : 0ull;
+  __syncthreads();
+  uint64_t pos = lbase + wb + (x - cnt);
+  for (uint32_t q = threadIdx.x; q < kOwnerTab; q += kPartBS) {
+    const uint32_t f = dflag[q];
+    if ((f & 3u) != 2u) continue;
+    if (pos < pair_cap) {
+      int64_t* r = pairs + pos * (uint64_t)width;
+      r[0] = da[q];
+      r[1] = db[q];
+      if (width == 3) r[2] = (int64_t)(f >> 2);
+    }
+    ++pos;
   }
 }
 
