@@ -104,6 +104,17 @@ def _as_i64(u):
     return u - (1 << 64) if u >= (1 << 63) else u
 
 
+def slice_digest_checks(part_digest, world, expected, device):
+    """Self-check of the partitioned line: the digests (gs_digest's terms) of the ranks' owned
+    slices, summed mod 2^64 over ranks, must equal the single-GPU summary's committed digest:
+    the slices together are exactly its (v, label) set."""
+    t = torch.tensor([_as_i64(part_digest)], dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(t)  # int64 sums wrap mod 2^64
+    d = int(t.item()) & ((1 << 64) - 1)
+    return {"digest": "%016x" % d, "owned_slices_digest_equals_single_gpu": None if expected is None else d == expected}
+
+
 def replica_digest_checks(digest, world, expected, device):
     """Self-check of an N-rank line, outside the timed region: every
     replica's gs_digest (order-independent digest of its full (v, label) set) must be the
@@ -165,6 +176,11 @@ def parse():
                         "environment before anything initialises HIP or RCCL, inherited by every rank; reported in "
                         "config.rccl. RCCL's collective kernels run beside the fold lanes and hold CU slots the "
                         "folds need (DESIGN.md section 5)")
+    p.add_argument("--combine", choices=["replica", "partitioned"], default="replica",
+                   help="N > 1 (or --exchange): replicated forests kept equal by delta all-gathers (DESIGN.md section 5), "
+                        "or local forests with the owner-partitioned label combine (section 5b)")
+    p.add_argument("--part-window-log2", type=int, default=0,
+                   help="partitioned combine: own edges per rank between combines (log2; 0 = one combine per pass)")
     p.add_argument("--exchange-impl", choices=["native", "torch"], default="native",
                    help="native: RCCL inside libgs_summary (gs_group_*); torch: torch.distributed all-gather")
     p.add_argument("--er-mode", choices=["launch", "server"], default="server",
@@ -257,6 +273,29 @@ def launch_check(args):
         if checks is not None:
             line["self_check"] = checks
         print(json.dumps(line), flush=True)
+
+
+class PartExchange:
+    """bench adapter of the owner-partitioned group (gs_group_create_partitioned, DESIGN.md
+    section 5b): each rank folds its shard into its LOCAL forest (pipelined micro-batches),
+    combines at every window end (window 0: once, at the end of the pass) and emits its owned
+    slice of the label pass."""
+
+    def __init__(self, group, summary, window):
+        self.g = group
+        self.s = summary
+        self.window = window
+
+    def run(self, src, dst, n, batch):
+        self.g.reset()
+        step = self.window or n
+        for w0 in range(0, n, step):
+            for o in range(w0, min(n, w0 + step), batch):
+                self.g.fold_device(src[o:], dst[o:], min(batch, n - o, w0 + step - o))
+            self.g.combine()
+
+    def labels(self, out_v, out_l):
+        return self.g.labels_device(out_v, out_l)
 
 
 class NativeExchange:
@@ -821,7 +860,8 @@ def main():
 
     E = (1 << args.scale) * args.edge_factor
     grouped = world > 1 or args.exchange
-    B = 1 << (args.exchange_log_batch if grouped else args.log_batch)
+    part = grouped and args.combine == "partitioned"
+    B = 1 << (args.exchange_log_batch if grouped and not part else args.log_batch)
     per = E // world
     start = rank * per
     nbatch = (per + B - 1) // B
@@ -838,7 +878,15 @@ def main():
     out_v = torch.empty(vcap, dtype=torch.int64, device=dev)
     out_l = torch.empty(vcap, dtype=torch.int64, device=dev)
     xch = None
-    if world > 1 or args.exchange:
+    if part:
+        uid = [gs.group_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        pwin = (1 << args.part_window_log2) if args.part_window_log2 else 0
+        xch = PartExchange(gs.PartGroup(summ, uid[0], world, rank, 1 << (args.capacity_log2 or xlog), pwin), summ,
+                           pwin)
+        if args.pipeline > 1 and not pwin:
+            summ.set_pipelining(args.pipeline)
+    elif world > 1 or args.exchange:
         if args.exchange_impl == "native":
             uid = [gs.group_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
@@ -852,6 +900,10 @@ def main():
     nlabels = [0]
 
     def one_step():
+        if isinstance(xch, PartExchange):  # (reset inside: local forest, owner table, label forest)
+            xch.run(src, dst, per, B)
+            nlabels[0] = xch.labels(out_v, out_l)
+            return
         summ.reset()
         if isinstance(xch, NativeExchange):
             xch.run(src, dst, per, B)
@@ -897,7 +949,7 @@ def main():
             summ.set_profiling(False)
             print(json.dumps({"serial_pass_fold_launches": int(nf), "fold_avg_us": round(fold_ms * 1e3 / max(nf, 1), 2)}),
                   flush=True)
-        if isinstance(xch, NativeExchange):
+        if isinstance(xch, (NativeExchange, PartExchange)):
             xch.g.close()
         summ.close()
         if dist.is_initialized():
@@ -910,9 +962,13 @@ def main():
     # every replica's (v, label) set -- not only its size -- against the single-GPU
     # summary's committed digest
     stream_key = "rmat%d-ef%d-seed%#x" % (args.scale, args.edge_factor, args.seed)
-    checks.update(replica_digest_checks(summ.digest(), world, KNOWN_DIGESTS.get(stream_key), dev))
+    if isinstance(xch, PartExchange):
+        checks.update(slice_digest_checks(gs.digest_rows(out_v[:labelled], out_l[:labelled]), world,
+                                          KNOWN_DIGESTS.get(stream_key), dev))
+    else:
+        checks.update(replica_digest_checks(summ.digest(), world, KNOWN_DIGESTS.get(stream_key), dev))
     checks["digest_stream"] = stream_key
-    if isinstance(xch, NativeExchange):  # the world RCCL formed (ncclCommCount of both communicators)
+    if isinstance(xch, (NativeExchange, PartExchange)):  # the world RCCL formed (ncclCommCount, both communicators)
         cc, dc = xch.g.comm_ranks()
         checks["rccl_comm_ranks"] = [cc, dc]
         checks["rccl_world_ok"] = cc == dc == world
@@ -920,13 +976,13 @@ def main():
         c = torch.tensor([labelled], dtype=torch.int64, device=dev)
         dist.all_reduce(c)
         labelled = int(c.item())
-        # every replica holds the same vertex count, and the slices cover it exactly
-        nv = summ.num_vertices()
-        lo = torch.tensor([nv], dtype=torch.int64, device=dev)
-        hi = torch.tensor([nv], dtype=torch.int64, device=dev)
-        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-        checks["replicas_same_vertex_count"] = int(lo.item()) == int(hi.item()) == labelled
+        if not part:  # every replica holds the same vertex count, and the slices cover it exactly
+            nv = summ.num_vertices()
+            lo = torch.tensor([nv], dtype=torch.int64, device=dev)
+            hi = torch.tensor([nv], dtype=torch.int64, device=dev)
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            checks["replicas_same_vertex_count"] = int(lo.item()) == int(hi.item()) == labelled
     else:  # the label pass covers every distinct endpoint of the stream (4 slices of the id space)
         distinct = 0
         for lo_bits in range(4):
@@ -986,6 +1042,25 @@ def main():
     # step with timing events around each phase (gs_group_set_phase_timing): the N > 1
     # line explains its own scaling. Max over ranks.
     phases = None
+    if isinstance(xch, PartExchange) and not args.profile_only:
+        xch.g.set_phase_timing(True)
+        t0p = time.perf_counter()
+        one_step()
+        summ.sync()
+        pstep = time.perf_counter() - t0p
+        ps = xch.g.phase_stats()
+        stp = xch.g.stats()
+        xch.g.set_phase_timing(False)
+        keys = sorted(k for k in ps if k not in ("combines", "own_fold_ms"))
+        vals = torch.tensor([ps[k] for k in keys] + [pstep * 1e3], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+        phases = {k: round(float(v), 3) for k, v in zip(keys + ["step_ms"], vals.tolist())}
+        phases.update({"combines_per_rank": int(ps["combines"]), "rows_exported_rank0": stp["rows_exported"],
+                       "rows_owned_rank0": stp["rows_owned"], "pairs_folded": stp["pairs_folded"],
+                       "label_forest_vertices": stp["label_forest_vertices"],
+                       "note": "max over ranks, one untimed step with HIP timing events around every combine phase; "
+                               "alltoall and pair_gather include the wait for the other ranks"})
     if isinstance(xch, NativeExchange) and not args.profile_only:
         xch.g.set_phase_timing(True)
         t0p = time.perf_counter()
@@ -1092,19 +1167,24 @@ def main():
                        "combine_every_edges_per_gpu": 1 << args.exchange_log_batch,
                        "combine_ramp": {"first_edges_per_gpu": 1 << args.ramp_log2 if args.ramp_log2 else 0,
                                         "every": 1 << args.ramp_log_batch},
-                       "combine": "delta exchange (native RCCL group)" if grouped else "none at 1 GPU (same cadence)",
+                       "combine": ("owner-partitioned label combine (native RCCL group), %s" % (
+                           "every 2^%d own edges" % args.part_window_log2 if args.part_window_log2 else
+                           "once per pass") if part else
+                                   "delta exchange (native RCCL group)" if grouped else "none at 1 GPU (same cadence)"),
                        "ids": "sparse 64-bit (scrambled)",
                        "capacity_hint": 1 << (args.capacity_log2 or xlog),
                        "vertices_labelled": int(labelled), "self_check": checks, "exchange_phases": phases,
                        "pcie_inclusive": pcie,
                        "rccl": rccl_setting() if grouped else None,
-                       "parallelism": ("edge-shard x%d, per-batch delta all-gather (%s)" % (world, args.exchange_impl))
+                       "parallelism": ("edge-shard x%d, local forests + owner all-to-all + label-pair all-gather"
+                                       % world if part else
+                                       "edge-shard x%d, per-batch delta all-gather (%s)" % (world, args.exchange_impl))
                        if xch is not None else "single GPU"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if isinstance(xch, NativeExchange):
+    if isinstance(xch, (NativeExchange, PartExchange)):
         xch.g.close()
     summ.close()
     if dist.is_initialized():

@@ -202,6 +202,26 @@ def create_bytes(kind, capacity_hint):
     return b.value
 
 
+def digest_rows(v, label, parity=None):
+    """gs_digest's order-independent terms (csrc/gs_kernels.hip digest_term) summed over rows
+    of device tensors, mod 2^64: the owned slices of a partitioned group sum to the digest of
+    the single summary of the same stream."""
+    import torch
+
+    def srl(x, k):  # logical shift right on int64 tensors
+        return (x >> k) & ((1 << (64 - k)) - 1)
+
+    def mix(z):
+        z = (z ^ srl(z, 30)) * -4658895280553007687  # 0xBF58476D1CE4E5B9 as int64
+        z = (z ^ srl(z, 27)) * -7723592293110705685  # 0x94D049BB133111EB
+        return z ^ srl(z, 31)
+    if v.numel() == 0:
+        return 0
+    a = mix(v ^ 0x243F6A8885A308D3)
+    b = mix(label + (parity.to(torch.int64) * 0x13198A2E03707344 if parity is not None else 0))
+    return int(torch.sum(a * b).item()) & ((1 << 64) - 1)
+
+
 # ---------------------------------------------------------------- test controls
 # include/gs_testing.h: private knobs the tests use (the product reads no environment)
 TESTING_KNOBS = {"server_idle_us": 0, "changes_walk_max": 1, "parse_lb_timeout_us": 2, "group_self_apply": 3,
@@ -755,6 +775,12 @@ class PartGroup:
         o = ctypes.c_int()
         _check(lib().gs_group_part_status(self._g, ctypes.byref(o)))
         return bool(o.value)
+
+    def comm_ranks(self):
+        """(ranks of the count communicator, ranks of the data communicator): ncclCommCount."""
+        c, d = ctypes.c_int(), ctypes.c_int()
+        _check(lib().gs_group_comm_ranks(self._g, ctypes.byref(c), ctypes.byref(d)))
+        return c.value, d.value
 
     def reset(self):
         _check(lib().gs_group_part_reset(self._g))

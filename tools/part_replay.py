@@ -30,21 +30,6 @@ import gsamd as gs  # noqa: E402
 SEED = {20: 0x5EED0020, 26: 0x5EED0026}
 
 
-def digest_rows(v, lab, par=None):
-    """gs_digest's term (csrc/gs_kernels.hip digest_term) summed over rows, mod 2^64."""
-    def srl(x, k):  # logical shift right on int64 tensors
-        return (x >> k) & ((1 << (64 - k)) - 1)
-
-    def mix_u(z):
-        z = (z ^ srl(z, 30)) * -4658895280553007687  # 0xBF58476D1CE4E5B9 as int64
-        z = (z ^ srl(z, 27)) * -7723592293110705685  # 0x94D049BB133111EB
-        return z ^ srl(z, 31)
-    a = mix_u(v ^ 0x243F6A8885A308D3)
-    k2 = 0x13198A2E03707344
-    b = mix_u(lab + (par.to(torch.int64) * k2 if par is not None else 0))
-    return int(torch.sum(a * b).item()) & ((1 << 64) - 1)
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", type=int, default=8)
@@ -119,7 +104,7 @@ def main():
                 labels_ms = (time.perf_counter() - t0) * 1e3
                 st = g.stats()
                 out = {"rank": r, "own_fold_ms": fold_ms, "labels_ms": labels_ms, **ph, **st, "owned": k}
-                out["digest"] = digest_rows(ov[:k], ol[:k])
+                out["digest"] = gs.digest_rows(ov[:k], ol[:k])
                 del ov, ol
             g.close()
             s.close()
