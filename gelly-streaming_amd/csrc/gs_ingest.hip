@@ -6,7 +6,7 @@
 //
 // Two launches + one scan, all HBM-streaming:
 //   k_count_lines : per 16 KiB tile, the number of '\n' (coalesced 16-B loads)
-//   exclusive scan of the tile counts (hipcub) -> '\n' before each tile
+//   k_tile_scan   : exclusive scan of the tile counts (one block) -> '\n' before each tile
 //   k_parse       : per tile, the tile (+ 512 B of the next) is staged in LDS; every
 //                   thread owns 64 bytes, finds the line starts in them (byte after a
 //                   '\n') and their ends ('\n' masks of its and the next two segments
@@ -18,7 +18,7 @@
 // with a per-character parse of compacted line starts, 592 us with the SWAR parse, 370 us
 // with lines parsed by the thread whose 32-byte segment they start in (no start list),
 // 338-354 us with 16 KiB tiles (five 16-B loads in flight per thread instead of three).
-#include <hipcub/hipcub.hpp>
+#include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
@@ -727,6 +727,35 @@ __device__ __forceinline__ void parse_tile(const uint8_t* __restrict__ text, uin
   }
 }
 
+// Exclusive scan of the tiles' '\n' counts (the two-pass path): one block walks the tiles in
+// rounds of 1024 with a wave scan + the wave totals, carrying the sum.
+__global__ __launch_bounds__(1024) void k_tile_scan(const uint64_t* __restrict__ cnt, uint64_t* __restrict__ pre,
+                                                    uint64_t n) {
+  __shared__ unsigned long long wsum[16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long carry = 0;
+  for (uint64_t c0 = 0; c0 < n; c0 += 1024) {
+    const uint64_t i = c0 + threadIdx.x;
+    const unsigned long long v = i < n ? cnt[i] : 0ull;
+    unsigned long long x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    unsigned long long wb = 0, tot = 0;
+    for (int q = 0; q < 16; ++q) {
+      if (q < wid) wb += wsum[q];
+      tot += wsum[q];
+    }
+    if (i < n) pre[i] = carry + wb + (x - v);
+    carry += tot;
+    __syncthreads();
+  }
+}
+
 // {line count, first malformed line (~0: none)} of a parsed text; with `host` (mapped
 // memory) also host[1..2] = the same two words and then host[0] = seq (system-scope
 // release): the caller spins on that word instead of a copy and a stream synchronisation
@@ -844,9 +873,7 @@ int parse_text_enqueue(hipStream_t st, const char* text, size_t len, int sep, in
   }
   hipLaunchKernelGGL(k_count_lines, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, s.tile_cnt, aligned,
                      (uint64_t)0);
-  size_t tmp = s.cub_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(s.cub_tmp, tmp, s.tile_cnt, s.tile_pre, (int)tiles, st) != hipSuccess)
-    return -1;
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, st, s.tile_cnt, s.tile_pre, tiles);
   if (hipMemsetAsync(s.bad, 0xFF, 8, st) != hipSuccess) return -1;
   hipLaunchKernelGGL(k_parse, dim3((unsigned)tiles), dim3(256), 0, st, t, (uint64_t)len, sep, s.tile_pre, src, dst,
                      (uint64_t)cap, s.bad, aligned, (uint64_t)0);
@@ -870,8 +897,7 @@ int parse_text(hipStream_t st, const char* text, size_t len, int sep, int64_t* s
 
 size_t parse_scratch_bytes(size_t max_len, size_t* cub_bytes) {
   const uint64_t tiles = (max_len + kTile - 1) / kTile + 1;
-  size_t tmp = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (uint64_t*)nullptr, (uint64_t*)nullptr, (int)tiles);
+  const size_t tmp = 0;  // (no library scan scratch: k_tile_scan)
   *cub_bytes = tmp;
   return tiles * 16 + 48 + tmp + 256;
 }

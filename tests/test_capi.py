@@ -62,6 +62,7 @@ def test_product_library_reads_no_environment_knob(gs):
         blob = f.read()
     found = sorted(set(re.findall(rb"GS_[A-Z0-9_]{4,}", blob)))
     assert not found, found
+    assert b"getenv" not in blob  # no environment read at all (the parse's scan is our own kernel)
 
 
 def test_testing_knobs_roundtrip(gs):
