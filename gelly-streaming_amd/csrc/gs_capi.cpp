@@ -338,10 +338,13 @@ int ensure_capacity(gs_summary* h, size_t n) {
   // for reports below is then only back-pressure with enough folds queued to keep the
   // GPU busy, instead of a drain before every fold (RMAT-20, config 2: 1.07 -> 0.72
   // ms/step).
-  const uint64_t slack = 2ull * n * (uint64_t)(std::max({1, h->pipe_depth, h->group_lanes}) + 1);
+  // (x 2: a chunk's report rides on the next launch of its stream, one more chunk per lane)
+  const uint64_t slack = 2ull * n * (uint64_t)(2 * std::max({1, h->pipe_depth, h->group_lanes}) + 2);
   const bool slack_grow = h->cap < kSlackGrowMaxCap && (double)(h->nv_exact + slack) > limit;
   if (!slack_grow) {
-    // wait for reports of the folds in flight (the GPU keeps working: no drain)
+    // wait for reports of the folds in flight (the GPU keeps working: no drain); the
+    // chunks whose report rides on a later launch are reported now
+    if (int rc = flush_reports(h)) return rc;
     h->cap_waits++;
     const auto t0 = std::chrono::steady_clock::now();
     while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200)) {
@@ -534,6 +537,43 @@ bool use_vertex_list(gs_summary* h, uint64_t nv_bound) {
   return h->vlist_ok && nv_bound * 8 < h->cap;
 }
 
+// report stream index of a stream: 0 the handle stream, 1.. the lanes, last the side stream
+int report_stream(const gs_summary* h, hipStream_t st) {
+  if (st == h->side && h->side) return gs_summary::kRepStreams - 1;
+  for (int i = 0; i < gs_summary::kLanes; ++i)
+    if (st == h->lane[i] && h->lane[i]) return 1 + i;
+  return 0;
+}
+
+hipStream_t report_stream_of(const gs_summary* h, int rs) {
+  if (rs == gs_summary::kRepStreams - 1) return h->side;
+  if (rs >= 1) return h->lane[rs - 1];
+  return h->stream;
+}
+
+// a standalone k_report claiming stream rs's pending chunks (queued on that stream)
+int launch_report_now(gs_summary* h, int rs, hipStream_t st) {
+  const uint64_t claim = h->rep_pending[rs];
+  if (!claim) return GS_OK;
+  gs::launch_report(h->ctr, claim, h->rep_dev + (h->rep_seq++ % gs_summary::kRepRing), (unsigned)(h->rep_epoch & 7u),
+                    st);
+  GS_HIP(hipGetLastError());
+  h->rep_pending_edges -= claim;
+  h->rep_pending[rs] = 0;
+  return GS_OK;
+}
+
+// every stream's unclaimed chunks reported (before the host waits for reports)
+int flush_reports(gs_summary* h) {
+  for (int rs = 0; rs < gs_summary::kRepStreams; ++rs) {
+    if (!h->rep_pending[rs]) continue;
+    hipStream_t st = report_stream_of(h, rs);
+    if (!st) continue;
+    if (int rc = launch_report_now(h, rs, st)) return rc;
+  }
+  return GS_OK;
+}
+
 int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, const uint8_t* w, size_t n,
                      size_t stride, size_t w_stride, bool track, bool check_cap, const FoldSource& fs) {
   if (n == 0) return GS_OK;
@@ -650,41 +690,37 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       f.seq = *fs.take_seq = ++h->done_seq;
     }
     h->shard0 = (h->shard0 + blocks) & (gs::kShards - 1);
+    // Capacity reports. A report may only claim chunks queued before it on ITS stream
+    // (handle, lanes, side). Each launch carries the report of the earlier chunks of its
+    // stream (report_wave in block 0: no launch of its own -- config 2's folds were each
+    // followed by a 4-14 us k_report on their lane); the last chunks of a burst are claimed
+    // by the next launch there, or by flush_reports before a capacity wait.
+    const int rs = report_stream(h, st);
+    const bool carry = check_cap && units && !fs.take_out && !fs.n_dev && h->rep_pending[rs];
+    if (carry) {
+      f.rep_out = h->rep_dev + (h->rep_seq++ % gs_summary::kRepRing);
+      f.rep_claim = h->rep_pending[rs];
+      f.rep_epoch = (unsigned)(h->rep_epoch & 7u);
+    }
     {
       Prof p(h, KID_FOLD, st);
       gs::launch_fold(sign, track, h->table(), h->delta(), f, st);
     }
     GS_HIP(hipGetLastError());
+    if (carry) {
+      h->rep_pending_edges -= f.rep_claim;
+      h->rep_pending[rs] = 0;
+    }
     if (check_cap && units) {
-      // A report may only claim chunks queued before it on ITS stream. Every stream
-      // (handle, lanes, side) reports every kRepEvery-th chunk queued on it, claiming
-      // that stream's chunks since its previous report: a report is a launch, and
-      // host launch cost bounds the multi-GPU exchange loop. Unclaimed edges stay
-      // "in flight" in the bound, which is therefore always valid.
-      int rs = 0;
-      if (st == h->side) rs = gs_summary::kRepStreams - 1;
-      for (int i = 0; i < gs_summary::kLanes; ++i)
-        if (st == h->lane[i]) rs = 1 + i;
       const uint64_t cu = fs.rows ? (off + c >= n ? units : 0) : c;
       h->rep_pending[rs] += cu;
       h->rep_pending_edges += cu;
-      // off the handle stream a report is not a gap between folds: report every chunk
-      // while the bound is near the load limit (small tables), so no fold has to wait
-      // A counted replay (the row count lives on the device) charges its full capacity:
-      // it reports at once, so the bound drops to the real count as soon as it lands
-      // instead of carrying kRepEvery replays' worth of phantom vertices.
-      const bool tight = (rs != 0 && (double)(h->nv_ub + 4ull * gs_summary::kRepEvery * c) > kMaxLoad * (double)h->cap) ||
-                         fs.n_dev != nullptr;
-      // (a fused take is waited for: its caller takes the exact count instead)
-      if (!fs.take_out && (++h->rep_skip[rs] >= gs_summary::kRepEvery || tight)) {
-        const uint64_t claim = h->rep_pending[rs];
-        gs::launch_report(h->ctr, claim, h->rep_dev + (h->rep_seq++ % gs_summary::kRepRing),
-                          (unsigned)(h->rep_epoch & 7u), st);
-        GS_HIP(hipGetLastError());
-        h->rep_pending_edges -= claim;
-        h->rep_pending[rs] = 0;
-        h->rep_skip[rs] = 0;
-      }
+      // A counted replay (the row count lives on the device) charges its full capacity: it
+      // reports at once, so the bound drops to the real count as soon as it lands instead
+      // of carrying phantom vertices. (A fused take is waited for: its caller
+      // takes the exact count instead.)
+      if (fs.n_dev && !fs.take_out)
+        if (int rc = launch_report_now(h, rs, st)) return rc;
     }
   }
   return GS_OK;

@@ -255,6 +255,7 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
                      const FoldSource& fs = FoldSource());
 int join_lanes(gs_summary* h);
 bool side_ok(const gs_summary* h);
+int flush_reports(gs_summary* h);  // standalone capacity reports of every stream's unclaimed chunks
 int ensure_lanes(gs_summary* h, int n);  // create lane streams 0..n-1 on first use
 int read_nv(gs_summary* h, uint64_t* nv);
 // wait until every operation queued on h->stream so far has completed; *value

@@ -113,7 +113,32 @@ struct FoldArgs {
   unsigned long long* done;
   unsigned long long seq;
   bool server = false;  // resident window server: vertices carried by the tickets (take_tail)
+  // capacity report carried by this launch for the chunks queued before it on its stream
+  // (k_report's work in block 0's first wave: no launch of its own)
+  unsigned long long* rep_out = nullptr;
+  unsigned long long rep_claim = 0;
+  unsigned rep_epoch = 0;
 };
+
+// The capacity report (k_report below) by one wave: edges covered += n, then the
+// new-vertex count of the 64 shards and the covered edges into one host-mapped word.
+__device__ __forceinline__ void report_wave(uint32_t* ctr, unsigned long long n, unsigned long long* out,
+                                            unsigned epoch) {
+  unsigned long long done = 0;
+  if (threadIdx.x == 0)
+    done = atomicAdd(reinterpret_cast<unsigned long long*>(ctr + ctr_index(CTR_EDONE)), n) + n;
+  done = __shfl(done, 0, 64);
+  uint32_t c = threadIdx.x < (uint32_t)kShards
+                   ? __hip_atomic_load(ctr + ctr_index(CTR_NV + threadIdx.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : 0u;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (threadIdx.x == 0) {
+    const unsigned long long w = ((unsigned long long)c << 34) | ((unsigned long long)(epoch & 7u) << 31) |
+                                 (done & ((1ull << 31) - 1));
+    __hip_atomic_store(out, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 
 #ifndef GS_ROWS_TTAS
 #define GS_ROWS_TTAS 3  // other replicas' rows: re-read before the key CAS on both sides (experiment switch)
@@ -391,6 +416,8 @@ __global__ __launch_bounds__(kFoldBS) void k_fold(Table t, Delta D, FoldArgs a) 
       ((a.fail_in && __hip_atomic_load(a.fail_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ||
        (n_word & kFailBit)))
     atomicOr(&t.ctr[ctr_index(CTR_FAIL)], 1u);  // the verdict is the AND (Candidates.java:79-81)
+  // the report of the earlier chunks of this stream (complete: stream order)
+  if (a.rep_out && blockIdx.x == 0 && threadIdx.x < 64) report_wave(t.ctr, a.rep_claim, a.rep_out, a.rep_epoch);
   // a failed verdict is final: no more work (a TAKE block still reaches its ticket)
   const bool failed = SIGNED && __builtin_amdgcn_readfirstlane(t.ctr[ctr_index(CTR_FAIL)]) != 0;
   if (failed && !TAKE) return;
@@ -1162,6 +1189,9 @@ void launch_fold(bool sign, bool track, const Table& t, const Delta& D, const Fo
   FoldArgs a{f.src,       f.dst,    f.w,      f.n,       f.stride,   f.w_stride,  f.rows,
              f.skip_rank, f.counts, f.base,   f.n_dev,   f.fail_in,  f.shard0,    f.take_out,
              f.take_cap,  f.take_count, f.done, f.seq};
+  a.rep_out = f.rep_out;
+  a.rep_claim = f.rep_claim;
+  a.rep_epoch = f.rep_epoch;
   const dim3 g((f.n + kFoldBS - 1) / kFoldBS), b(kFoldBS);
   if (f.take_out) {  // fused window take (always tracked)
     if (sign) hipLaunchKernelGGL((k_fold<true, true, true>), g, b, 0, st, t, D, a);

@@ -29,6 +29,10 @@ struct FoldLaunch {
   unsigned long long* take_count = nullptr;
   unsigned long long* done = nullptr;
   unsigned long long seq = 0;
+  // the capacity report of the earlier chunks of this stream, carried by this launch
+  unsigned long long* rep_out = nullptr;
+  unsigned long long rep_claim = 0;
+  unsigned rep_epoch = 0;
 };
 
 // Resident window server (latency path, gs_set_window_server): the host posts each
