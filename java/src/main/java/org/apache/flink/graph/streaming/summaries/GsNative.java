@@ -68,4 +68,12 @@ final class GsNative {
 	static native void groupFinish(long g);
 	static native void groupTreeCombine(long g);
 	static native void groupDestroy(long g);
+	// owner-partitioned group (gs_group_create_partitioned, DESIGN.md section 5b): local forests,
+	// owned label slices; device addresses as longs
+	static native long groupCreatePartitioned(long h, byte[] id, int nranks, int rank, long verticesHint,
+			long windowEdges);
+	static native void groupPartFold(long g, long srcDev, long dstDev, long n);
+	static native void groupPartCombine(long g);
+	static native long groupPartLabels(long g, long vDev, long labelDev, long parityDev, long cap);
+	static native void groupPartReset(long g);
 }

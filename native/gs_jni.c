@@ -398,6 +398,51 @@ JNIEXPORT void JNICALL FN(groupTreeCombine)(JNIEnv* env, jclass c, jlong g) {
   CHECK(gs_group_tree_combine(G(g)));
 }
 
+/* owner-partitioned group (gs_group_create_partitioned): device addresses as longs */
+JNIEXPORT jlong JNICALL FN(groupCreatePartitioned)(JNIEnv* env, jclass c, jlong h, jbyteArray id, jint nranks,
+                                                   jint rank, jlong verticesHint, jlong windowEdges) {
+  (void)c;
+  if ((*env)->GetArrayLength(env, id) != GS_GROUP_ID_BYTES) {
+    throw_msg(env, "groupCreatePartitioned: id must be GS_GROUP_ID_BYTES long");
+    return 0;
+  }
+  jbyte buf[GS_GROUP_ID_BYTES];
+  (*env)->GetByteArrayRegion(env, id, 0, GS_GROUP_ID_BYTES, buf);
+  gs_group_t g = NULL;
+  if (gs_group_create_partitioned(&g, H(h), buf, nranks, rank, (uint64_t)verticesHint, (size_t)windowEdges) != GS_OK) {
+    throw_gs(env);
+    return 0;
+  }
+  return (jlong)(intptr_t)g;
+}
+
+JNIEXPORT void JNICALL FN(groupPartFold)(JNIEnv* env, jclass c, jlong g, jlong s, jlong d, jlong n) {
+  (void)c;
+  CHECK(gs_group_part_fold_device(G(g), (const int64_t*)(intptr_t)s, (const int64_t*)(intptr_t)d, (size_t)n));
+}
+
+JNIEXPORT void JNICALL FN(groupPartCombine)(JNIEnv* env, jclass c, jlong g) {
+  (void)c;
+  CHECK(gs_group_part_combine(G(g)));
+}
+
+JNIEXPORT jlong JNICALL FN(groupPartLabels)(JNIEnv* env, jclass c, jlong g, jlong v, jlong label, jlong parity,
+                                            jlong cap) {
+  (void)c;
+  size_t n = 0;
+  if (gs_group_part_labels_device(G(g), (int64_t*)(intptr_t)v, (int64_t*)(intptr_t)label, (uint8_t*)(intptr_t)parity,
+                                  (size_t)cap, &n) != GS_OK) {
+    throw_gs(env);
+    return 0;
+  }
+  return (jlong)n;
+}
+
+JNIEXPORT void JNICALL FN(groupPartReset)(JNIEnv* env, jclass c, jlong g) {
+  (void)c;
+  CHECK(gs_group_part_reset(G(g)));
+}
+
 JNIEXPORT void JNICALL FN(groupDestroy)(JNIEnv* env, jclass c, jlong g) {
   (void)env;
   (void)c;
