@@ -7,7 +7,7 @@
 //                -> count all-gather (communicator C, stream xc) -> k_headers: the
 //                   gathered counts in host-mapped memory
 //   then, still inside the call for exchange b, after fold b is queued, the DATA of
-//                exchange b-2 (data lag 2, the default; GS_GROUP_DATA_LAG 1..3):
+//                exchange b-2 (data lag 2; 1..3 through gs_testing_set(GS_TESTING_GROUP_DATA_LAG)):
 //                host reads b-2's counts (landed while fold b-1 ran) -> data all-gather
 //                of exactly max-count rows per rank (communicator D, stream xd) -> fold
 //                of the other ranks' live rows on the apply (side) stream, beside this

@@ -60,7 +60,7 @@ def test_group_fold_batches_native_loop(gs, oracle_mod, knobs):
 @pytest.mark.parametrize("inject", [(), (1 << 15,)])
 def test_group_signed_rows_self_apply(gs, oracle_mod, knobs, inject):
     """Signed summary in a group: 24-B rows {a, b, parity}; the rank folds its own
-    gathered rows back (GS_GROUP_SELF_APPLY) -- verdict and colouring must equal
+    gathered rows back (GS_TESTING_GROUP_SELF_APPLY) -- verdict and colouring must equal
     the truth."""
     import torch
     knobs(group_self_apply=1)

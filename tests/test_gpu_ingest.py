@@ -258,7 +258,7 @@ def test_parse_release_frees_the_cache_and_parses_again(gs, oracle_mod):
 def test_parse_lookback_fallback_counts_directly(gs, oracle_mod, offset, knobs):
     """a tile whose predecessors have not published within the look-back's timeout
     counts the '\\n' before it itself (16-byte loads across the wave, an unaligned head and
-    tail byte by byte). GS_PARSE_LB_TIMEOUT_US=0 makes every tile that finds an unpublished
+    tail byte by byte). GS_TESTING_PARSE_LB_TIMEOUT_US = 0 makes every tile that finds an unpublished
     predecessor take that path; the result is still the oracle's, for aligned and unaligned
     texts of many tiles."""
     rng = np.random.default_rng(17 + offset)

@@ -8,8 +8,8 @@ with the oracle's; on a mismatch the log answers, for every own-fold block whose
 edges name a missing vertex: was it dispatched at all, with which arguments, on which
 XCD, and what did its edges find.
 
-    GPU_MAX_HW_QUEUES=32 GS_GROUP_HIPRIO=1 GS_LIB_VARIANT=blocklog \\
-        python tools/lostwork_probe.py --ranks 8 --passes 4
+    make -C gelly-streaming_amd blocklog BLFLAGS=-DGS_GROUP_HIPRIO=1
+    GPU_MAX_HW_QUEUES=32 GS_LIB_VARIANT=blocklog python tools/lostwork_probe.py --ranks 8 --passes 4
 """
 import argparse
 import os
@@ -46,8 +46,7 @@ def main():
     import ctypes
     L.gs_debug_blocklog.argtypes = [ctypes.c_void_p, ctypes.c_ulonglong]
     L.gs_debug_blocklog_count.restype = ctypes.c_ulonglong
-    print("env: GPU_MAX_HW_QUEUES=%s GS_GROUP_HIPRIO=%s" % (os.environ.get("GPU_MAX_HW_QUEUES"),
-                                                             os.environ.get("GS_GROUP_HIPRIO")), flush=True)
+    print("env: GPU_MAX_HW_QUEUES=%s" % os.environ.get("GPU_MAX_HW_QUEUES"), flush=True)
     E, B, n = 16 << a.scale, 1 << a.log_batch, a.ranks
     src = torch.empty(E, dtype=torch.int64, device="cuda")
     dst = torch.empty(E, dtype=torch.int64, device="cuda")
