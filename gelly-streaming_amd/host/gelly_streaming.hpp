@@ -105,8 +105,10 @@ struct MapFunction {
 // at its release. A create of gs_create_bytes(hint) that would pass the budget first runs
 // set_budget's `collect` hook (System.gc() + System.runFinalization(): summaries a Flink
 // job dropped without release() come back through their finalizers), then destroys pooled
-// handles until it fits. The total then stays within the budget plus the table being
-// created, unless live summaries alone need more.
+// handles until it fits. Tables also grow in place (a reused pooled table inside the window's
+// fold), so any acquire that finds the device past the budget collects first, too, and trims
+// the pool back to it. The total then stays within the budget plus the table being created,
+// unless live summaries alone need more.
 // --------------------------------------------------------------------------
 class HandlePool {
  public:
@@ -140,25 +142,24 @@ class HandlePool {
     collect_ = std::move(collect);
   }
   gs_handle acquire(int kind, int device, uint64_t capacity_hint) {
-    const uint64_t slots = slots_for(capacity_hint);
-    if (gs_handle h = take(kind, device, size_class(slots), false)) return h;
+    const int cls = size_class(slots_for(capacity_hint));
+    // tables grow in place inside folds and combines, pooled or handed out: a device already
+    // past the budget finalizes the dropped summaries first even when a pooled handle would
+    // serve this request, takes any larger pooled table, and gives up pooled ones beyond it
+    const bool over = budget_ && device_bytes(device) > budget_;
+    if (over) collect();
+    if (gs_handle h = take(kind, device, cls, over)) {
+      if (over) evict_for(device, 0);
+      return h;
+    }
     uint64_t need = 0;
     gs_check(gs_create_bytes(kind, capacity_hint, &need));
     if (budget_ && device_bytes(device) + need > budget_) {
-      if (collect_) {
-        ++collections_;
-        collect_();  // the dropped summaries' destructors release into this pool
-        if (gs_handle h = take(kind, device, size_class(slots), true)) return h;
+      if (!over) {
+        collect();  // the dropped summaries' destructors release into this pool
+        if (gs_handle h = take(kind, device, cls, true)) return h;
       }
-      // still over: pooled handles (largest first) make room before a table is created
-      for (auto it = free_.rbegin(); it != free_.rend() && device_bytes(device) + need > budget_; ++it)
-        while (!it->second.empty() && device_bytes(device) + need > budget_) {
-          gs_handle f = it->second.back();
-          it->second.pop_back();
-          --nfree_;
-          live_.erase(f);
-          gs_destroy(f);
-        }
+      evict_for(device, need);  // still over: pooled handles (largest first) make room
     }
     gs_handle h = nullptr;
     gs_check(gs_create(&h, device, kind, capacity_hint));
@@ -215,6 +216,22 @@ class HandlePool {
     return nullptr;
   }
   void note(int device) { peak_total_ = std::max(peak_total_, device_bytes(device)); }
+  void collect() {
+    if (!collect_) return;
+    ++collections_;
+    collect_();
+  }
+  // destroy pooled handles, largest first, until a create of `need` bytes fits the budget
+  void evict_for(int device, uint64_t need) {
+    for (auto it = free_.rbegin(); it != free_.rend() && device_bytes(device) + need > budget_; ++it)
+      while (!it->second.empty() && device_bytes(device) + need > budget_) {
+        gs_handle f = it->second.back();
+        it->second.pop_back();
+        --nfree_;
+        live_.erase(f);
+        gs_destroy(f);
+      }
+  }
   std::map<std::tuple<int, int, int>, std::vector<gs_handle>> free_;
   std::set<gs_handle> live_;
   size_t nfree_ = 0, created_ = 0, reused_ = 0, reused_larger_ = 0, collections_ = 0;

@@ -21,7 +21,8 @@
  * (gs_hbm_bytes: tables, vertex lists, staging), so a table that grew inside a fold or
  * combine while handed out -- the Merger's running summary -- counts at once. A create of
  * gs_create_bytes(hint) is reserved under the pool's lock (concurrent task slots cannot
- * all pass the check); if it would pass gs.hbmBudgetBytes, System.gc() and
+ * all pass the check); if it would pass gs.hbmBudgetBytes -- or the device is past it already
+ * at any acquire, tables having grown in place -- System.gc() and
  * System.runFinalization() run outside the lock (the finalizers release into the pool; a
  * pass that returned nothing blocks the next for gs.gcBackoffMs), then pooled handles are
  * destroyed, largest first, to make room. Device work (gs_reset_config, gs_destroy) never
@@ -83,16 +84,28 @@ final class HandlePool {
 	 *  create would take the device's summary HBM past the budget. */
 	long acquire(long hint) {
 		final int cls = sizeClass(slotsFor(hint));
-		Long h = take(cls, false);
+		// Tables grow in place inside folds and combines, pooled or handed out: a device already
+		// past the budget finalizes the dropped summaries first even when a pooled handle would
+		// serve this request, takes any larger pooled table, and gives up pooled ones beyond it.
+		final boolean over = !reserve(0, false);
+		if (over) {
+			collect();
+		}
+		Long h = take(cls, over);
 		if (h != null) {
+			if (over) {
+				evictFor(0);
+			}
 			return h;
 		}
 		final long need = GsNative.createBytes(kind, hint);
 		if (!reserve(need, false)) {
-			collect();
-			h = take(cls, true);
-			if (h != null) {
-				return h;
+			if (!over) {
+				collect();
+				h = take(cls, true);
+				if (h != null) {
+					return h;
+				}
 			}
 			evictFor(need);
 			reserve(need, true);  // live summaries alone may need more than the budget: create anyway
