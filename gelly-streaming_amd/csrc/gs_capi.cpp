@@ -230,6 +230,7 @@ int alloc_table(gs_summary* h, uint64_t cap, bool keep_delta = false) {
   } else {
     GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
   }
+  h->export_ctr_zero = true;  // (both forms clear CTR_EXPORT)
   {
     Prof p(h, KID_INIT);
     gs::launch_init(h->tab, cap + 1, h->stream);
@@ -455,18 +456,20 @@ int join_lanes(gs_summary* h) {
 // tools/calib_launch.hip). A wait that outlasts kSpinWait (a fold queue, not a small
 // window) hands over to hipStreamSynchronize, which also surfaces asynchronous HIP
 // errors and leaves the core to other threads (N emulated ranks in one process).
-int wait_stream(gs_summary* h, const uint32_t* vals, uint64_t* value, int nvals, int stride) {
-  if (!vals && hipStreamQuery(h->stream) == hipSuccess) return GS_OK;  // already idle (0.6 us, no launch)
+int wait_stream(gs_summary* h, const uint32_t* vals, uint64_t* value, int nvals, int stride, bool clear,
+                hipStream_t st) {
+  if (!st) st = h->stream;
+  if (!vals && hipStreamQuery(st) == hipSuccess) return GS_OK;  // already idle (0.6 us, no launch)
   const unsigned long long seq = ++h->done_seq;
-  gs::launch_signal(h->done_dev, seq, vals, nvals, stride, h->stream);
+  gs::launch_signal(h->done_dev, seq, vals, nvals, stride, st, clear);
   GS_HIP(hipGetLastError());
-  if (int rc = wait_done(h, seq)) return rc;
+  if (int rc = wait_done(h, seq, st)) return rc;
   if (value) return done_value_read(h, 1, seq, value);
   return GS_OK;
 }
 
 // Spin until the completion word reaches seq (its writer is queued on h->stream).
-int wait_done(gs_summary* h, unsigned long long seq) {
+int wait_done(gs_summary* h, unsigned long long seq, hipStream_t st) {
   constexpr auto kSpinWait = std::chrono::microseconds(250);
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t i = 1;; ++i) {
@@ -474,7 +477,7 @@ int wait_done(gs_summary* h, unsigned long long seq) {
     if ((i & 255u) == 0 && std::chrono::steady_clock::now() - t0 > kSpinWait) break;
     __builtin_ia32_pause();
   }
-  GS_HIP(hipStreamSynchronize(h->stream));
+  GS_HIP(hipStreamSynchronize(st ? st : h->stream));
   if (__atomic_load_n(h->h_done, __ATOMIC_ACQUIRE) < seq) return fail(GS_ERR_HIP, "completion word not written");
   return GS_OK;
 }
@@ -628,6 +631,7 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       if (int rc = join_pipe_lanes(h)) return rc;  // (idle after a reset)
     } else if (pipe) {  // the lane waits for the caller's work on the handle stream, not for the other lane
       st = h->lane[h->lane_next];
+      h->last_lane = h->lane_next;
       h->lane_next = (h->lane_next + 1) % h->pipe_depth;
       // An idle handle stream has nothing to order behind: no marker. (With 4 hardware
       // queues a lane can share one with the handle stream, and a marker recorded there
@@ -639,6 +643,7 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       h->lanes_dirty = true;
     } else if (on_lane) {  // the caller ordered the lane (a group's own fold)
       st = h->lane[fs.lane];
+      h->last_lane = fs.lane;
       h->lanes_dirty = true;
     }
     gs::FoldLaunch f;
@@ -727,20 +732,49 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
 }
 
 // Export every (vertex, label, parity) into device arrays; returns the count.
+// After a burst of pipelined folds the label pass runs on the lane of the LAST fold queued,
+// behind events of the other lanes (and of the handle stream, if it holds work): the lanes
+// that finished earlier are passed at once, and the pass follows its lane's last fold with
+// no cross-queue wait. On the handle stream it waited for all lanes there (config 2: a
+// 13-22 us gap per step before the label pass). Its host wait observes that lane's
+// completion signal, so every stream the pass waited for is idle when it returns.
 int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n, int part,
                        int nparts) {
-  if (int rc = join_lanes(h)) return rc;
-  GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, h->stream));
+  if (int rc = server_stop(h)) return rc;
+  hipStream_t es = h->stream;
+  const bool on_lane = h->lanes_dirty && !h->side_dirty && h->last_lane >= 0 && h->lane[h->last_lane] && !h->profiling;
+  if (on_lane) {
+    es = h->lane[h->last_lane];
+    for (int i = 0; i < gs_summary::kLanes && h->lane[i]; ++i) {
+      if (i == h->last_lane) continue;
+      GS_HIP(hipEventRecord(h->lane_ev[i], h->lane[i]));
+      GS_HIP(hipStreamWaitEvent(es, h->lane_ev[i], 0));
+    }
+    if (hipStreamQuery(h->stream) != hipSuccess) {
+      GS_HIP(hipEventRecord(h->main_ev, h->stream));
+      GS_HIP(hipStreamWaitEvent(es, h->main_ev, 0));
+    }
+  } else if (int rc = join_lanes(h)) {
+    return rc;
+  }
+  if (!h->export_ctr_zero) GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, es));
+  h->export_ctr_zero = false;
   {
-    Prof pr(h, KID_EXPORT);
+    Prof pr(h, KID_EXPORT, es);
     if (nparts == 1 && use_vertex_list(h, h->nv_ub))
-      gs::launch_export_list(h->table(), v, l, p, cap, h->nv_ub, h->stream);
+      gs::launch_export_list(h->table(), v, l, p, cap, h->nv_ub, es);
     else
-      gs::launch_export(h->table(), v, l, p, cap, h->stream, part, nparts, h->vlist_ok);
+      gs::launch_export(h->table(), v, l, p, cap, es, part, nparts, h->vlist_ok);
   }
   GS_HIP(hipGetLastError());
   uint64_t cnt = 0;
-  if (int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_EXPORT), &cnt)) return rc;
+  const int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_EXPORT), &cnt, 1, 0, true, es);
+  if (rc) {
+    if (on_lane) (void)join_lanes(h);  // (the handle stream still orders behind everything)
+    return rc;
+  }
+  h->export_ctr_zero = true;  // cleared behind the read
+  if (on_lane) h->lanes_dirty = false;  // every lane and the handle stream's work completed
   *n = cnt;
   if (cnt > cap) return fail(GS_ERR_TRUNCATED, "output capacity " + std::to_string(cap) + " < " + std::to_string(cnt));
   return GS_OK;
@@ -880,7 +914,7 @@ int gs_reset(gs_handle h) {
   const bool by_list = use_vertex_list(h, h->nv_ub);
   {
     Prof p(h, KID_INIT);
-    if (by_list) {  // O(vertices): only the touched slots (no host sync)
+    if (by_list) {  // O(vertices): only the touched slots (no host sync); its last block zeroes the counters
       gs::launch_reset_list(h->table(), h->nxt, h->nv_ub, h->stream);
     } else {
       gs::launch_init(h->tab, h->cap + 1, h->stream);
@@ -888,7 +922,8 @@ int gs_reset(gs_handle h) {
   }
   GS_HIP(hipGetLastError());
   if (int rc = change_tracking_reset(h, by_list ? 0 : 1)) return rc;
-  GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
+  if (!by_list) GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
+  h->export_ctr_zero = true;
   // host mirror: a flag a fold queued before this reset raises later is an error of
   // that fold's epoch and surfaces at the next check
   memset(h->h_flags, 0, 16);
@@ -1267,7 +1302,8 @@ int gs_combine(gs_handle dst, gs_handle src) {
     bound = std::min<uint64_t>(src->nv_ub, src->cap + 1);
     if (int rc = ensure_x(src, bound + 1)) return rc;
     if (int rc = wait_x_consumer(src)) return rc;
-    GS_HIP(hipMemsetAsync(src->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, src->stream));
+    if (!src->export_ctr_zero) GS_HIP(hipMemsetAsync(src->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, src->stream));
+    src->export_ctr_zero = false;  // (the count stays behind for the copy below)
     GS_HIP(hipMemsetAsync(src->x_cnt, 0, 16, src->stream));
     {
       Prof pr(src, KID_EXPORT);

@@ -171,7 +171,9 @@ struct gs_summary {
   hipEvent_t main_ev = nullptr;
   hipEvent_t ext_ev = nullptr;  // gs_wait_stream: recorded on a producer's stream
   int lane_next = 0;
+  int last_lane = -1;  // lane of the most recently queued fold (the label pass runs there)
   bool lanes_dirty = false;
+  bool export_ctr_zero = false;  // CTR_EXPORT is zero behind the queued work (no fill before an export)
   // side stream (a multi-GPU group's apply stream): folds of remote rows run there,
   // overlapping this rank's own folds; every reader joins it (join_lanes), the
   // handle's own folds do not (union commutes)
@@ -258,15 +260,15 @@ bool side_ok(const gs_summary* h);
 int flush_reports(gs_summary* h);  // standalone capacity reports of every stream's unclaimed chunks
 int ensure_lanes(gs_summary* h, int n);  // create lane streams 0..n-1 on first use
 int read_nv(gs_summary* h, uint64_t* nv);
-// wait until every operation queued on h->stream so far has completed; *value
+// wait until every operation queued on h->stream (or `st`) so far has completed; *value
 // (optional) = the sum of nvals device u32 counters vals[i * stride], read in the same
-// round trip
+// round trip (and zeroed behind the read with `clear`)
 int wait_stream(gs_summary* h, const uint32_t* vals = nullptr, uint64_t* value = nullptr, int nvals = 1,
-                int stride = 0);
+                int stride = 0, bool clear = false, hipStream_t st = nullptr);
 int check_device_flags(gs_summary* h);
 int check_flags_now(gs_summary* h);
 int done_value_read(gs_summary* h, int i, unsigned long long seq, uint64_t* out);  // tagged completion value
-int wait_done(gs_summary* h, unsigned long long seq);  // spin on the completion word (h->stream)  // after a wait: the host-mapped flags only
+int wait_done(gs_summary* h, unsigned long long seq, hipStream_t st = nullptr);  // spin on the completion word (h->stream / st)  // after a wait: the host-mapped flags only
 int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n, int part = 0,
                        int nparts = 1);
 // stage every pending delta record into out (first cap rows, `width` int64 each) and

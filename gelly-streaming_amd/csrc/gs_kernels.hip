@@ -72,18 +72,32 @@ __device__ __forceinline__ void reset_slot(const Table& t, uint32_t* nxt, uint32
   if (nxt) nxt[s] = s;
 }
 
+// The block that finishes last (a ticket) zeroes the whole counter block: every other
+// block has read the list counts and CTR_VOVF by then, and the reset needs no fill launch
+// of its own after it (config 2: a 5 us fill + its gap per step).
 __global__ __launch_bounds__(256) void k_reset_list(Table t, uint32_t* nxt) {
   __shared__ uint32_t cnt[kShards];
   __shared__ uint64_t pre[kShards + 1];
+  __shared__ uint32_t last;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t.ctr[ctr_index(CTR_VOVF)]) {  // rare: the list is incomplete
+  if (t.ctr[ctr_index(CTR_VOVF)]) {  // rare (block-uniform): the list is incomplete
     for (uint64_t s = g0; s <= t.r0; s += stride) reset_slot(t, nxt, (uint32_t)s);
-    return;
+  } else {
+    const uint64_t total = vlist_prefix(t, cnt, pre);
+    for (uint64_t g = g0; g < total; g += stride) reset_slot(t, nxt, vlist_at(t, pre, g));
+    if (g0 == 0) reset_slot(t, nxt, t.r0);
   }
-  const uint64_t total = vlist_prefix(t, cnt, pre);
-  for (uint64_t g = g0; g < total; g += stride) reset_slot(t, nxt, vlist_at(t, pre, g));
-  if (g0 == 0) reset_slot(t, nxt, t.r0);
+  __syncthreads();  // the block's reads of the counters are done
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(&t.ctr[ctr_index(CTR_RESET_DONE)], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  uint4* c = reinterpret_cast<uint4*>(t.ctr);
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(CTR_COUNT * kCtrStride / 4); i += blockDim.x) c[i] = make_uint4(0, 0, 0, 0);
 }
 
 // k_fold: one edge per thread (edge i = block*256 + tid: coalesced 8-B loads of src
@@ -1093,8 +1107,10 @@ __global__ __launch_bounds__(64) void k_headers(const unsigned long long* __rest
 // device counters (stride apart, <= 64) handed to the host in the same round trip
 // (row counts, the sharded vertex count) instead of a copy and a second wait.
 __global__ __launch_bounds__(64) void k_signal(unsigned long long* out, unsigned long long seq, const uint32_t* vals,
-                                               int nvals, int stride) {
+                                               int nvals, int stride, int clear) {
   unsigned long long v = (vals && (int)threadIdx.x < nvals) ? vals[(size_t)threadIdx.x * stride] : 0ull;
+  if (clear && vals && (int)threadIdx.x < nvals)  // (one wave: every lane has read before any lane stores)
+    const_cast<uint32_t*>(vals)[(size_t)threadIdx.x * stride] = 0u;
   if (nvals < 0)  // one u64 word (a count word with its flag bits) instead of u32 counters
     v = (vals && threadIdx.x == 0) ? *reinterpret_cast<const unsigned long long*>(vals) : 0ull;
 #pragma unroll
@@ -1264,8 +1280,8 @@ void launch_headers(const unsigned long long* counts, int nranks, long long* out
 }
 
 void launch_signal(unsigned long long* out, unsigned long long seq, const uint32_t* vals, int nvals, int stride,
-                   hipStream_t st) {
-  hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, out, seq, vals, nvals, stride);
+                   hipStream_t st, bool clear) {
+  hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, out, seq, vals, nvals, stride, clear ? 1 : 0);
 }
 
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st) {

@@ -93,9 +93,10 @@ void launch_stage(const Table& t, const Delta& D, int64_t* out, uint64_t cap, in
 void launch_report(uint32_t* ctr, uint64_t n, unsigned long long* out, unsigned epoch, hipStream_t st);
 void launch_headers(const unsigned long long* counts, int nranks, long long* out, long long seq, hipStream_t st);
 // completion word for host waits: out[1] = sum of nvals (<= 64) counters vals[i * stride]
-// (if vals), then out[0] = seq (release, system scope)
+// (if vals), then out[0] = seq (release, system scope); `clear`: the counters are zeroed
+// behind the read (the export counter: no fill launch before the next export)
 void launch_signal(unsigned long long* out, unsigned long long seq, const uint32_t* vals, int nvals, int stride,
-                   hipStream_t st);
+                   hipStream_t st, bool clear = false);
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st);
 void launch_find_batch(const Table& t, const int64_t* v, uint64_t n, int64_t* label, uint8_t* found, uint8_t* parity,
                        hipStream_t st);
