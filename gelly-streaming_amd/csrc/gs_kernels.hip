@@ -88,14 +88,12 @@ __global__ __launch_bounds__(256) void k_reset_list(Table t, uint32_t* nxt) {
     for (uint64_t g = g0; g < total; g += stride) reset_slot(t, nxt, vlist_at(t, pre, g));
     if (g0 == 0) reset_slot(t, nxt, t.r0);
   }
-  __syncthreads();  // the block's reads of the counters are done
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(&t.ctr[ctr_index(CTR_RESET_DONE)], 1u) == gridDim.x - 1;
-  }
+  __syncthreads();  // the block's reads of the counters have returned (their values are in LDS)
+  // (no fence: the slot stores need no order against the zeroing, only the counter reads
+  // do, and every block's reads precede its ticket; the next kernel sees both)
+  if (threadIdx.x == 0) last = atomicAdd(&t.ctr[ctr_index(CTR_RESET_DONE)], 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  __threadfence();
   uint4* c = reinterpret_cast<uint4*>(t.ctr);
   for (uint32_t i = threadIdx.x; i < (uint32_t)(CTR_COUNT * kCtrStride / 4); i += blockDim.x) c[i] = make_uint4(0, 0, 0, 0);
 }

@@ -305,34 +305,26 @@ __device__ __forceinline__ uint32_t owner_hash(int64_t v, int shift) {
   return (uint32_t)(((uint64_t)v * 0x9E3779B97F4A7C15ull) >> shift);
 }
 
-// Insert-or-find of an owned vertex; its anchor word and anchor as loaded with the probe
-// (possibly stale: a published anchor never changes, so a line that shows it published
-// also holds the anchor).
-__device__ __forceinline__ uint32_t owner_insert(const OwnerTable& ot, int64_t v, uint32_t& aw, int64_t& anchor) {
+// Insert-or-find of an owned vertex. `inserted`: this row's key CAS created the slot -- its
+// row sets the anchor (no claim atomic of its own).
+__device__ __forceinline__ uint32_t owner_insert(const OwnerTable& ot, int64_t v, bool& inserted) {
+  inserted = false;
   if (v == kEmpty) {
-    atomicOr(&ot.tab[ot.r0].aw, kAncPresent);
-    aw = 0;  // (goes to the claim path)
-    anchor = 0;
+    inserted = !(atomicOr(&ot.tab[ot.r0].aw, kAncPresent) & kAncPresent);
     return ot.r0;
   }
   uint32_t h = owner_hash(v, ot.shift);
   for (uint32_t probes = 0; probes <= ot.mask; ++probes) {
-    const uint4 lo = *reinterpret_cast<const uint4*>(ot.tab + h);  // key, anchor
-    const uint4 hi = *(reinterpret_cast<const uint4*>(ot.tab + h) + 1);  // aw
-    const int64_t k = (int64_t)(((uint64_t)lo.y << 32) | lo.x);
-    if (k == v) {
-      anchor = (int64_t)(((uint64_t)lo.w << 32) | lo.z);
-      aw = hi.x;
-      return h;
-    }
+    const int64_t k = ot.tab[h].key;
+    if (k == v) return h;
     if (k == kEmpty) {
       const unsigned long long old =
           atomicCAS((unsigned long long*)&ot.tab[h].key, (unsigned long long)kEmpty, (unsigned long long)v);
-      if (old == (unsigned long long)kEmpty || (int64_t)old == v) {
-        aw = 0;
-        anchor = 0;
+      if (old == (unsigned long long)kEmpty) {
+        inserted = true;
         return h;
       }
+      if ((int64_t)old == v) return h;
     }
     h = (h + 1) & ot.mask;
   }
@@ -374,39 +366,29 @@ __global__ __launch_bounds__(kPartBS) void k_part_owner(OwnerTable ot, const int
     }
     uint32_t aw = 0, s = kNoSlot;
     int64_t anchor = 0;
-    if (valid) s = owner_insert(ot, v, aw, anchor);
+    bool claimer = false;
+    if (valid) s = owner_insert(ot, v, claimer);
     const bool live = valid && s != kNoSlot;
-    // claim: only a row that did not see the anchor published
-    const bool seen = live && (aw & kAncPublished);  // anchor from the probe's line
-    bool claimer = false, known = seen;
-    if (live && !seen) {
-      const uint32_t old = atomicOr(&ot.tab[s].aw, kAncClaimed);
-      claimer = !(old & kAncClaimed);
-      if (old & kAncPublished) {
-        aw = old;
-        anchor = __hip_atomic_load(&ot.tab[s].anchor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        known = true;
-      }
-    }
-    // publish (every claimer of the wave before any lane of it waits below)
+    // Publish without a fence (a release fence is an L2 write-back + invalidate: one per claim
+    // made this step 24 ms at one rank): the anchor goes out write-through (agent scope), its
+    // acknowledgement is awaited, then the published bit -- a memory-side atomic -- follows.
+    // A reader sees the bit at the memory side and only then reads the anchor there.
     if (claimer) {
       __hip_atomic_store(&ot.tab[s].anchor, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       atomicOr(&ot.tab[s].aw, kAncPublished | (p ? kAncParity : 0u));
     }
     bool has = false;
     int64_t A = 0;
     uint32_t w = 0;
     if (live && !claimer) {
-      if (!known) {
-        // the claimer (a resident wave past its claim) publishes without waiting
-        do {
-          __builtin_amdgcn_s_sleep(1);
-          aw = __hip_atomic_load(&ot.tab[s].aw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } while (!(aw & kAncPublished));
-        __threadfence();
-        anchor = __hip_atomic_load(&ot.tab[s].anchor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the claimer (a resident wave past its key CAS) publishes without waiting on anyone
+      aw = __hip_atomic_load(&ot.tab[s].aw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (!(aw & kAncPublished)) {
+        __builtin_amdgcn_s_sleep(1);
+        aw = __hip_atomic_load(&ot.tab[s].aw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      anchor = __hip_atomic_load(&ot.tab[s].anchor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       A = anchor;
       const uint32_t pa = (aw & kAncParity) ? 1u : 0u;
       w = SIGNED ? (p ^ pa) : 0u;
