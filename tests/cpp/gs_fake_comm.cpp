@@ -28,6 +28,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gs_group.h"
@@ -68,6 +69,7 @@ std::mutex g_mu;
 std::map<std::string, Shared*> g_reg;
 thread_local uint64_t t_order = 0x9E3779B97F4A7C15ull;  // this rank thread's order hash
 std::atomic<int> g_last_err{0};
+std::atomic<int> g_timeout_ms{20000};  // a collective's ranks must meet within this
 
 // Serialized replay (gs_fake_comm_set_serialize): a rank thread holds the GPU token
 // whenever it is outside a collective, so the ranks' work between two collectives runs
@@ -111,7 +113,7 @@ int barrier(Shared* s) {
     s->cv.notify_all();
     return 0;
   }
-  if (!s->cv.wait_for(lk, std::chrono::seconds(20), [&] { return s->gen != g0; })) {
+  if (!s->cv.wait_for(lk, std::chrono::milliseconds(g_timeout_ms.load()), [&] { return s->gen != g0; })) {
     --s->arrived;
     return kErrTimeout;
   }
@@ -325,5 +327,36 @@ void gs_fake_comm_set_serialize(int on) { g_serialize = on != 0; }
 void gs_fake_comm_token(int take) {
   if (take) token_acquire();
   else token_release();
+}
+// Self-test of the order check (tests/test_gpu_group_emulated.py): two rank threads join two
+// communicators C and D and issue one empty all-gather on each -- rank 1 in the other order
+// when `misorder`. errs[2 * r + k] = rank r's k-th collective result (misordered: each rank
+// waits on the communicator the other rank is not in, kErrTimeout after timeout_ms, or
+// kErrOrder where they meet with different histories; in order: 0).
+int gs_fake_comm_selftest(int misorder, int timeout_ms, int* errs) {
+  const int saved = g_timeout_ms.exchange(timeout_ms);
+  char idc[kIdBytes], idd[kIdBytes];
+  f_unique_id(idc);
+  f_unique_id(idd);
+  auto rank = [&](int r) {
+    void *c = nullptr, *d = nullptr;
+    if (f_init(&c, 2, idc, r) || f_init(&d, 2, idd, r)) {
+      errs[2 * r] = errs[2 * r + 1] = kErrHip;
+      return;
+    }
+    void* first = (misorder && r == 1) ? d : c;
+    void* second = first == c ? d : c;
+    errs[2 * r] = f_all_gather(nullptr, nullptr, 0, 1, first, nullptr);
+    errs[2 * r + 1] = f_all_gather(nullptr, nullptr, 0, 1, second, nullptr);
+    (void)hipStreamSynchronize(nullptr);
+    f_destroy(c);
+    f_destroy(d);
+  };
+  std::thread t0(rank, 0), t1(rank, 1);
+  t0.join();
+  t1.join();
+  g_timeout_ms = saved;
+  g_last_err = 0;
+  return 0;
 }
 }

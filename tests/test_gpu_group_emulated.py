@@ -239,3 +239,18 @@ def test_eight_ranks_many_hw_queues_subprocess():
                         "--log-batch", "17", "--passes", "2"], env=env, capture_output=True, text=True,
                        timeout=110)
     assert r.returncode == 0 and "all replicas equal the oracle" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+def test_order_check_catches_a_misordered_rank(gs):
+    """the emulation's order check itself. Two rank threads join a count
+    and a data communicator and issue one collective on each; rank 1 in the other order makes
+    every collective fail (each rank waits on the communicator the other is not in: a timeout,
+    or an order-hash mismatch where they meet with different histories) instead of hanging --
+    the condition that deadlocked an earlier build under RCCL. In order: all succeed."""
+    import ctypes
+    F = gs.fake_comm()
+    errs = (ctypes.c_int * 4)()
+    assert F.gs_fake_comm_selftest(0, 2000, errs) == 0
+    assert list(errs) == [0, 0, 0, 0]
+    assert F.gs_fake_comm_selftest(1, 500, errs) == 0
+    assert all(e in (90, 91) for e in errs), list(errs)  # kErrOrder / kErrTimeout
