@@ -339,8 +339,10 @@ int ensure_capacity(gs_summary* h, size_t n) {
   // for reports below is then only back-pressure with enough folds queued to keep the
   // GPU busy, instead of a drain before every fold (RMAT-20, config 2: 1.07 -> 0.72
   // ms/step).
-  // (x 2: a chunk's report rides on the next launch of its stream, one more chunk per lane)
-  const uint64_t slack = 2ull * n * (uint64_t)(2 * std::max({1, h->pipe_depth, h->group_lanes}) + 2);
+  // (Not x 2 for the chunk per lane whose report rides on the lane's next launch: a wait
+  // flushes those reports, and the larger table the doubled slack bought -- 2^25 instead of
+  // 2^23 slots for config 2 -- cost more in the folds than the waits: 0.556 -> 0.62 ms/step.)
+  const uint64_t slack = 2ull * n * (uint64_t)(std::max({1, h->pipe_depth, h->group_lanes}) + 1);
   const bool slack_grow = h->cap < kSlackGrowMaxCap && (double)(h->nv_exact + slack) > limit;
   if (!slack_grow) {
     // wait for reports of the folds in flight (the GPU keeps working: no drain); the

@@ -35,8 +35,7 @@ struct alignas(32) OwnerSlot {
   uint32_t pad0;
   int64_t pad1;
 };
-constexpr uint32_t kAncClaimed = 1u;    // a row of this vertex is setting the anchor
-constexpr uint32_t kAncPublished = 2u;  // anchor written (release)
+constexpr uint32_t kAncPublished = 2u;  // anchor written (the row whose key CAS inserted v sets it)
 constexpr uint32_t kAncParity = 4u;     // parity of the vertex relative to its anchor
 constexpr uint32_t kAncPresent = 8u;    // reserved slot only: INT64_MIN is an owned vertex
 

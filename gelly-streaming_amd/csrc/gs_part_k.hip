@@ -459,52 +459,86 @@ __global__ void k_part_count_word(const unsigned long long* npairs, const uint32
   *word = *npairs | (f ? kFailBit : 0ull);
 }
 
-// owned vertices -> (v, label, parity)
-__global__ __launch_bounds__(256) void k_part_labels(OwnerTable ot, Table G, int64_t* __restrict__ ov,
-                                                     int64_t* __restrict__ ol, uint8_t* __restrict__ op,
-                                                     uint64_t cap_out, unsigned long long* count) {
+// owned vertices -> (v, label, parity). Each thread reads kLabPer slots of a block tile (32-B
+// slots, coalesced), and the block reserves its tile's output with ONE atomic: one per wave
+// put 2^21 same-address atomics into the one-rank pass (11.4 ns each at the memory side:
+// 25 ms for a 2^27-slot owner table).
+constexpr int kLabPer = 8;
+constexpr uint32_t kLabBS = 256;
+__global__ __launch_bounds__(kLabBS) void k_part_labels(OwnerTable ot, Table G, int64_t* __restrict__ ov,
+                                                        int64_t* __restrict__ ol, uint8_t* __restrict__ op,
+                                                        uint64_t cap_out, unsigned long long* count) {
+  __shared__ uint32_t wsum[kLabBS / 64];
+  __shared__ unsigned long long base_sh;
   const uint64_t n = (uint64_t)ot.cap + 1;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t rounds = (n + stride - 1) / stride;
-  for (uint64_t q = 0; q < rounds; ++q) {  // wave-uniform
-    const uint64_t s = q * stride + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool has = false;
-    int64_t v = 0, L = 0;
-    uint32_t par = 0;
-    if (s < n) {
-      const OwnerSlot os = ot.tab[s];
-      const bool present = (s == ot.r0) ? ((os.aw & kAncPresent) != 0) : (os.key != kEmpty);
-      if (present) {
-        has = true;
-        v = (s == ot.r0) ? kEmpty : os.key;
-        const int64_t A = os.anchor;
-        par = (os.aw & kAncParity) ? 1u : 0u;
-        L = A;
-        uint32_t la;
-        const uint32_t sa = lookup_find(G, A, la);
-        if (sa != kNoSlot) {
-          int64_t kx = A;
-          uint32_t acc = 0;
-          find_ro(G, sa, la, kx, acc);
-          L = kx;
-          par ^= acc & 1u;
+  const int lane = (int)(threadIdx.x & 63u), wid = (int)(threadIdx.x >> 6);
+  for (uint64_t tile = (uint64_t)blockIdx.x * (kLabBS * kLabPer); tile < n;
+       tile += (uint64_t)gridDim.x * (kLabBS * kLabPer)) {  // block-uniform
+    int64_t vk[kLabPer], lk[kLabPer];
+    uint32_t pk = 0, occ = 0, cnt = 0;
+#pragma unroll
+    for (int j = 0; j < kLabPer; ++j) {  // every slot of the thread in flight together
+      const uint64_t s = tile + (uint64_t)j * kLabBS + threadIdx.x;
+      vk[j] = kEmpty;
+      lk[j] = 0;
+      uint32_t aw = 0;
+      if (s < n) {
+        const uint4 lo = *reinterpret_cast<const uint4*>(ot.tab + s);
+        aw = (reinterpret_cast<const uint4*>(ot.tab + s) + 1)->x;
+        vk[j] = (int64_t)(((uint64_t)lo.y << 32) | lo.x);
+        lk[j] = (int64_t)(((uint64_t)lo.w << 32) | lo.z);
+        const bool present = (s == ot.r0) ? ((aw & kAncPresent) != 0) : (vk[j] != kEmpty);
+        if (present) {
+          occ |= 1u << j;
+          ++cnt;
+          if (aw & kAncParity) pk |= 1u << j;
         }
       }
     }
-    const unsigned long long m = __ballot(has);
-    if (!m) continue;
-    const int lane = (int)(threadIdx.x & 63u);
-    const int leader = __ffsll((long long)m) - 1;
-    unsigned long long b = 0;
-    if (lane == leader) b = atomicAdd(count, (unsigned long long)__popcll(m));
-    b = __shfl(b, leader, 64);
-    if (!has) continue;
-    const uint64_t pos = b + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
-    if (pos < cap_out) {
-      ov[pos] = v;
-      ol[pos] = L;
-      if (op) op[pos] = (uint8_t)par;
+#pragma unroll
+    for (int j = 0; j < kLabPer; ++j) {
+      if (!((occ >> j) & 1u)) continue;
+      const int64_t A = lk[j];
+      uint32_t la;
+      const uint32_t sa = lookup_find(G, A, la);
+      if (sa != kNoSlot) {  // the anchor took part in a union: G's canonical label, parities composed
+        int64_t kx = A;
+        uint32_t acc = 0;
+        find_ro(G, sa, la, kx, acc);
+        lk[j] = kx;
+        pk ^= (acc & 1u) << j;
+      }
     }
+    // block exclusive scan of cnt: wave inclusive scan + wave totals in LDS
+    uint32_t x = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+#pragma unroll
+    for (int q = 0; q < (int)(kLabBS / 64); ++q) {
+      if (q < wid) wbase += wsum[q];
+      total += wsum[q];
+    }
+    if (threadIdx.x == 0) base_sh = total ? atomicAdd(count, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    uint64_t pos = base_sh + wbase + (x - cnt);
+#pragma unroll
+    for (int j = 0; j < kLabPer; ++j) {
+      if (!((occ >> j) & 1u)) continue;
+      if (pos < cap_out) {
+        const uint64_t s = tile + (uint64_t)j * kLabBS + threadIdx.x;
+        ov[pos] = (s == ot.r0) ? kEmpty : vk[j];
+        ol[pos] = lk[j];
+        if (op) op[pos] = (uint8_t)((pk >> j) & 1u);
+      }
+      ++pos;
+    }
+    __syncthreads();  // (wsum and base_sh are rewritten by the next tile)
   }
 }
 
@@ -574,8 +608,8 @@ void launch_part_count_word(const unsigned long long* npairs, const uint32_t* lo
 
 void launch_part_labels(const OwnerTable& ot, const Table& G, int64_t* ov, int64_t* ol, uint8_t* op, uint64_t cap_out,
                         unsigned long long* count, hipStream_t st) {
-  hipLaunchKernelGGL(k_part_labels, dim3(grid_for((uint64_t)ot.cap + 1, 256, 16384)), dim3(256), 0, st, ot, G, ov,
-                     ol, op, cap_out, count);
+  hipLaunchKernelGGL(k_part_labels, dim3(grid_for((uint64_t)ot.cap + 1, kLabBS * kLabPer, 16384)), dim3(kLabBS), 0, st,
+                     ot, G, ov, ol, op, cap_out, count);
 }
 
 }  // namespace gs

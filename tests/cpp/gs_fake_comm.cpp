@@ -220,6 +220,8 @@ int f_all_gather(const void* send, void* recv, size_t count, int dtype, void* co
                      hipSuccess)
       return kErrHip;
   }
+  // serialized replay: the collective's copies are done on every rank before any rank runs on
+  if (g_serialize && hipStreamSynchronize(st) != hipSuccess) return kErrHip;
   if (int e = finish_collective(c, st)) return g_last_err = e;
   return 0;
 }
@@ -248,6 +250,8 @@ int f_all_to_allv(const void* send, const size_t* sc, const size_t* sd, void* re
                             hipMemcpyDeviceToDevice, st) != hipSuccess)
       return kErrHip;
   }
+  // serialized replay: the collective's copies are done on every rank before any rank runs on
+  if (g_serialize && hipStreamSynchronize(st) != hipSuccess) return kErrHip;
   if (int e = finish_collective(c, st)) return g_last_err = e;
   return 0;
 }
