@@ -902,7 +902,7 @@ def main():
         pwin = (1 << args.part_window_log2) if args.part_window_log2 else 0
         xch = PartExchange(gs.PartGroup(summ, uid[0], world, rank, 1 << (args.capacity_log2 or xlog), pwin), summ,
                            pwin)
-        if args.pipeline > 1 and not pwin:
+        if args.pipeline > 1:  # (windowed: tracked folds pipeline too, the combine joins the lanes)
             summ.set_pipelining(args.pipeline)
     elif world > 1 or args.exchange:
         if args.exchange_impl == "native":

@@ -614,7 +614,8 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
   // Pipelined: plain folds (no delta tracking, no exchange layout, not profiling) may
   // overlap the previous fold. Union is associative and commutative, so the forest
   // after both is the same; readers join the lanes.
-  const bool pipe = fs.allow_pipe && h->pipe_depth > 1 && !track && fs.rows == 0 && !h->profiling && !h->changes;
+  const bool pipe = fs.allow_pipe && h->pipe_depth > 1 && (!track || fs.pipe_tracked) && fs.rows == 0 &&
+                    !h->profiling && !h->changes;
   const bool on_lane = fs.lane >= 0 && !h->profiling;
   // remote rows of a group exchange: on the side stream, overlapping own folds
   const bool side = fs.on_side && side_ok(h) && !track;

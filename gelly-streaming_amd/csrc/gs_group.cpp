@@ -966,7 +966,10 @@ int gs_group_part_fold_device(gs_group_t g, const int64_t* src, const int64_t* d
   gs_summary* h = g->h;
   DeviceGuard dg(h->device);
   FoldSource fs;
-  fs.allow_pipe = g->window == 0;  // untracked folds may pipeline (gs_set_pipelining)
+  // folds pipeline (gs_set_pipelining), tracked ones too: the combine joins the lanes before it
+  // reads the window's records
+  fs.allow_pipe = true;
+  fs.pipe_tracked = g->window != 0;
   hipEvent_t pa = ph_begin(g, h->stream);
   if (int rc = fold_device_impl(h, src, dst, nullptr, n, 1, 1, /*track=*/g->window != 0, true, fs)) return rc;
   ph_end(g, 0, pa, h->stream);

@@ -243,6 +243,9 @@ struct FoldSource {
   const uint32_t* fail_in = nullptr;           // device failure flag of a combined summary
   bool on_side = false;  // launch on h->side (a group's apply stream) instead of h->stream
   bool allow_pipe = false;
+  // a TRACKED fold may pipeline too: its caller takes the delta set only after joining the
+  // lanes (the partitioned group's windows: records go to one set through sharded atomics)
+  bool pipe_tracked = false;
   int lane = -1;         // >= 0: launch on this pipelining lane (a group's own tracked fold)
   // fused window take (gs_fold_take_device): one tracked launch that also writes the
   // rows, the count and the completion word {seq, vertices, rows}

@@ -52,9 +52,11 @@ def _merge(slices, world):
     return (v[o], lab[o], *extra)
 
 
-@pytest.mark.parametrize("world,window,hint", [(1, 0, 1 << 14), (2, 0, 1 << 8), (3, 1 << 12, 1 << 8),
-                                               (4, 1 << 11, 1 << 14), (8, 1 << 12, 1 << 8), (8, 0, 1 << 14)])
-def test_partitioned_cc_every_combine_equals_oracle(gs, oracle_mod, fake_comm, world, window, hint):
+@pytest.mark.parametrize("world,window,hint,pipe", [(1, 0, 1 << 14, 1), (2, 0, 1 << 8, 3), (3, 1 << 12, 1 << 8, 1),
+                                                    (4, 1 << 11, 1 << 14, 3), (8, 1 << 12, 1 << 8, 3),
+                                                    (8, 0, 1 << 14, 1)])
+def test_partitioned_cc_every_combine_equals_oracle(gs, oracle_mod, fake_comm, world, window, hint, pipe):
+    """(pipe 3: pipelined own folds -- tracked ones too in windowed mode -- joined by the combine)"""
     import torch
     scale, n = 14, 1 << 17
     src = torch.empty(n, dtype=torch.int64, device="cuda")
@@ -71,10 +73,13 @@ def test_partitioned_cc_every_combine_equals_oracle(gs, oracle_mod, fake_comm, w
 
     def rank(r):
         with gs.Summary("cc", capacity_hint=hint) as s:  # small hints: the local table rebuilds mid-stream
+            s.set_pipelining(pipe)
             g = gs.PartGroup(s, uid, world, r, 1 << scale, window)
             for w in range(nwin):
-                lo = r * per + w * W
-                g.fold_device(src[lo:], dst[lo:], min(W, per - w * W))
+                lo, m = r * per + w * W, min(W, per - w * W)
+                q = max(m // 4, 1)
+                for o in range(0, m, q):  # four folds per window (they overlap on the lanes with pipe 3)
+                    g.fold_device(src[lo + o:], dst[lo + o:], min(q, m - o))
                 g.combine()
                 got[(w, r)] = g.labels(1 << (scale + 1))
                 barrier.wait()
