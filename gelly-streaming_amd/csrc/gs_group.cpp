@@ -247,6 +247,8 @@ struct gs_group {
   uint64_t stage_cap = 0, send_cap = 0, recv_cap = 0, pairs_cap = 0, pairs_all_cap = 0;
   uint32_t* bcnt = nullptr;
   uint64_t bcnt_cap = 0;
+  gs::PairSlot* pset = nullptr;  // the owner step's set of label pairs emitted this combine (N > 1)
+  uint64_t pset_cap = 0;
   uint64_t cap_seen = 0;         // the local table's capacity at the previous combine (a rebuild re-exports all)
   hipEvent_t pev = nullptr;      // the combine's pair gather -> the label forest's fold
   uint64_t combines = 0, rows_exported = 0, rows_owned = 0, pairs_sent = 0, pairs_folded = 0;
@@ -828,7 +830,7 @@ int gs_group_destroy(gs_group_t g) {
   if (g->part) {
     if (g->G) (void)gs_destroy(g->G);
     for (void* q : {(void*)g->ot.tab, (void*)g->mark, (void*)g->snap, (void*)g->pflags, (void*)g->pdev, (void*)g->stage,
-                    (void*)g->sendbuf, (void*)g->recvbuf, (void*)g->pairs, (void*)g->pairs_all, (void*)g->bcnt})
+                    (void*)g->sendbuf, (void*)g->recvbuf, (void*)g->pairs, (void*)g->pairs_all, (void*)g->bcnt, (void*)g->pset})
       (void)dfree(q);
     if (g->phost) (void)hipHostFree(g->phost);
     if (g->pev) (void)hipEventDestroy(g->pev);
@@ -1051,7 +1053,18 @@ int gs_group_part_combine(gs_group_t g) {
   // 5. the owner step: anchors and label pairs
   hipEvent_t p3 = ph_begin(g, st);
   if (int rc = ensure_buf(g->pairs, g->pairs_cap, (nrec + total_recv + 1) * W, st, nrec * W)) return rc;
-  gs::launch_part_owner(sign, g->ot, g->recvbuf, total_recv, W, g->pairs, g->pdev + 3, g->pairs_cap / W,
+  // the pair set: ~1 slot per 4 received rows (2^12 .. 2^20: its probe bound lets a full set
+  // emit a repeat, never drop a pair), cleared per combine
+  gs::PairSet ps{nullptr, 0};
+  if (N > 1 && total_recv) {
+    uint64_t slots = 1ull << 12;
+    while (slots < total_recv / 4 && slots < (1ull << 20)) slots <<= 1;
+    if (int rc = ensure_buf(g->pset, g->pset_cap, slots, st)) return rc;
+    GS_HIP(hipMemsetAsync(g->pset, 0, slots * sizeof(gs::PairSlot), st));
+    ps.tab = g->pset;
+    ps.mask = (uint32_t)(slots - 1);
+  }
+  gs::launch_part_owner(sign, g->ot, ps, g->recvbuf, total_recv, W, g->pairs, g->pdev + 3, g->pairs_cap / W,
                         g->pflags + 1, st);
   GS_HIP(hipGetLastError());
   gs::launch_part_count_word(g->pdev + 3, sign ? h->ctr + gs::ctr_index(gs::CTR_FAIL) : nullptr,

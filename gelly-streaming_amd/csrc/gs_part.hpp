@@ -47,6 +47,22 @@ struct OwnerTable {
   uint32_t* err;      // device flag: probe limit hit (the table is too small)
 };
 
+// Label pairs already emitted in this combine (exact): open addressing on a 64-bit fingerprint
+// of (a, b, w); the inserting row writes the pair, then marks the slot ready; a row that meets
+// its fingerprint compares the pair itself once the slot is ready. The giant component's pairs
+// (its local roots, a few per rank) recur in every block of the owner step: without the set
+// they reached the label forest ~460 K times per rank and pass at RMAT-26, N = 8.
+struct alignas(32) PairSlot {
+  unsigned long long fp;  // 0: empty
+  int64_t a, b;
+  uint32_t state;         // bit 0 ready, bit 1 parity w
+  uint32_t pad;
+};
+struct PairSet {
+  PairSlot* tab;  // nullptr: no set (every pair is emitted)
+  uint32_t mask;
+};
+
 // owner rank of a vertex id: the same function on every rank
 __host__ __device__ __forceinline__ int part_owner(int64_t v, int nranks) {
   unsigned long long z = (unsigned long long)v ^ 0x5851F42D4C957F2Dull;
@@ -71,8 +87,9 @@ void launch_part_records(bool sign, const Table& t, const Delta& D, int64_t* pai
 void launch_part_scan(uint32_t* bcnt, uint32_t nblocks, int nranks, unsigned long long* send_counts, hipStream_t st);
 void launch_part_scatter(const int64_t* stage, uint64_t total, int width, const uint32_t* bcnt, uint32_t nblocks,
                          const unsigned long long* send_counts, int nranks, int64_t* sendbuf, hipStream_t st);
-void launch_part_owner(bool sign, const OwnerTable& ot, const int64_t* rows, uint64_t nrows, int width, int64_t* pairs,
-                       unsigned long long* npairs, uint64_t pair_cap, uint32_t* fail, hipStream_t st);
+void launch_part_owner(bool sign, const OwnerTable& ot, const PairSet& ps, const int64_t* rows, uint64_t nrows,
+                       int width, int64_t* pairs, unsigned long long* npairs, uint64_t pair_cap, uint32_t* fail,
+                       hipStream_t st);
 // the pair count word: npairs | kFailBit when the local summary, the owner step or the
 // previous combines failed (signed)
 void launch_part_count_word(const unsigned long long* npairs, const uint32_t* local_fail, const uint32_t* part_fail,

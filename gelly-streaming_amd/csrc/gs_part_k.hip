@@ -332,6 +332,66 @@ __device__ __forceinline__ uint32_t owner_insert(const OwnerTable& ot, int64_t v
   return kNoSlot;
 }
 
+// Pair-set insert, phase 1 (per lane, no waiting): the slot this pair claimed (*win) or whose
+// fingerprint it met (*win false), or kNoSlot when it met neither within the probe bound (the
+// pair is then emitted: a repeat is harmless, the label forest's fold drops it).
+__device__ __forceinline__ unsigned long long pair_fp(int64_t a, int64_t b, uint32_t w) {
+  unsigned long long z = (unsigned long long)a * 0x9E3779B97F4A7C15ull ^ ((unsigned long long)b + 0x632BE59BD9B4E019ull);
+  z ^= (unsigned long long)w << 63;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z | 1ull;  // never 0 (empty)
+}
+constexpr uint32_t kPairProbes = 32;
+__device__ __forceinline__ uint32_t pairset_probe(const PairSet& ps, unsigned long long fp, bool& win) {
+  win = false;
+  uint32_t h = (uint32_t)(fp >> 32) & ps.mask;
+  for (uint32_t k = 0; k < kPairProbes; ++k, h = (h + 1) & ps.mask) {
+    unsigned long long cur = __hip_atomic_load(&ps.tab[h].fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == 0ull) {
+      cur = atomicCAS(&ps.tab[h].fp, 0ull, fp);
+      if (cur == 0ull) {
+        win = true;
+        return h;
+      }
+    }
+    if (cur == fp) return h;
+  }
+  return kNoSlot;
+}
+// Phases 2 and 3, in this order for the whole wave (a lane that met a fingerprint waits for its
+// inserter, which is resident and publishes here without waiting on anyone): inserters publish
+// their pair (write-through, drained, then the ready bit); the others wait for ready and compare.
+// Returns whether the pair is new (to be emitted).
+__device__ __forceinline__ bool pairset_settle(const PairSet& ps, uint32_t h, bool win, bool active, int64_t a,
+                                               int64_t b, uint32_t w) {
+  if (active && h != kNoSlot && win) {
+    __hip_atomic_store(&ps.tab[h].a, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ps.tab[h].b, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    atomicOr(&ps.tab[h].state, 1u | (w << 1));
+  }
+  bool fresh = active;
+  if (active && h != kNoSlot && !win) {
+    uint32_t st = __hip_atomic_load(&ps.tab[h].state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (!(st & 1u)) {
+      __builtin_amdgcn_s_sleep(1);
+      st = __hip_atomic_load(&ps.tab[h].state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const int64_t a2 = __hip_atomic_load(&ps.tab[h].a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t b2 = __hip_atomic_load(&ps.tab[h].b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fresh = !(a2 == a && b2 == b && ((st >> 1) & 1u) == w);  // (a different pair: a fingerprint collision)
+  }
+  return fresh;
+}
+__device__ __forceinline__ bool pairset_new(const PairSet& ps, bool active, int64_t a, int64_t b, uint32_t w) {
+  if (!ps.tab) return active;
+  bool win = false;
+  const uint32_t h = active ? pairset_probe(ps, pair_fp(a, b, w), win) : kNoSlot;
+  return pairset_settle(ps, h, win, active, a, b, w);
+}
+
 // The owner step: every received row (v, l[, p]) claims or reads v's anchor; a row whose
 // label differs from the anchor (or, signed, whose parity does) becomes the label pair
 // (anchor, l, p ^ parity(anchor)). A row whose label equals the anchor with the other
@@ -343,9 +403,9 @@ __device__ __forceinline__ uint32_t owner_insert(const OwnerTable& ot, int64_t v
 // times per block: one append atomic per pair would queue on a single address).
 constexpr uint32_t kOwnerTab = 1024;
 template <bool SIGNED>
-__global__ __launch_bounds__(kPartBS) void k_part_owner(OwnerTable ot, const int64_t* __restrict__ rows, uint64_t nrows,
-                                                        int width, int64_t* pairs, unsigned long long* npairs,
-                                                        uint64_t pair_cap, uint32_t* fail) {
+__global__ __launch_bounds__(kPartBS) void k_part_owner(OwnerTable ot, PairSet ps, const int64_t* __restrict__ rows,
+                                                        uint64_t nrows, int width, int64_t* pairs,
+                                                        unsigned long long* npairs, uint64_t pair_cap, uint32_t* fail) {
   __shared__ uint32_t dflag[kOwnerTab];  // 0 empty, 1 claimed, 2 | w << 2 ready
   __shared__ int64_t da[kOwnerTab], db[kOwnerTab];
   __shared__ uint32_t lwave[kPartBS / 64];
@@ -417,13 +477,22 @@ __global__ __launch_bounds__(kPartBS) void k_part_owner(OwnerTable ot, const int
       const uint32_t g = dflag[e];
       direct = !((g >> 2) == w && da[e] == A && db[e] == l);  // another pair holds the entry
     }
-    append_pair(direct, A, l, w, pairs, width, npairs, pair_cap);
+    append_pair(pairset_new(ps, direct, A, l, w), A, l, w, pairs, width, npairs, pair_cap);
   }
   __syncthreads();
-  // the table's pairs: one reservation per block
+  // the table's pairs not emitted by another block yet (the pair set): one reservation per block
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t cnt = 0;
-  for (uint32_t q = threadIdx.x; q < kOwnerTab; q += kPartBS) cnt += (dflag[q] & 3u) == 2u;
+  uint32_t keep = 0, cnt = 0;  // bit q: entry threadIdx.x + q * kPartBS goes out
+#pragma unroll
+  for (uint32_t q = 0; q < kOwnerTab / kPartBS; ++q) {
+    const uint32_t e = threadIdx.x + q * kPartBS;
+    const uint32_t f = dflag[e];
+    const bool ready = (f & 3u) == 2u;
+    if (pairset_new(ps, ready, da[e], db[e], f >> 2)) {
+      keep |= 1u << q;
+      ++cnt;
+    }
+  }
   uint32_t x = cnt;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -440,14 +509,15 @@ __global__ __launch_bounds__(kPartBS) void k_part_owner(OwnerTable ot, const int
   if (threadIdx.x == 0) lbase = tot ? atomicAdd(npairs, (unsigned long long)tot) : 0ull;
   __syncthreads();
   uint64_t pos = lbase + wb + (x - cnt);
-  for (uint32_t q = threadIdx.x; q < kOwnerTab; q += kPartBS) {
-    const uint32_t f = dflag[q];
-    if ((f & 3u) != 2u) continue;
+#pragma unroll
+  for (uint32_t q = 0; q < kOwnerTab / kPartBS; ++q) {
+    if (!((keep >> q) & 1u)) continue;
+    const uint32_t e = threadIdx.x + q * kPartBS;
     if (pos < pair_cap) {
       int64_t* r = pairs + pos * (uint64_t)width;
-      r[0] = da[q];
-      r[1] = db[q];
-      if (width == 3) r[2] = (int64_t)(f >> 2);
+      r[0] = da[e];
+      r[1] = db[e];
+      if (width == 3) r[2] = (int64_t)(dflag[e] >> 2);
     }
     ++pos;
   }
@@ -589,15 +659,16 @@ void launch_part_scatter(const int64_t* stage, uint64_t total, int width, const 
                      send_counts, nranks, sendbuf);
 }
 
-void launch_part_owner(bool sign, const OwnerTable& ot, const int64_t* rows, uint64_t nrows, int width, int64_t* pairs,
-                       unsigned long long* npairs, uint64_t pair_cap, uint32_t* fail, hipStream_t st) {
+void launch_part_owner(bool sign, const OwnerTable& ot, const PairSet& ps, const int64_t* rows, uint64_t nrows,
+                       int width, int64_t* pairs, unsigned long long* npairs, uint64_t pair_cap, uint32_t* fail,
+                       hipStream_t st) {
   if (!nrows) return;
   const uint32_t nb = (uint32_t)((nrows + kPartRowsPB - 1) / kPartRowsPB);
   if (sign)
-    hipLaunchKernelGGL(k_part_owner<true>, dim3(nb), dim3(kPartBS), 0, st, ot, rows, nrows, width, pairs, npairs,
+    hipLaunchKernelGGL(k_part_owner<true>, dim3(nb), dim3(kPartBS), 0, st, ot, ps, rows, nrows, width, pairs, npairs,
                        pair_cap, fail);
   else
-    hipLaunchKernelGGL(k_part_owner<false>, dim3(nb), dim3(kPartBS), 0, st, ot, rows, nrows, width, pairs, npairs,
+    hipLaunchKernelGGL(k_part_owner<false>, dim3(nb), dim3(kPartBS), 0, st, ot, ps, rows, nrows, width, pairs, npairs,
                        pair_cap, fail);
 }
 

@@ -87,6 +87,7 @@ def main():
                 fold_ms = 0.0
                 lo = r * per
                 step = W or per
+                torch.cuda.synchronize()  # (device-wide: nothing of another rank's is still running)
                 for w0 in range(0, per, step):
                     t0 = time.perf_counter()
                     for o in range(w0, min(per, w0 + step), B):
