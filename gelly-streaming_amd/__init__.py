@@ -58,7 +58,7 @@ EXPORTED_SYMBOLS = (
     "gs_fold_records_counted_device", "gs_reset_config", "gs_wait_event", "gs_wait_stream", "gs_fold_device_after",
     "gs_fold_parity", "gs_set_window_server", "gs_window_server_stats", "gs_set_batch_dedup",
     "gs_digest", "gs_group_comm_ranks", "gs_group_set_phase_timing", "gs_group_phase_stats",
-    "gs_group_set_comm_api", "gs_testing_set", "gs_testing_get", "gs_hbm_bytes", "gs_create_bytes",
+    "gs_group_set_comm_api", "gs_testing_set", "gs_testing_get", "gs_testing_group_forest", "gs_hbm_bytes", "gs_create_bytes",
     "gs_group_create_partitioned", "gs_group_part_fold_device", "gs_group_part_combine",
     "gs_group_part_labels_device", "gs_group_part_status", "gs_group_part_reset", "gs_group_part_stats",
     "gs_group_part_phase_stats",
@@ -183,6 +183,7 @@ def lib():
     L.gs_testing_set.argtypes = [ctypes.c_int, _i64]
     L.gs_testing_get.argtypes = [ctypes.c_int]
     L.gs_testing_get.restype = _i64
+    L.gs_testing_group_forest.argtypes = [_vp, ctypes.POINTER(_vp)]
     _lib = L
     return L
 
@@ -794,6 +795,20 @@ class PartGroup:
 
     def set_phase_timing(self, on=True):
         _check(lib().gs_group_set_phase_timing(self._g, 1 if on else 0))
+
+    def forest_counters(self):
+        """Diagnostics of the label forest (include/gs_testing.h gs_testing_group_forest):
+        gs_counters (vertices, hooks, hook-loop iterations, failed hook CASes -- the last three
+        in the debug build) and gs_debug_counters (debug build, GS_LIB_VARIANT=debug)."""
+        f = _vp()
+        _check(lib().gs_testing_group_forest(self._g, ctypes.byref(f)))
+        a, d = (_u64 * 8)(), (_u64 * 16)()
+        _check(lib().gs_counters(f, a))
+        _check(lib().gs_debug_counters(f, d, 16))
+        out = dict(zip(("vertices", "failed", "err", "ovf", "sent", "hooks", "hook_iters", "cas_fail"), list(a)))
+        out.update(zip(("edges", "key_cas", "key_cas_lost", "ttas", "shortcut", "same_root", "find_loads", "hooks_ok",
+                        "extra_probes"), list(d)))
+        return out
 
     def phase_stats(self):
         out = (ctypes.c_double * 8)()

@@ -345,10 +345,12 @@ int ensure_capacity(gs_summary* h, size_t n) {
   const uint64_t slack = 2ull * n * (uint64_t)(std::max({1, h->pipe_depth, h->group_lanes}) + 1);
   const bool slack_grow = h->cap < kSlackGrowMaxCap && (double)(h->nv_exact + slack) > limit;
   if (!slack_grow) {
-    // wait for reports of the folds in flight (the GPU keeps working: no drain); the
-    // chunks whose report rides on a later launch are reported now
-    if (int rc = flush_reports(h)) return rc;
+    // wait for reports of the folds in flight (the GPU keeps working: no drain). The reports
+    // of queued chunks ride on the launches queued behind them and land as those start; only
+    // when nothing more can land that way are the last chunks' reports launched on their own
+    // (config 2 flushed before every wait: a standalone k_report beside most folds)
     h->cap_waits++;
+    bool flushed = false;
     const auto t0 = std::chrono::steady_clock::now();
     while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200)) {
       b = capacity_bound(h, &all);
@@ -358,7 +360,12 @@ int ensure_capacity(gs_summary* h, size_t n) {
         h->e_launched += n;
         return GS_OK;
       }
-      if (all) break;
+      if (all) {
+        if (flushed) break;
+        if (int rc = flush_reports(h)) return rc;
+        flushed = true;
+        continue;
+      }
       std::this_thread::yield();
     }
     h->cap_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -778,6 +785,10 @@ int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t
   }
   h->export_ctr_zero = true;  // cleared behind the read
   if (on_lane) h->lanes_dirty = false;  // every lane and the handle stream's work completed
+  // a whole-table export after every queued fold completed counts the vertices exactly: the
+  // capacity bound (and the next reset's choice of the listed reset over a table scan) starts
+  // from it instead of 2 per edge of the chunks whose reports ride on launches not yet made
+  if (nparts == 1) note_exact_count(h, cnt);
   *n = cnt;
   if (cnt > cap) return fail(GS_ERR_TRUNCATED, "output capacity " + std::to_string(cap) + " < " + std::to_string(cnt));
   return GS_OK;

@@ -1170,6 +1170,13 @@ int gs_group_part_stats(gs_group_t g, uint64_t* out8) {
   return GS_OK;
 }
 
+int gs_testing_group_forest(void* gv, void** forest) {
+  gs_group_t g = static_cast<gs_group_t>(gv);
+  if (!g || !forest) return fail(GS_ERR_INVALID, "null argument");
+  *forest = g->part ? g->G : nullptr;
+  return GS_OK;
+}
+
 int gs_group_part_phase_stats(gs_group_t g, double* out8) {
   if (int rc = part_of(g)) return rc;
   if (!out8) return fail(GS_ERR_INVALID, "out is null");

@@ -43,6 +43,11 @@ int gs_testing_set(int knob, int64_t value);
 /* The current value of a knob (the product value when unset). */
 int64_t gs_testing_get(int knob);
 
+/* Diagnostics: the label forest of a partitioned group (gs_group_create_partitioned), as a
+ * summary handle the caller may read (gs_counters, gs_debug_counters, gs_num_vertices) but
+ * not destroy; *forest = NULL for a replica group. `g` is a gs_group_t. */
+int gs_testing_group_forest(void* g, void** forest);
+
 #ifdef __cplusplus
 }
 #endif

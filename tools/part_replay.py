@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--window-log", type=int, default=0, help="own edges between combines (0: one per pass)")
     ap.add_argument("--micro-log", type=int, default=20)
     ap.add_argument("--link-gbs", type=float, default=64.0, help="xGMI GB/s per link and direction (model)")
+    ap.add_argument("--forest-counters", action="store_true",
+                    help="rank 0: the label forest's fold counters after the pass (debug build: GS_LIB_VARIANT=debug)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     N, scale, E = a.ranks, a.scale, 1 << a.log_edges
@@ -104,6 +106,8 @@ def main():
                 k = g.labels_device(ov, ol)
                 labels_ms = (time.perf_counter() - t0) * 1e3
                 st = g.stats()
+                if a.forest_counters and r == 0:
+                    print("label forest counters (rank 0):", g.forest_counters(), flush=True)
                 out = {"rank": r, "own_fold_ms": fold_ms, "labels_ms": labels_ms, **ph, **st, "owned": k}
                 out["digest"] = gs.digest_rows(ov[:k], ol[:k])
                 del ov, ol
