@@ -926,16 +926,19 @@ int gs_reset(gs_handle h) {
   DeviceGuard g(h->device);
   if (int rc_ = join_lanes(h)) return rc_;
   const bool by_list = use_vertex_list(h, h->nv_ub);
+  // the member lists are restored with the slots only while change tracking keeps them sized
+  // for this table (they outlive tracking and a rebuild leaves them smaller than the table)
+  const bool nxt_ok = h->changes && h->nxt && h->nxt_slots == h->cap + 1;
   {
     Prof p(h, KID_INIT);
     if (by_list) {  // O(vertices): only the touched slots (no host sync); its last block zeroes the counters
-      gs::launch_reset_list(h->table(), h->nxt, h->nv_ub, h->stream);
+      gs::launch_reset_list(h->table(), nxt_ok ? h->nxt : nullptr, h->nv_ub, h->stream);
     } else {
       gs::launch_init(h->tab, h->cap + 1, h->stream);
     }
   }
   GS_HIP(hipGetLastError());
-  if (int rc = change_tracking_reset(h, by_list ? 0 : 1)) return rc;
+  if (int rc = change_tracking_reset(h, by_list && nxt_ok ? 0 : 1)) return rc;
   if (!by_list) GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
   h->export_ctr_zero = true;
   // host mirror: a flag a fold queued before this reset raises later is an error of
