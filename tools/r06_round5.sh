@@ -8,6 +8,8 @@ R=$GRAFT_REPO_ROOT
 O=gpurun_out/$TAG
 mkdir -p $O
 export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ordering.py -m gpu -x -q --timeout 120 --timeout-method thread \
+  > $O/gpu_tests_ordering.txt 2>&1 || { echo "ordering tests failed"; tail -30 $O/gpu_tests_ordering.txt; exit 1; }
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1
 rc=$?
 grep -E "FAILED|ERROR" $O/gpu_tests.txt | head -20
@@ -25,6 +27,8 @@ timeout -k 10 300 python -u bench.py --exchange --steps 5 --warmup 2 --no-cpu-ba
   > $O/bench_exch.json 2> $O/bench_exch.err || { echo "exch rc=$?"; tail $O/bench_exch.err; exit 1; }
 timeout -k 10 300 python -u bench.py --exchange --combine partitioned --steps 5 --warmup 2 --no-cpu-baseline \
   > $O/bench_part1.json 2> $O/bench_part1.err || { echo "bench part rc=$?"; tail -20 $O/bench_part1.err; exit 1; }
+timeout -k 10 120 python -u tools/sync_check.py > $O/sync_check.txt 2>&1 || { echo "sync check rc=$?"; tail $O/sync_check.txt; exit 1; }
+cat $O/sync_check.txt
 grep -h '^{' $O/bench_r20_*.json $O/bench_bip_*.json $O/bench.json $O/bench_exch.json $O/bench_part1.json | cut -c1-170
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace -d /tmp/r20_$TAG -o run -- python3 $R/bench.py --scale 20 --steps 3 --warmup 1 \
