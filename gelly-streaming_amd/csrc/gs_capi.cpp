@@ -612,9 +612,11 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
   // stream, so a fold the caller put on a lane or the side stream (and joins there) has none
   // (ADVICE r5).
   constexpr int young_head_log2 = GS_YOUNG_HEAD_LOG2;
-  const bool young_head = young_head_log2 > 0 && check_cap && !track && fs.rows == 0 && !fs.take_out &&
-                          fs.lane < 0 && !fs.on_side && h->e_launched == 0 && h->nv_exact == 0 &&
-                          n > ((size_t)2 << young_head_log2);
+  // (Gathered rows too: a partitioned group's label forest is empty at every pass and its
+  // pairs name the giant component's few local labels over and over -- the head is then the
+  // first 2^14 rows of the flat row range, whatever rank blocks they belong to.)
+  const bool young_head = young_head_log2 > 0 && check_cap && !track && !fs.take_out && fs.lane < 0 && !fs.on_side &&
+                          h->e_launched == 0 && h->nv_exact == 0 && n > ((size_t)2 << young_head_log2);
   if (check_cap && units) {
     if (int rc = ensure_capacity(h, units)) return rc;
   }
