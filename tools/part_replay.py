@@ -5,7 +5,9 @@ N rank threads drive N local summaries through the in-process collectives emulat
 SERIALIZED mode (tests/cpp/gs_fake_comm.cpp: a rank holds the GPU token whenever it is
 outside a collective), so every rank's work between two collectives runs alone on the GPU
 and its HIP events and host clocks time its own work. Per rank and pass:
-  own folds (pipelined, untracked in bulk mode) -> combine phases (export + records,
+  own folds (pipelined, untracked in bulk mode; in bulk mode each rank's shard is also folded
+  ALONE into a fresh local forest, as a rank's own process would, and that time is the one
+  priced) -> combine phases (export + records,
   bucketing, count + row all-to-all (an HBM copy here), owner step, pair all-gather +
   label-forest fold) -> the owned label pass.
 The all-to-all is priced from its bytes at a per-link xGMI rate instead of the emulated
@@ -67,6 +69,25 @@ def main():
         ref_digest = s1.digest()
         nv_total = s1.num_vertices()
     print("T1 %.2f ms (%d vertices)" % (t1_ms, nv_total), flush=True)
+    # each rank's own folds as its own process pays them: its shard into a fresh local forest,
+    # pipelined, alone on the GPU (the threaded replay below shares one process's queues and
+    # streams between the ranks)
+    alone = []
+    for r in range(N):
+        with gs.Summary("cc", capacity_hint=V) as sr:
+            sr.set_pipelining(3)
+            for rep in range(2):
+                sr.reset()
+                sr.sync()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for o in range(r * per, (r + 1) * per, B):
+                    sr.fold_device(src[o:], dst[o:], n=min(B, (r + 1) * per - o))
+                sr.sync()
+                torch.cuda.synchronize()
+                ms = (time.perf_counter() - t0) * 1e3
+            alone.append(ms)
+    print("own folds alone per rank (ms):", " ".join("%.2f" % x for x in alone), flush=True)
 
     gs.use_comm_emulation(True)
     F = gs.fake_comm()
@@ -86,7 +107,7 @@ def main():
                 g.reset()
                 s.sync()
                 g.set_phase_timing(True)
-                fold_ms = 0.0
+                fold_ms = fold_dev_ms = 0.0
                 lo = r * per
                 step = W or per
                 torch.cuda.synchronize()  # (device-wide: nothing of another rank's is still running)
@@ -96,6 +117,8 @@ def main():
                         g.fold_device(src[lo + o:], dst[lo + o:], min(B, per - o, w0 + step - o))
                     s.sync()
                     fold_ms += (time.perf_counter() - t0) * 1e3
+                    torch.cuda.synchronize()  # (a device-wide check that Summary.sync() waited for every lane)
+                    fold_dev_ms += (time.perf_counter() - t0) * 1e3
                     g.combine()
                 ph = g.phase_stats()
                 torch.cuda.synchronize()
@@ -108,7 +131,7 @@ def main():
                 st = g.stats()
                 if a.forest_counters and r == 0:
                     print("label forest counters (rank 0):", g.forest_counters(), flush=True)
-                out = {"rank": r, "own_fold_ms": fold_ms, "labels_ms": labels_ms, **ph, **st, "owned": k}
+                out = {"rank": r, "own_fold_ms": fold_ms, "own_fold_device_sync_ms": fold_dev_ms, "labels_ms": labels_ms, **ph, **st, "owned": k}
                 out["digest"] = gs.digest_rows(ov[:k], ol[:k])
                 del ov, ol
             g.close()
@@ -144,7 +167,10 @@ def main():
         x["a2a_model_ms"] = a2a_model
         x["pair_gather_model_ms"] = gather_model
         x["combine_compute_ms"] = comp
-        x["rank_ms"] = x["own_fold_ms"] + comp + a2a_model + gather_model + x["labels_ms"]
+        x["own_fold_alone_ms"] = alone[x["rank"]]
+        # (windowed: the own folds are tracked, timed in the threaded run to a device-wide sync)
+        own = x["own_fold_alone_ms"] if W == 0 else x["own_fold_device_sync_ms"]
+        x["rank_ms"] = own + comp + a2a_model + gather_model + x["labels_ms"]
         rows.append(x)
     tmax = max(x["rank_ms"] for x in rows)
     summary = {
