@@ -176,9 +176,11 @@ def parse():
                         "environment before anything initialises HIP or RCCL, inherited by every rank; reported in "
                         "config.rccl. RCCL's collective kernels run beside the fold lanes and hold CU slots the "
                         "folds need (DESIGN.md section 5)")
-    p.add_argument("--combine", choices=["replica", "partitioned"], default="replica",
+    p.add_argument("--combine", choices=["auto", "replica", "partitioned"], default="auto",
                    help="N > 1 (or --exchange): replicated forests kept equal by delta all-gathers (DESIGN.md section 5), "
-                        "or local forests with the owner-partitioned label combine (section 5b)")
+                        "or local forests with the owner-partitioned label combine (section 5b). auto: partitioned at "
+                        "N > 1 (its per-rank replay projects above the replica's, section 5b), replica for the one-rank "
+                        "--exchange line (the replica protocol's overhead measurement)")
     p.add_argument("--part-window-log2", type=int, default=0,
                    help="partitioned combine: own edges per rank between combines (log2; 0 = one combine per pass)")
     p.add_argument("--exchange-impl", choices=["native", "torch"], default="native",
@@ -878,6 +880,8 @@ def main():
 
     E = (1 << args.scale) * args.edge_factor
     grouped = world > 1 or args.exchange
+    if args.combine == "auto":
+        args.combine = "partitioned" if world > 1 else "replica"
     part = grouped and args.combine == "partitioned"
     B = 1 << (args.exchange_log_batch if grouped and not part else args.log_batch)
     per = E // world

@@ -460,6 +460,15 @@ int join_lanes(gs_summary* h) {
   return GS_OK;
 }
 
+// Whether every operation queued on st so far (cross-stream waits included) has completed: an
+// event recorded now and queried. (hipStreamQuery reported a handle stream idle while it still
+// waited on its lanes' events -- gs_sync returned with folds running in the multi-rank replay:
+// 3.4 ms of "own folds" that a device-wide synchronisation put at 5.7-6.1 ms.)
+bool stream_idle(gs_summary* h, hipStream_t st) {
+  if (hipEventRecord(h->idle_ev, st) != hipSuccess) return false;
+  return hipEventQuery(h->idle_ev) == hipSuccess;
+}
+
 // Host wait for h->stream: k_signal queued behind everything, then a spin on its
 // host-mapped word (6.5 vs 12.2 us for hipStreamSynchronize after a short kernel,
 // tools/calib_launch.hip). A wait that outlasts kSpinWait (a fold queue, not a small
@@ -468,7 +477,7 @@ int join_lanes(gs_summary* h) {
 int wait_stream(gs_summary* h, const uint32_t* vals, uint64_t* value, int nvals, int stride, bool clear,
                 hipStream_t st) {
   if (!st) st = h->stream;
-  if (!vals && hipStreamQuery(st) == hipSuccess) return GS_OK;  // already idle (0.6 us, no launch)
+  if (!vals && stream_idle(h, st)) return GS_OK;  // already idle (no launch)
   const unsigned long long seq = ++h->done_seq;
   gs::launch_signal(h->done_dev, seq, vals, nvals, stride, st, clear);
   GS_HIP(hipGetLastError());
@@ -648,10 +657,8 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       // An idle handle stream has nothing to order behind: no marker. (With 4 hardware
       // queues a lane can share one with the handle stream, and a marker recorded there
       // waits behind that lane's fold: every fold would then wait for the previous one.)
-      if (hipStreamQuery(h->stream) != hipSuccess) {
-        GS_HIP(hipEventRecord(h->main_ev, h->stream));
-        GS_HIP(hipStreamWaitEvent(st, h->main_ev, 0));
-      }
+      GS_HIP(hipEventRecord(h->main_ev, h->stream));
+      if (hipEventQuery(h->main_ev) != hipSuccess) GS_HIP(hipStreamWaitEvent(st, h->main_ev, 0));
       h->lanes_dirty = true;
     } else if (on_lane) {  // the caller ordered the lane (a group's own fold)
       st = h->lane[fs.lane];
@@ -762,10 +769,8 @@ int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t
       GS_HIP(hipEventRecord(h->lane_ev[i], h->lane[i]));
       GS_HIP(hipStreamWaitEvent(es, h->lane_ev[i], 0));
     }
-    if (hipStreamQuery(h->stream) != hipSuccess) {
-      GS_HIP(hipEventRecord(h->main_ev, h->stream));
-      GS_HIP(hipStreamWaitEvent(es, h->main_ev, 0));
-    }
+    GS_HIP(hipEventRecord(h->main_ev, h->stream));
+    if (hipEventQuery(h->main_ev) != hipSuccess) GS_HIP(hipStreamWaitEvent(es, h->main_ev, 0));
   } else if (int rc = join_lanes(h)) {
     return rc;
   }
@@ -868,7 +873,8 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
     if (hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming) != hipSuccess)
       return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
   if (hipEventCreateWithFlags(&h->main_ev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ext_ev, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&h->ext_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->idle_ev, hipEventDisableTiming) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
   memset(h->h_flags, 0, 16);
   if (hipHostMalloc(&h->rep, gs_summary::kRepRing * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -893,6 +899,7 @@ int gs_destroy(gs_handle h) {
   }
   if (h->main_ev) (void)hipEventDestroy(h->main_ev);
   if (h->ext_ev) (void)hipEventDestroy(h->ext_ev);
+  if (h->idle_ev) (void)hipEventDestroy(h->idle_ev);
   for (int i = 0; i < gs_summary::kDedupSets; ++i) {
     (void)dfree(h->dd_tab[i]);
     (void)dfree(h->dd_w[i]);

@@ -170,6 +170,7 @@ struct gs_summary {
   hipEvent_t lane_ev[kLanes] = {};
   hipEvent_t main_ev = nullptr;
   hipEvent_t ext_ev = nullptr;  // gs_wait_stream: recorded on a producer's stream
+  hipEvent_t idle_ev = nullptr;  // stream_idle: recorded and queried
   int lane_next = 0;
   int last_lane = -1;  // lane of the most recently queued fold (the label pass runs there)
   bool lanes_dirty = false;
