@@ -107,7 +107,7 @@ def main():
                 g.reset()
                 s.sync()
                 g.set_phase_timing(True)
-                fold_ms = fold_dev_ms = 0.0
+                fold_ms = fold_dev_ms = fold_nv_ms = 0.0
                 lo = r * per
                 step = W or per
                 torch.cuda.synchronize()  # (device-wide: nothing of another rank's is still running)
@@ -117,6 +117,8 @@ def main():
                         g.fold_device(src[lo + o:], dst[lo + o:], min(B, per - o, w0 + step - o))
                     s.sync()
                     fold_ms += (time.perf_counter() - t0) * 1e3
+                    s.num_vertices()  # (a wait through a completion kernel queued behind every lane)
+                    fold_nv_ms += (time.perf_counter() - t0) * 1e3
                     torch.cuda.synchronize()  # (a device-wide check that Summary.sync() waited for every lane)
                     fold_dev_ms += (time.perf_counter() - t0) * 1e3
                     g.combine()
@@ -131,7 +133,7 @@ def main():
                 st = g.stats()
                 if a.forest_counters and r == 0:
                     print("label forest counters (rank 0):", g.forest_counters(), flush=True)
-                out = {"rank": r, "own_fold_ms": fold_ms, "own_fold_device_sync_ms": fold_dev_ms, "labels_ms": labels_ms, **ph, **st, "owned": k}
+                out = {"rank": r, "own_fold_ms": fold_ms, "own_fold_device_sync_ms": fold_dev_ms, "own_fold_nv_ms": fold_nv_ms, "labels_ms": labels_ms, **ph, **st, "owned": k}
                 out["digest"] = gs.digest_rows(ov[:k], ol[:k])
                 del ov, ol
             g.close()
