@@ -628,7 +628,7 @@ def bench_er_latency(args):
             "records_per_window_64_on": round(float(rec_of[64:].mean()), 1),
             "young_window_floor_us": round(young_floor, 2),
             "young_p50_over_floor": round(young_p50 / young_floor, 3),
-            "note": "where the slowest 1% of windows sit in the stream: the young table's windows insert most "
+            "note": "where the slowest 1%% of windows sit in the stream: the young table's windows insert most "
                     "of their endpoints (CAS + vertex-list append per new vertex); their floor = the hand-off "
                     "floor + 2 memory-side atomics per record at the calibrated %.1f G CAS/s" %
                     (ATOMIC_CAS64_PER_S / 1e9)}

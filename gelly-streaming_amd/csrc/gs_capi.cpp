@@ -138,6 +138,7 @@ int join_pipe_lanes(gs_summary* h) {
     GS_HIP(hipEventRecord(h->lane_ev[i], h->lane[i]));
     GS_HIP(hipStreamWaitEvent(h->stream, h->lane_ev[i], 0));
   }
+  h->xwait = true;
   h->lanes_dirty = false;
   return GS_OK;
 }
@@ -147,6 +148,7 @@ int join_pipe_lanes(gs_summary* h) {
 int wait_x_consumer(gs_summary* h) {
   if (!h->x_pending) return GS_OK;
   GS_HIP(hipStreamWaitEvent(h->stream, h->x_used, 0));
+  h->xwait = true;
   h->x_pending = false;
   return GS_OK;
 }
@@ -455,6 +457,7 @@ int join_lanes(gs_summary* h) {
   if (h->side_dirty) {
     GS_HIP(hipEventRecord(h->side_ev, h->side));
     GS_HIP(hipStreamWaitEvent(h->stream, h->side_ev, 0));
+    h->xwait = true;
     h->side_dirty = false;
   }
   return GS_OK;
@@ -477,11 +480,12 @@ bool stream_idle(gs_summary* h, hipStream_t st) {
 int wait_stream(gs_summary* h, const uint32_t* vals, uint64_t* value, int nvals, int stride, bool clear,
                 hipStream_t st) {
   if (!st) st = h->stream;
-  if (!vals && stream_idle(h, st)) return GS_OK;  // already idle (no launch)
+  if (!vals && !(st == h->stream && h->xwait) && stream_idle(h, st)) return GS_OK;  // already idle (no launch)
   const unsigned long long seq = ++h->done_seq;
   gs::launch_signal(h->done_dev, seq, vals, nvals, stride, st, clear);
   GS_HIP(hipGetLastError());
   if (int rc = wait_done(h, seq, st)) return rc;
+  if (st == h->stream) h->xwait = false;
   if (value) return done_value_read(h, 1, seq, value);
   return GS_OK;
 }
@@ -1124,6 +1128,11 @@ int gs_wait_event(gs_handle h, void* event) {
   DeviceGuard g(h->device);
   if (int rc = server_stop(h)) return rc;
   GS_HIP(hipStreamWaitEvent(h->stream, static_cast<hipEvent_t>(event), 0));
+  // the lanes wait for the producer themselves: a pipelined fold must not rely on a marker of
+  // the handle stream to carry this wait (see xwait)
+  for (int i = 0; i < gs_summary::kLanes && h->lane[i]; ++i)
+    GS_HIP(hipStreamWaitEvent(h->lane[i], static_cast<hipEvent_t>(event), 0));
+  h->xwait = true;
   return GS_OK;
 }
 
@@ -1135,6 +1144,8 @@ int gs_wait_stream(gs_handle h, void* stream) {
   if (int rc = server_stop(h)) return rc;
   GS_HIP(hipEventRecord(h->ext_ev, st));  // (stream 0 = the device's null stream)
   GS_HIP(hipStreamWaitEvent(h->stream, h->ext_ev, 0));
+  for (int i = 0; i < gs_summary::kLanes && h->lane[i]; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], h->ext_ev, 0));
+  h->xwait = true;
   return GS_OK;
 }
 

@@ -514,6 +514,7 @@ int gs_group_fold_device(gs_group_t g, const int64_t* src, const int64_t* dst, s
       for (int i = 0; i < kGroupLanes; ++i) GS_HIP(hipStreamWaitEvent(h->lane[i], g->staged[d], 0));
   } else if (b >= (uint64_t)gs::kDeltaSets) {
     GS_HIP(hipStreamWaitEvent(h->stream, g->staged[d], 0));
+    h->xwait = true;
   }
   h->dset = d;
   int frc = GS_OK;
@@ -1095,6 +1096,7 @@ int gs_group_part_combine(gs_group_t g) {
   ph_end(g, 5, p4, st);
   gs_summary* G = g->G;
   GS_HIP(hipStreamWaitEvent(G->stream, g->pev, 0));
+  G->xwait = true;
   hipEvent_t p5 = ph_begin(g, G->stream);
   FoldSource fs;
   fs.rows = (uint32_t)rows;
@@ -1108,6 +1110,7 @@ int gs_group_part_combine(gs_group_t g) {
   // the next combine reuses pairs_all and the words only after this fold
   GS_HIP(hipEventRecord(g->pev, G->stream));
   GS_HIP(hipStreamWaitEvent(st, g->pev, 0));
+  h->xwait = true;
   g->combines++;
   g->rows_exported += total;
   g->rows_owned += total_recv;
@@ -1127,6 +1130,7 @@ int gs_group_part_labels_device(gs_group_t g, int64_t* v, int64_t* label, uint8_
   if (int rc = join_lanes(g->G)) return rc;
   GS_HIP(hipEventRecord(g->pev, g->G->stream));
   GS_HIP(hipStreamWaitEvent(st, g->pev, 0));
+  h->xwait = true;
   GS_HIP(hipMemsetAsync(g->pdev + 5, 0, 8, st));
   gs::launch_part_labels(g->ot, g->G->table(), v, label, parity, cap, g->pdev + 5, st);
   GS_HIP(hipGetLastError());

@@ -171,6 +171,10 @@ struct gs_summary {
   hipEvent_t main_ev = nullptr;
   hipEvent_t ext_ev = nullptr;  // gs_wait_stream: recorded on a producer's stream
   hipEvent_t idle_ev = nullptr;  // stream_idle: recorded and queried
+  // h->stream holds waits on other streams' events queued since its last completion-kernel wait:
+  // only a kernel queued behind them observes them (an event recorded there completed at once
+  // in the multi-rank replay), so an idle check must not be taken then
+  bool xwait = false;
   int lane_next = 0;
   int last_lane = -1;  // lane of the most recently queued fold (the label pass runs there)
   bool lanes_dirty = false;
