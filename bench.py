@@ -1186,9 +1186,11 @@ def main():
             "data": "synthetic",
             "config": {"workload": "rmat%d-cc-stream" % args.scale, "scale": args.scale,
                        "edges": E, "micro_batch": 1 << args.log_batch if not grouped else 1 << 20,
-                       "combine_every_edges_per_gpu": 1 << args.exchange_log_batch,
-                       "combine_ramp": {"first_edges_per_gpu": 1 << args.ramp_log2 if args.ramp_log2 else 0,
-                                        "every": 1 << args.ramp_log_batch},
+                       "combine_every_edges_per_gpu": ((1 << args.part_window_log2) if args.part_window_log2 else per)
+                       if part else 1 << args.exchange_log_batch,
+                       "combine_ramp": None if part else {
+                           "first_edges_per_gpu": 1 << args.ramp_log2 if args.ramp_log2 else 0,
+                           "every": 1 << args.ramp_log_batch},
                        "combine": ("owner-partitioned label combine (native RCCL group), %s" % (
                            "every 2^%d own edges" % args.part_window_log2 if args.part_window_log2 else
                            "once per pass") if part else
