@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--window-log", type=int, default=0, help="own edges between combines (0: one per pass)")
     ap.add_argument("--micro-log", type=int, default=20)
     ap.add_argument("--link-gbs", type=float, default=64.0, help="xGMI GB/s per link and direction (model)")
+    ap.add_argument("--local-hint", type=int, default=0, help="capacity hint of each rank's local forest (0: V)")
     ap.add_argument("--forest-counters", action="store_true",
                     help="rank 0: the label forest's fold counters after the pass (debug build: GS_LIB_VARIANT=debug)")
     ap.add_argument("--out", default="")
@@ -74,7 +75,7 @@ def main():
     # streams between the ranks)
     alone = []
     for r in range(N):
-        with gs.Summary("cc", capacity_hint=V) as sr:
+        with gs.Summary("cc", capacity_hint=a.local_hint or V) as sr:
             sr.set_pipelining(3)
             for rep in range(2):
                 sr.reset()
@@ -99,7 +100,7 @@ def main():
     def rank(r):
         try:
             F.gs_fake_comm_token(1)
-            s = gs.Summary("cc", capacity_hint=V)
+            s = gs.Summary("cc", capacity_hint=a.local_hint or V)
             s.set_pipelining(3)
             g = gs.PartGroup(s, uid, N, r, V, W)
             out = {}
