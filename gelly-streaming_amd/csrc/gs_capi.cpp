@@ -652,23 +652,12 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
     if (track && !fs.take_out) h->delta_fill_ub[h->dset] += per_shard_edges(c);  // (a fused take bypasses the set)
     hipStream_t st = side ? h->side : h->stream;
     if (side) h->side_dirty = true;
-    const bool head_on_lane = head && pipe && h->gate_lane >= 0 && h->lane[h->gate_lane];
-    if (head_on_lane) {  // behind the reset on its lane; the rest of this fold follows it there
-      st = h->lane[h->gate_lane];
-      h->lane_next = h->gate_lane;
-      h->last_lane = h->gate_lane;
-      h->lanes_dirty = true;
-    } else if (head) {
+    if (head) {
       if (int rc = join_pipe_lanes(h)) return rc;  // (idle after a reset)
     } else if (pipe) {  // the lane waits for the caller's work on the handle stream, not for the other lane
-      const int li = h->lane_next;
-      st = h->lane[li];
-      h->last_lane = li;
+      st = h->lane[h->lane_next];
+      h->last_lane = h->lane_next;
       h->lane_next = (h->lane_next + 1) % h->pipe_depth;
-      if (h->gate_mask & (1u << li)) {  // behind the reset (and the young head) on the gate lane
-        GS_HIP(hipStreamWaitEvent(st, h->gate_ev, 0));
-        h->gate_mask &= ~(1u << li);
-      }
       // An idle handle stream has nothing to order behind: no marker. (With 4 hardware
       // queues a lane can share one with the handle stream, and a marker recorded there
       // waits behind that lane's fold: every fold would then wait for the previous one.)
@@ -746,11 +735,6 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
       gs::launch_fold(sign, track, h->table(), h->delta(), f, st);
     }
     GS_HIP(hipGetLastError());
-    if (head_on_lane) {  // the other lanes now wait for the head (its hubs inserted) instead
-      GS_HIP(hipEventRecord(h->gate_ev, st));
-      h->gate_mask = ((1u << h->pipe_depth) - 1u) & ~(1u << h->gate_lane);
-      h->gate_lane = -1;
-    }
     if (carry) {
       h->rep_pending_edges -= f.rep_claim;
       h->rep_pending[rs] = 0;
@@ -894,8 +878,7 @@ int gs_create(gs_handle* out, int device, int kind, uint64_t capacity_hint) {
       return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
   if (hipEventCreateWithFlags(&h->main_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ext_ev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->idle_ev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->gate_ev, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&h->idle_ev, hipEventDisableTiming) != hipSuccess)
     return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
   memset(h->h_flags, 0, 16);
   if (hipHostMalloc(&h->rep, gs_summary::kRepRing * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -921,7 +904,6 @@ int gs_destroy(gs_handle h) {
   if (h->main_ev) (void)hipEventDestroy(h->main_ev);
   if (h->ext_ev) (void)hipEventDestroy(h->ext_ev);
   if (h->idle_ev) (void)hipEventDestroy(h->idle_ev);
-  if (h->gate_ev) (void)hipEventDestroy(h->gate_ev);
   for (int i = 0; i < gs_summary::kDedupSets; ++i) {
     (void)dfree(h->dd_tab[i]);
     (void)dfree(h->dd_w[i]);
@@ -960,42 +942,17 @@ int gs_reset(gs_handle h) {
   // the member lists are restored with the slots only while change tracking keeps them sized
   // for this table (they outlive tracking and a rebuild leaves them smaller than the table)
   const bool nxt_ok = h->changes && h->nxt && h->nxt_slots == h->cap + 1;
-  // Pipelined plain folds: the reset runs on the lane of the next fold, behind every lane's and
-  // the handle stream's work, and the young head follows it there; the other lanes wait on the
-  // gate (config 2: the head on the handle stream left the GPU idle ~15 us while the lanes'
-  // waits on it resolved)
-  const bool on_lane = h->pipe_depth > 1 && !h->profiling && !h->changes && !h->side && h->group_lanes == 0 &&
-                       h->lane[h->lane_next];
-  hipStream_t rs = h->stream;
-  if (on_lane) {
-    const int rl = h->lane_next;
-    rs = h->lane[rl];
-    for (int i = 0; i < gs_summary::kLanes && h->lane[i]; ++i) {
-      if (i == rl) continue;
-      GS_HIP(hipEventRecord(h->lane_ev[i], h->lane[i]));
-      GS_HIP(hipStreamWaitEvent(rs, h->lane_ev[i], 0));
-    }
-    GS_HIP(hipEventRecord(h->main_ev, h->stream));
-    GS_HIP(hipStreamWaitEvent(rs, h->main_ev, 0));
-    h->lanes_dirty = true;
-    h->last_lane = rl;
-    h->gate_lane = rl;
-  }
   {
     Prof p(h, KID_INIT);
     if (by_list) {  // O(vertices): only the touched slots (no host sync); its last block zeroes the counters
-      gs::launch_reset_list(h->table(), nxt_ok ? h->nxt : nullptr, h->nv_ub, rs);
+      gs::launch_reset_list(h->table(), nxt_ok ? h->nxt : nullptr, h->nv_ub, h->stream);
     } else {
-      gs::launch_init(h->tab, h->cap + 1, rs);
+      gs::launch_init(h->tab, h->cap + 1, h->stream);
     }
   }
   GS_HIP(hipGetLastError());
   if (int rc = change_tracking_reset(h, by_list && nxt_ok ? 0 : 1)) return rc;
-  if (!by_list) GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, rs));
-  if (on_lane) {
-    GS_HIP(hipEventRecord(h->gate_ev, rs));
-    h->gate_mask = ((1u << h->pipe_depth) - 1u) & ~(1u << h->gate_lane);
-  }
+  if (!by_list) GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
   h->export_ctr_zero = true;
   // host mirror: a flag a fold queued before this reset raises later is an error of
   // that fold's epoch and surfaces at the next check
@@ -1871,8 +1828,6 @@ int gs_set_pipelining(gs_handle h, int depth) {
   if (int rc_ = ensure_lanes(h, depth)) return rc_;
   h->pipe_depth = depth;
   h->lane_next = 0;
-  h->gate_mask = 0;
-  h->gate_lane = -1;
   return GS_OK;
 }
 

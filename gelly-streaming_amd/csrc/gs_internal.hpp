@@ -177,12 +177,6 @@ struct gs_summary {
   bool xwait = false;
   int lane_next = 0;
   int last_lane = -1;  // lane of the most recently queued fold (the label pass runs there)
-  // The lanes' gate (pipelining): a reset runs on the next fold lane, and the young head after
-  // it on the same lane; the other lanes wait once on gate_ev, recorded there after the reset
-  // and again after the head (no cross-queue wait on the handle stream between them)
-  hipEvent_t gate_ev = nullptr;
-  unsigned gate_mask = 0;  // lanes that still wait on gate_ev before their next fold
-  int gate_lane = -1;      // the lane of the last reset (its young head goes there too)
   bool lanes_dirty = false;
   bool export_ctr_zero = false;  // CTR_EXPORT is zero behind the queued work (no fill before an export)
   // side stream (a multi-GPU group's apply stream): folds of remote rows run there,
