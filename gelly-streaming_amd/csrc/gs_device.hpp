@@ -89,9 +89,6 @@ enum CounterBlock : int {
   CTR_TAKE_SHARD,                // [kTicketShards] block tickets, first level (block b -> shard b mod 16)
   CTR_SRV_NV = CTR_TAKE_SHARD + 16,  // resident window server: vertices after its last window (u64)
   CTR_SRV_NV_HI,
-  CTR_RESET_DONE,                // k_reset_list block ticket, top level (its last block zeroes the counters)
-  CTR_RESET_SHARD,               // [kTicketShards] its first level (block b -> shard b mod 16)
-  CTR_RESET_SHARD_END_ = CTR_RESET_SHARD + 16,
   // debug build only (-DGS_DEBUG_COUNTERS, gs_debug_counters): where a fold's memory operations go
   CTR_DBG_EDGES,                 // valid edges / rows folded
   CTR_DBG_KCAS,                  // key CASes issued (inserts)

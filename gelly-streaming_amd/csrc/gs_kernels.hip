@@ -92,17 +92,19 @@ __global__ __launch_bounds__(256) void k_reset_list(Table t, uint32_t* nxt) {
   // (no fence: the slot stores need no order against the zeroing, only the counter reads
   // do, and every block's reads precede its ticket; the next kernel sees both). Two-level
   // ticket: same-address atomics serialise at the memory side (11.4 ns each), and one counter
-  // for config 2's 2.5 K blocks cost the reset ~29 us.
+  // for config 2's 2.5 K blocks cost the reset ~29 us. The window take's ticket counters serve
+  // (zero at rest: a take leaves them zeroed, no take runs beside a reset, and this kernel's
+  // last block zeroes them again).
   if (threadIdx.x == 0) {
     constexpr uint32_t kTS = 16;
     bool l = true;
     if (gridDim.x > kTS) {
       const uint32_t shard = blockIdx.x % kTS;
       const uint32_t in_shard = (gridDim.x - shard + kTS - 1) / kTS;
-      l = atomicAdd(&t.ctr[ctr_index(CTR_RESET_SHARD + (int)shard)], 1u) == in_shard - 1;
-      if (l) l = atomicAdd(&t.ctr[ctr_index(CTR_RESET_DONE)], 1u) == kTS - 1;
+      l = atomicAdd(&t.ctr[ctr_index(CTR_TAKE_SHARD + (int)shard)], 1u) == in_shard - 1;
+      if (l) l = atomicAdd(&t.ctr[ctr_index(CTR_TAKE_DONE)], 1u) == kTS - 1;
     } else {
-      l = atomicAdd(&t.ctr[ctr_index(CTR_RESET_DONE)], 1u) == gridDim.x - 1;
+      l = atomicAdd(&t.ctr[ctr_index(CTR_TAKE_DONE)], 1u) == gridDim.x - 1;
     }
     last = l;
   }
