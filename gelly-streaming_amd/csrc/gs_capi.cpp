@@ -761,23 +761,31 @@ int fold_device_impl(gs_summary* h, const int64_t* src, const int64_t* dst, cons
 // no cross-queue wait. On the handle stream it waited for all lanes there (config 2: a
 // 13-22 us gap per step before the label pass). Its host wait observes that lane's
 // completion signal, so every stream the pass waited for is idle when it returns.
+// A reader that ends in a host wait, after a burst of pipelined folds: it runs on the lane of
+// the last fold queued, behind events of the other lanes and of the handle stream (*es; *on_lane
+// true), else on the handle stream after join_lanes. The host wait then observes that lane's
+// completion, so every stream it waited for is idle when it returns (clear lanes_dirty then).
+int join_into_last_lane(gs_summary* h, hipStream_t* es, bool* on_lane) {
+  if (int rc = server_stop(h)) return rc;
+  *es = h->stream;
+  *on_lane = h->lanes_dirty && !h->side_dirty && h->last_lane >= 0 && h->lane[h->last_lane] && !h->profiling;
+  if (!*on_lane) return join_lanes(h);
+  *es = h->lane[h->last_lane];
+  for (int i = 0; i < gs_summary::kLanes && h->lane[i]; ++i) {
+    if (i == h->last_lane) continue;
+    GS_HIP(hipEventRecord(h->lane_ev[i], h->lane[i]));
+    GS_HIP(hipStreamWaitEvent(*es, h->lane_ev[i], 0));
+  }
+  GS_HIP(hipEventRecord(h->main_ev, h->stream));
+  if (h->xwait || hipEventQuery(h->main_ev) != hipSuccess) GS_HIP(hipStreamWaitEvent(*es, h->main_ev, 0));
+  return GS_OK;
+}
+
 int export_device_impl(gs_summary* h, int64_t* v, int64_t* l, uint8_t* p, size_t cap, size_t* n, int part,
                        int nparts) {
-  if (int rc = server_stop(h)) return rc;
   hipStream_t es = h->stream;
-  const bool on_lane = h->lanes_dirty && !h->side_dirty && h->last_lane >= 0 && h->lane[h->last_lane] && !h->profiling;
-  if (on_lane) {
-    es = h->lane[h->last_lane];
-    for (int i = 0; i < gs_summary::kLanes && h->lane[i]; ++i) {
-      if (i == h->last_lane) continue;
-      GS_HIP(hipEventRecord(h->lane_ev[i], h->lane[i]));
-      GS_HIP(hipStreamWaitEvent(es, h->lane_ev[i], 0));
-    }
-    GS_HIP(hipEventRecord(h->main_ev, h->stream));
-    if (hipEventQuery(h->main_ev) != hipSuccess) GS_HIP(hipStreamWaitEvent(es, h->main_ev, 0));
-  } else if (int rc = join_lanes(h)) {
-    return rc;
-  }
+  bool on_lane = false;
+  if (int rc = join_into_last_lane(h, &es, &on_lane)) return rc;
   if (!h->export_ctr_zero) GS_HIP(hipMemsetAsync(h->ctr + gs::ctr_index(gs::CTR_EXPORT), 0, 4, es));
   h->export_ctr_zero = false;
   {
@@ -947,12 +955,11 @@ int gs_reset(gs_handle h) {
     if (by_list) {  // O(vertices): only the touched slots (no host sync); its last block zeroes the counters
       gs::launch_reset_list(h->table(), nxt_ok ? h->nxt : nullptr, h->nv_ub, h->stream);
     } else {
-      gs::launch_init(h->tab, h->cap + 1, h->stream);
+      gs::launch_init(h->tab, h->cap + 1, h->stream, h->ctr);  // (its block 0 zeroes the counters)
     }
   }
   GS_HIP(hipGetLastError());
   if (int rc = change_tracking_reset(h, by_list && nxt_ok ? 0 : 1)) return rc;
-  if (!by_list) GS_HIP(hipMemsetAsync(h->ctr, 0, gs::CTR_COUNT * gs::kCtrStride * 4, h->stream));
   h->export_ctr_zero = true;
   // host mirror: a flag a fold queued before this reset raises later is an error of
   // that fold's epoch and surfaces at the next check
@@ -1294,11 +1301,19 @@ int gs_bip_status(gs_handle h, int* ok) {
   if (int rc = check(h)) return rc;
   if (!ok) return fail(GS_ERR_INVALID, "ok is null");
   DeviceGuard g(h->device);
-  if (int rc_ = join_lanes(h)) return rc_;
   // the verdict handed to the host with the completion word (k_signal): no device-to-host
-  // copy and no hipStreamSynchronize wake-up (config 4 reads it at the end of every step)
+  // copy and no hipStreamSynchronize wake-up (config 4 reads it at the end of every step), on
+  // the last fold's lane (no cross-queue join before it: 14-22 us of config 4's step)
+  hipStream_t es = h->stream;
+  bool on_lane = false;
+  if (int rc = join_into_last_lane(h, &es, &on_lane)) return rc;
   uint64_t f = 0;
-  if (int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_FAIL), &f, 1, 0)) return rc;
+  const int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_FAIL), &f, 1, 0, false, es);
+  if (rc) {
+    if (on_lane) (void)join_lanes(h);
+    return rc;
+  }
+  if (on_lane) h->lanes_dirty = false;  // every lane and the handle stream's work completed
   *ok = f ? 0 : 1;
   return GS_OK;
 }

@@ -18,8 +18,13 @@
 
 namespace gs {
 
-// slot s := {EMPTY, s << 1, 0} (the reserved slot's key field IS its id, INT64_MIN)
-__global__ __launch_bounds__(256) void k_init(Slot* tab, uint64_t nslots) {
+// slot s := {EMPTY, s << 1, 0} (the reserved slot's key field IS its id, INT64_MIN).
+// ctr (optional): block 0 also zeroes the counters -- the first 16 B of every counter line
+// (nothing reads them during a reset: no fill launch of its own).
+__global__ __launch_bounds__(256) void k_init(Slot* tab, uint64_t nslots, uint32_t* ctr) {
+  if (ctr && blockIdx.x == 0)
+    for (uint32_t i = threadIdx.x; i < (uint32_t)CTR_COUNT; i += blockDim.x)
+      *reinterpret_cast<uint4*>(ctr + ctr_index((int)i)) = make_uint4(0, 0, 0, 0);
   for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
        s += (uint64_t)gridDim.x * blockDim.x) {
     uint4 v;
@@ -1201,11 +1206,14 @@ extern "C" int gs_debug_server_trace(void* buf, unsigned long long cap) {  // di
 }
 namespace gs {
 #endif
-void launch_init(Slot* tab, uint64_t nslots, hipStream_t st) {
-  // one slot per thread: 2 GiB in 0.30 ms vs 0.48 ms with 8192 grid-strided blocks
+void launch_init(Slot* tab, uint64_t nslots, hipStream_t st, uint32_t* ctr) {
+  // one slot per thread for large tables: 2 GiB in 0.30 ms vs 0.48 ms with 8192 grid-strided
+  // blocks; at most 16 slots per thread below 2^26 slots, where the dispatch of one block per
+  // 256 slots dominated (config 4's 2^22-slot reset: 41 us for 67 MB)
   const uint64_t blocks = (nslots + 255) / 256;
-  const unsigned g = (unsigned)(blocks < (1u << 22) ? blocks : (1u << 22));
-  hipLaunchKernelGGL(k_init, dim3(g), dim3(256), 0, st, tab, nslots);
+  const uint64_t want = nslots < (1ull << 26) ? (blocks + 15) / 16 : blocks;
+  const unsigned g = (unsigned)(want < 1 ? 1 : (want < (1u << 22) ? want : (1u << 22)));
+  hipLaunchKernelGGL(k_init, dim3(g), dim3(256), 0, st, tab, nslots, ctr);
 }
 
 static unsigned list_grid(uint64_t bound) {

@@ -74,7 +74,7 @@ void launch_window_server(bool sign, const Table& t, const Delta& D, ServerBox* 
 // CUs): a window completes only when all kServerBlocks of them run together.
 int window_server_resident_blocks(bool sign, int device);
 
-void launch_init(Slot* tab, uint64_t nslots, hipStream_t st);
+void launch_init(Slot* tab, uint64_t nslots, hipStream_t st, uint32_t* ctr = nullptr);
 // micro-batch dedup: w[i] = 1 (keep) or 0x81 (skip: a repeat of an earlier pair of the batch)
 void launch_dedup(const int64_t* src, const int64_t* dst, uint32_t n, unsigned long long* tab, uint32_t mask,
                   uint8_t* w, hipStream_t st);
