@@ -478,11 +478,11 @@ bool stream_idle(gs_summary* h, hipStream_t st) {
 // window) hands over to hipStreamSynchronize, which also surfaces asynchronous HIP
 // errors and leaves the core to other threads (N emulated ranks in one process).
 int wait_stream(gs_summary* h, const uint32_t* vals, uint64_t* value, int nvals, int stride, bool clear,
-                hipStream_t st) {
+                hipStream_t st, const uint32_t* flag) {
   if (!st) st = h->stream;
   if (!vals && !(st == h->stream && h->xwait) && stream_idle(h, st)) return GS_OK;  // already idle (no launch)
   const unsigned long long seq = ++h->done_seq;
-  gs::launch_signal(h->done_dev, seq, vals, nvals, stride, st, clear);
+  gs::launch_signal(h->done_dev, seq, vals, nvals, stride, st, clear, flag);
   GS_HIP(hipGetLastError());
   if (int rc = wait_done(h, seq, st)) return rc;
   if (st == h->stream) h->xwait = false;
@@ -1307,14 +1307,19 @@ int gs_bip_status(gs_handle h, int* ok) {
   hipStream_t es = h->stream;
   bool on_lane = false;
   if (int rc = join_into_last_lane(h, &es, &on_lane)) return rc;
-  uint64_t f = 0;
-  const int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_FAIL), &f, 1, 0, false, es);
+  // With it, the exact vertex count (every queued fold has completed when the host sees the
+  // word): the next reset walks the vertex list instead of scanning a slack-sized table
+  // (config 4: 2^24 slots, 42 us, for 2^20 vertices)
+  uint64_t w = 0;
+  const int rc = wait_stream(h, h->ctr + gs::ctr_index(gs::CTR_NV), &w, gs::kShards, gs::kCtrStride, false, es,
+                             h->ctr + gs::ctr_index(gs::CTR_FAIL));
   if (rc) {
     if (on_lane) (void)join_lanes(h);
     return rc;
   }
   if (on_lane) h->lanes_dirty = false;  // every lane and the handle stream's work completed
-  *ok = f ? 0 : 1;
+  if (!h->side_dirty && !h->lanes_dirty) note_exact_count(h, w & (gs::kSignalFlagBit - 1));
+  *ok = (w & gs::kSignalFlagBit) ? 0 : 1;
   return GS_OK;
 }
 

@@ -272,7 +272,7 @@ int read_nv(gs_summary* h, uint64_t* nv);
 // (optional) = the sum of nvals device u32 counters vals[i * stride], read in the same
 // round trip (and zeroed behind the read with `clear`)
 int wait_stream(gs_summary* h, const uint32_t* vals = nullptr, uint64_t* value = nullptr, int nvals = 1,
-                int stride = 0, bool clear = false, hipStream_t st = nullptr);
+                int stride = 0, bool clear = false, hipStream_t st = nullptr, const uint32_t* flag = nullptr);
 int check_device_flags(gs_summary* h);
 int check_flags_now(gs_summary* h);
 int done_value_read(gs_summary* h, int i, unsigned long long seq, uint64_t* out);  // tagged completion value

@@ -1128,7 +1128,7 @@ __global__ __launch_bounds__(64) void k_headers(const unsigned long long* __rest
 // device counters (stride apart, <= 64) handed to the host in the same round trip
 // (row counts, the sharded vertex count) instead of a copy and a second wait.
 __global__ __launch_bounds__(64) void k_signal(unsigned long long* out, unsigned long long seq, const uint32_t* vals,
-                                               int nvals, int stride, int clear) {
+                                               int nvals, int stride, int clear, const uint32_t* flag) {
   unsigned long long v = (vals && (int)threadIdx.x < nvals) ? vals[(size_t)threadIdx.x * stride] : 0ull;
   if (clear && vals && (int)threadIdx.x < nvals)  // (one wave: every lane has read before any lane stores)
     const_cast<uint32_t*>(vals)[(size_t)threadIdx.x * stride] = 0u;
@@ -1137,6 +1137,7 @@ __global__ __launch_bounds__(64) void k_signal(unsigned long long* out, unsigned
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   if (threadIdx.x != 0) return;
+  if (flag && *flag) v |= kSignalFlagBit;  // (a second value in the same round trip: the verdict)
   // (a system release: the host may read what earlier work of the stream wrote to host
   // memory once it sees the word; the value is tagged as take_tail's)
   if (vals) __hip_atomic_store(out + 1, done_value(seq, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1304,8 +1305,8 @@ void launch_headers(const unsigned long long* counts, int nranks, long long* out
 }
 
 void launch_signal(unsigned long long* out, unsigned long long seq, const uint32_t* vals, int nvals, int stride,
-                   hipStream_t st, bool clear) {
-  hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, out, seq, vals, nvals, stride, clear ? 1 : 0);
+                   hipStream_t st, bool clear, const uint32_t* flag) {
+  hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, out, seq, vals, nvals, stride, clear ? 1 : 0, flag);
 }
 
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st) {
