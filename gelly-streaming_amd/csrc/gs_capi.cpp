@@ -1318,7 +1318,7 @@ int gs_bip_status(gs_handle h, int* ok) {
     return rc;
   }
   if (on_lane) h->lanes_dirty = false;  // every lane and the handle stream's work completed
-  if (!h->side_dirty && !h->lanes_dirty) note_exact_count(h, w & (gs::kSignalFlagBit - 1));
+  if (!h->side_dirty && !h->lanes_dirty) note_exact_count(h, w & ((1ull << 47) - 1));
   *ok = (w & gs::kSignalFlagBit) ? 0 : 1;
   return GS_OK;
 }

@@ -95,8 +95,9 @@ void launch_headers(const unsigned long long* counts, int nranks, long long* out
 // completion word for host waits: out[1] = sum of nvals (<= 64) counters vals[i * stride]
 // (if vals), then out[0] = seq (release, system scope); `clear`: the counters are zeroed
 // behind the read (the export counter: no fill launch before the next export)
-// `flag` (optional): bit 47 of the value is set when *flag != 0 (the sum stays below 2^47)
-constexpr unsigned long long kSignalFlagBit = 1ull << 47;
+// `flag` (optional): bit 62 of the value is set when *flag != 0 (a count word's failed-verdict
+// bit: the completion record carries it as bit 47, the sum stays below 2^47)
+constexpr unsigned long long kSignalFlagBit = 1ull << 62;
 void launch_signal(unsigned long long* out, unsigned long long seq, const uint32_t* vals, int nvals, int stride,
                    hipStream_t st, bool clear = false, const uint32_t* flag = nullptr);
 void launch_find_one(const Table& t, int64_t key, int64_t* out, hipStream_t st);
